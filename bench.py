@@ -1,0 +1,274 @@
+"""bench.py — device-resident Internet-checksum throughput on MI355X.
+
+Workload (BASELINE.json configs[1], the metric's config): per GPU, a batch of
+1,048,576 IPv4/UDP frames of 1500 B packed back to back in HBM behind an
+offset/length array.  One step = the checksum work the native stack does on
+that traffic when offload is off, both directions:
+  generate: sccsum_ipv4_frames over the tx batch (checksum fields zero) ->
+            IPv4 header + UDP checksums       (src/net/ip.cc:271-277, udp.cc:184-195)
+  verify:   sccsum_ipv4_frames over the rx batch (checksums stored, 1 % of
+            frames corrupted) -> per-frame pass/fail status (ip.cc:121-127, tcp.hh:876-883)
+value = bytes checksummed by all ranks / max-over-ranks wall time, GiB/s.
+Multi-GPU: one process per GPU, each with its own independent shard (weak
+scaling, no data-path collective; the only collectives are the timing
+barrier and the max-over-ranks reduction).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from seastar_amd import batch, devsynth, native  # noqa: E402
+
+METRIC = "GiB/s device-resident Internet checksum, 1500B-packet batches, 1/2/4/8 GPUs"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+FRAME = 1500
+META_BYTES = 12  # u64 offset + u32 length per packet
+SEED = 0x5EA57A2C
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--packets", type=int, default=1 << 20, help="frames per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (rank 0, N=1)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc", default=None, help="PMC summary JSON for roofline.traffic (default: newest in profiles/)")
+    return ap.parse_args()
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    native.check(native.load().sccsum_init(local), "sccsum_init")
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(tx, budget_s: float):
+    """Oracle (C restatement of src/net/ip_checksum.cc, -O2) on a bounded
+    sample of the same frames, on this host's cores: threads = cores we may
+    use (capped at 16, the box's CPU share), plus the 1-thread rate."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # cpu_baseline leg only
+
+    n_sample = min(65536, tx.n)
+    host = tx.data[: n_sample * FRAME].cpu().numpy()
+    off = np.arange(n_sample, dtype=np.uint64) * FRAME
+    length = np.full(n_sample, FRAME, dtype=np.uint32)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+
+    def rate(nt, seconds):
+        oracle.batch_ipv4(host, off, length, nthreads=nt)  # warm
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            oracle.batch_ipv4(host, off, length, nthreads=nt)
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= seconds:
+                break
+        # generate + verify = the same checksum work twice per frame on the GPU
+        # side; the CPU rate is bytes checksummed per second either way.
+        return reps * n_sample * FRAME / dt / 2**30, reps
+
+    v1, r1 = rate(1, budget_s / 2)
+    vn, rn = rate(threads, budget_s / 2)
+    return {
+        "value": round(vn, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n_sample} x {FRAME} B IPv4/UDP frames ({n_sample * FRAME / 1e6:.0f} MB) from the same batch, "
+                  f"IPv4 header + UDP checksum per frame, {rn} passes on {threads} threads "
+                  f"(~{budget_s / 2:.0f} s) and {r1} passes on 1 thread",
+        "value_1core": round(v1, 3),
+        "cpu_model": cpu_model(),
+    }
+
+
+def pmc_traffic(path: str | None, kernel_substr: str):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (see
+    tools/pmc_summary.py); None when no summary exists."""
+    cands = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))
+    for p in reversed(cands):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(kernel_substr)
+        if k and k.get("hbm_bytes_per_launch"):
+            return float(k["hbm_bytes_per_launch"]), os.path.relpath(p, REPO)
+    return None, None
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup()
+    dev = torch.device("cuda", local)
+    n = args.packets
+
+    tx = devsynth.udp_frames(n, FRAME, seed=SEED + 7919 * rank, device=dev)
+    out_tx = torch.empty(2 * n, dtype=torch.int16, device=dev)
+    first = batch.ipv4_frames(tx, out2=out_tx)
+    rx = devsynth.store_checksums(tx, first)
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED + rank)
+    bad = torch.randperm(n, device=dev, generator=g)[: n // 100]
+    devsynth.corrupt(rx, bad, byte=700)
+    out_rx = torch.empty(2 * n, dtype=torch.int16, device=dev)
+    st_rx = torch.empty(n, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        batch.ipv4_frames(tx, out2=out_tx, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        batch.ipv4_frames(rx, out2=out_rx, status=st_rx, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # sanity: every uncorrupted rx frame verifies, every corrupted one fails
+    n_fail = int(((st_rx & 2) == 0).sum())
+    assert n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = time.perf_counter() - t0
+    wall_max = max_over_ranks(wall, world)
+
+    launch_ms = []
+    for e in evs:
+        launch_ms.append(e[0].elapsed_time(e[1]))
+        launch_ms.append(e[1].elapsed_time(e[2]))
+    avg_launch_s = float(np.mean(launch_ms)) / 1e3
+
+    bytes_per_step = 2 * n * FRAME  # per rank
+    value = world * bytes_per_step * args.steps / wall_max / 2**30
+    alg_bytes_launch = n * (FRAME + META_BYTES + 4) + n // 2  # + status byte on the rx launch (avg)
+    achieved = alg_bytes_launch / avg_launch_s / 1e9
+
+    # measured HBM read ceiling with the same load shape over the tx bytes
+    sink = torch.zeros(native.load().sccsum_read_probe_blocks(), dtype=torch.int64, device=dev)
+    for _ in range(3):
+        batch.read_probe(tx.data, tx.bytes_len, sink=sink, stream=stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    reps = 10
+    for _ in range(reps):
+        batch.read_probe(tx.data, tx.bytes_len, sink=sink, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ceiling = (tx.bytes_len & ~15) * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+
+    traffic, traffic_src = pmc_traffic(args.pmc, "csum_kernel")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(tx, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": "cfg2: 1,048,576 x 1500 B IPv4/UDP frames per GPU in HBM (offset/length array); "
+                            "step = generate (IP+UDP csum) + verify (1% corrupted) pass",
+                "packets_per_gpu": n,
+                "frame_bytes": FRAME,
+                "global_batch": n * world,
+                "parallelism": f"{world} independent shards, no collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "csum_kernel<2,true> (sccsum_ipv4_frames)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "alg_bytes_per_launch": alg_bytes_launch,
+                "avg_launch_us": round(avg_launch_s * 1e6, 2),
+                "measured_read_ceiling_GBps": round(ceiling, 1),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,126 @@
+/*
+ * sccsum.h — C-ABI boundary of the MI355X (gfx950) batch Internet-checksum
+ * engine.  Plain pointers and sizes only; every entry point returns 0 on
+ * success, a positive hipError_t value for a HIP runtime failure, or a
+ * negative SCCSUM_E* code; nothing throws.
+ *
+ * What each entry replaces in scylladb/seastar (paths relative to the
+ * reference tree):
+ *
+ *   sccsum_spans        N x { checksummer c; [pseudo-header seed];
+ *                             c.sum(data, len); c.get(); }
+ *                       = ip_checksum(const void*, size_t)  src/net/ip_checksum.cc:70-74
+ *                         checksummer::sum(const char*, size_t)  src/net/ip_checksum.cc:31-53
+ *                         checksummer::get() const  src/net/ip_checksum.cc:55-62
+ *                       as used by UDP generate  src/net/udp.cc:184-195,
+ *                       TCP generate  include/seastar/net/tcp.hh:1656-1694, 1004-1016,
+ *                       ICMP echo  src/net/ip.cc:471-474, demos/echo_demo.cc:76-78
+ *   sccsum_ipv4_frames  N x { IPv4 header verify/generate over sizeof(ip_hdr)=20 B
+ *                             src/net/ip.cc:121-127, 271-277;
+ *                             length checks / trim / strip 4*ihl  src/net/ip.cc:128-140, 220-225;
+ *                             L4 pseudo-header + segment  include/seastar/net/tcp.hh:876-883 }
+ *   sccsum_pseudo_seed  ipv4_traits::{tcp,udp}_pseudo_header_checksum
+ *                       include/seastar/net/ip.hh:70-75 (host arithmetic, O(1))
+ *
+ * Result convention (same as the reference): each 16-bit checksum is returned
+ * with its bytes already in network order, i.e. storing the uint16_t to the
+ * packet's checksum field writes the wire bytes (ip_checksum.cc:61,
+ * tcp.hh:283-285).  A verify passes when the recomputed value is 0.
+ *
+ * Memory contract:
+ *   - d_bytes, d_off, d_len, d_seed, d_out*, d_status are DEVICE pointers
+ *     (hipMalloc / torch CUDA tensors) on the calling thread's current device.
+ *   - bytes_len is the number of valid bytes at d_bytes.  The kernels read in
+ *     aligned 16-byte units, so the allocation must be readable up to
+ *     roundup(bytes_len, 16) (hipMalloc allocations always are).
+ *   - A packet whose [off, off+len) is not inside [0, bytes_len) is not read:
+ *     its outputs are 0 and its status has SCCSUM_ST_RANGE.
+ *   - d_off must be 8-byte aligned, d_len/d_seed/d_out2 4-byte aligned,
+ *     d_out 2-byte aligned.
+ *   - Launches are asynchronous on `stream` (a hipStream_t; NULL = the
+ *     device's null stream).  No allocation, no host synchronisation: the
+ *     calls are safe inside hipStreamBeginCapture.
+ *
+ * Threading: one host thread per device (Seastar's shard-per-core model).
+ * Calls are re-entrant per stream.
+ */
+#ifndef SCCSUM_H
+#define SCCSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCCSUM_ABI_VERSION 1
+
+#define SCCSUM_OK 0
+#define SCCSUM_EINVAL (-1)   /* bad argument (null pointer, misalignment) */
+#define SCCSUM_ENODEV (-2)   /* no HIP device / device index out of range */
+
+/* per-packet status bits (d_status) */
+#define SCCSUM_ST_OK        0x01u /* spans: result == 0; frames: IPv4 header verifies */
+#define SCCSUM_ST_L4_OK     0x02u /* frames: L4 (pseudo-header + segment) verifies */
+#define SCCSUM_ST_MALFORMED 0x04u /* frames: len < 20, len < ip total length, or 4*ihl > ip length */
+#define SCCSUM_ST_RANGE     0x08u /* [off, off+len) outside the byte buffer: not read */
+
+/* ABI version of the loaded library (== SCCSUM_ABI_VERSION it was built with). */
+int sccsum_abi_version(void);
+
+/* Static text for an error code returned by any entry point. */
+const char* sccsum_strerror(int err);
+
+/* Number of visible HIP devices. */
+int sccsum_device_count(int* count);
+
+/* Bind the calling host thread to `device` (hipSetDevice) and cache its
+ * compute-unit count for launch sizing. */
+int sccsum_init(int device);
+
+/* Pseudo-header partial sum exactly as ipv4_traits::*_pseudo_header_checksum
+ * leaves it in a fresh checksummer (ip.hh:70-75), folded to 16 bits with
+ * end-around carry.  src_host/dst_host are host-order addresses
+ * (ipv4_address.ip); len is uint16_t so 65536 wraps to 0 like the reference. */
+uint32_t sccsum_pseudo_seed(uint32_t src_host, uint32_t dst_host, uint8_t proto, uint16_t len);
+
+/* Checksum n independent byte spans.
+ *   d_out[i]    = checksum of d_bytes[d_off[i] .. d_off[i]+d_len[i]) started
+ *                 from seed d_seed[i] (d_seed may be NULL: no seed).
+ *   d_status[i] = SCCSUM_ST_OK if d_out[i] == 0 (verify); may be NULL.
+ *   max_len     = upper bound of d_len[] used to pick the kernel variant
+ *                 (0 = unknown; any value is correct, it only tunes speed). */
+int sccsum_spans(const void* d_bytes, uint64_t bytes_len,
+                 const uint64_t* d_off, const uint32_t* d_len, const uint32_t* d_seed,
+                 uint16_t* d_out, uint8_t* d_status, uint64_t n, uint32_t max_len,
+                 void* stream);
+
+/* Checksum n IPv4 frames (IPv4 header first, no Ethernet header).
+ *   d_out2[2i]   = IPv4 header checksum over 20 bytes
+ *   d_out2[2i+1] = L4 checksum over [4*ihl, min(ip_len, len)) seeded with the
+ *                  pseudo-header (src, dst, proto from the header; length =
+ *                  that L4 span's length as uint16_t)
+ *   For generate, pass frames whose checksum fields are zero and store the
+ *   outputs; for verify, pass received frames and test the status bits.
+ *   d_status may be NULL.  max_len as for sccsum_spans. */
+int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len,
+                       const uint64_t* d_off, const uint32_t* d_len,
+                       uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len,
+                       void* stream);
+
+/* Wait for all work queued on `stream`. */
+int sccsum_sync(void* stream);
+
+/* Diagnostic: stream-read `bytes` (multiple of 16) from d_src with the same
+ * load width as the checksum kernels and write one 64-bit word per workgroup
+ * to d_sink (capacity >= sccsum_read_probe_blocks()).  Used by bench.py as
+ * the measured HBM read ceiling. */
+int sccsum_read_probe(const void* d_src, uint64_t bytes, uint64_t* d_sink, void* stream);
+int sccsum_read_probe_blocks(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SCCSUM_H */

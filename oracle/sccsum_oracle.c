@@ -1,0 +1,249 @@
+/*
+ * sccsum ORACLE — TEST INFRASTRUCTURE ONLY (see sccsum_oracle.h).
+ *
+ * Restates scylladb/seastar's software Internet checksum in C, keeping the
+ * reference's arithmetic shape (big-endian 64-bit words into a 128-bit
+ * accumulator, 128->16 fold, htons(~x)) so that its timing is representative
+ * when bench.py reports it as the CPU baseline.  Compiled -O2 like Seastar's
+ * release mode (configure.py:265).
+ */
+#include "sccsum_oracle.h"
+
+#include <arpa/inet.h>
+#include <pthread.h>
+#include <string.h>
+
+void oracle_init(oracle_checksummer* c) {
+    c->csum = 0;
+    c->odd = 0;
+}
+
+/* src/net/ip_checksum.cc:31-53.  A pending odd byte (odd==1) is the LOW half
+ * of the current 16-bit word (:33-36); then 8-byte big-endian words (:37-41,
+ * ntohq = bswap64 on little-endian, byteorder.hh:32-40); then 2-byte words
+ * (:42-46); then a trailing byte as the HIGH half (:47-51); odd flips on odd
+ * lengths (:52). */
+void oracle_sum_bytes(oracle_checksummer* c, const uint8_t* data, size_t len) {
+    size_t n = len;
+    if (c->odd && n) {
+        c->csum += *data++;
+        --n;
+    } else if (c->odd) {
+        /* the reference dereferences data even for len==0 when odd; it then
+         * decrements a size_t 0 -> huge.  No caller passes len==0 with odd
+         * set (fragments are non-empty, packet.hh:43-46), so stop here. */
+        return;
+    }
+    while (n >= 8) {
+        uint64_t w;
+        memcpy(&w, data, 8);
+        c->csum += __builtin_bswap64(w);
+        data += 8;
+        n -= 8;
+    }
+    while (n >= 2) {
+        uint16_t h;
+        memcpy(&h, data, 2);
+        c->csum += ntohs(h);
+        data += 2;
+        n -= 2;
+    }
+    if (n) {
+        c->csum += (uint32_t)(*data) << 8;
+    }
+    c->odd ^= (int)(len & 1);
+}
+
+/* include/seastar/net/ip_checksum.hh:40-47 */
+void oracle_sum_u8(oracle_checksummer* c, uint8_t v) {
+    if (!c->odd) {
+        c->csum += (uint32_t)v << 8;
+    } else {
+        c->csum += v;
+    }
+    c->odd = !c->odd;
+}
+
+/* include/seastar/net/ip_checksum.hh:48-55 */
+void oracle_sum_u16(oracle_checksummer* c, uint16_t v) {
+    if (c->odd) {
+        oracle_sum_u8(c, (uint8_t)(v >> 8));
+        oracle_sum_u8(c, (uint8_t)v);
+    } else {
+        c->csum += v;
+    }
+}
+
+/* include/seastar/net/ip_checksum.hh:56-63 (odd case adds the LOW half first) */
+void oracle_sum_u32(oracle_checksummer* c, uint32_t v) {
+    if (c->odd) {
+        oracle_sum_u16(c, (uint16_t)v);
+        oracle_sum_u16(c, (uint16_t)(v >> 16));
+    } else {
+        c->csum += v;
+    }
+}
+
+/* src/net/ip_checksum.cc:55-62: 128->64 (twice, end-around), 64->16 by four
+ * 16-bit lanes, two more end-around folds, complement, htons. */
+uint16_t oracle_get(const oracle_checksummer* c) {
+    const unsigned __int128 m64 = (unsigned __int128)0xffffffffffffffffULL;
+    unsigned __int128 x = (unsigned __int128)c->csum;
+    unsigned __int128 y = (x & m64) + (x >> 64);
+    uint64_t s = (uint64_t)((y & m64) + (y >> 64));
+    s = (s & 0xffff) + ((s >> 16) & 0xffff) + ((s >> 32) & 0xffff) + (s >> 48);
+    s = (s & 0xffff) + (s >> 16);
+    s = (s & 0xffff) + (s >> 16);
+    return htons((uint16_t)~s);
+}
+
+/* src/net/ip_checksum.cc:64-68 */
+void oracle_sum_fragments(oracle_checksummer* c, const uint8_t* const* bases,
+                          const size_t* sizes, size_t nfrag) {
+    for (size_t i = 0; i < nfrag; ++i) {
+        oracle_sum_bytes(c, bases[i], sizes[i]);
+    }
+}
+
+/* src/net/ip_checksum.cc:70-74 */
+uint16_t oracle_ip_checksum(const uint8_t* data, size_t len) {
+    oracle_checksummer c;
+    oracle_init(&c);
+    oracle_sum_bytes(&c, data, len);
+    return oracle_get(&c);
+}
+
+/* include/seastar/net/ip.hh:70-75: sum_many(src.ip.raw, dst.ip.raw,
+ * uint8_t(0), uint8_t(proto), uint16_t len) */
+void oracle_pseudo_header(oracle_checksummer* c, uint32_t src_host, uint32_t dst_host,
+                          uint8_t proto, uint16_t len) {
+    oracle_sum_u32(c, src_host);
+    oracle_sum_u32(c, dst_host);
+    oracle_sum_u8(c, 0);
+    oracle_sum_u8(c, proto);
+    oracle_sum_u16(c, len);
+}
+
+uint32_t oracle_fold_seed(const oracle_checksummer* c) {
+    unsigned __int128 x = (unsigned __int128)c->csum;
+    while (x >> 16) {
+        x = (x & 0xffff) + (x >> 16);
+    }
+    return (uint32_t)x;
+}
+
+/* ---------------- batch drivers ---------------- */
+
+static uint32_t rd_be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+static void one_span(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+                     const uint32_t* seed, uint16_t* out, uint64_t i) {
+    oracle_checksummer c;
+    oracle_init(&c);
+    if (seed) {
+        c.csum = seed[i];
+    }
+    oracle_sum_bytes(&c, bytes + off[i], len[i]);
+    out[i] = oracle_get(&c);
+}
+
+/* One IPv4 frame, following the rx path src/net/ip.cc:114-140, 220-225
+ * (header checksum over sizeof(ip_hdr)=20 B, drop if shorter than the IP
+ * total length, trim beyond it, strip 4*ihl) and the L4 checksum of
+ * include/seastar/net/tcp.hh:876-883 / src/net/udp.cc:184-195. */
+static void one_ipv4(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+                     uint16_t* out2, uint8_t* status, uint64_t i) {
+    const uint8_t* p = bytes + off[i];
+    uint32_t n = len[i];
+    uint8_t st = 0;
+    if (n < 20) {
+        out2[2 * i] = 0;
+        out2[2 * i + 1] = 0;
+        if (status) status[i] = 4;
+        return;
+    }
+    uint16_t ipc = oracle_ip_checksum(p, 20);
+    uint32_t ihl = p[0] & 0xf;
+    uint32_t ip_len = ((uint32_t)p[2] << 8) | p[3];
+    uint8_t proto = p[9];
+    uint32_t src = rd_be32(p + 12);
+    uint32_t dst = rd_be32(p + 16);
+    uint32_t l4_off = 4 * ihl;
+    uint32_t l4_end = ip_len < n ? ip_len : n;
+    if (n < ip_len) st |= 4;
+    uint32_t l4_len = 0;
+    if (l4_off > l4_end) {
+        st |= 4;
+    } else {
+        l4_len = l4_end - l4_off;
+    }
+    oracle_checksummer c;
+    oracle_init(&c);
+    oracle_pseudo_header(&c, src, dst, proto, (uint16_t)l4_len);
+    oracle_sum_bytes(&c, p + l4_off, l4_len);
+    uint16_t l4c = oracle_get(&c);
+    out2[2 * i] = ipc;
+    out2[2 * i + 1] = l4c;
+    if (ipc == 0) st |= 1;
+    if (l4c == 0) st |= 2;
+    if (status) status[i] = st;
+}
+
+typedef struct {
+    int kind;
+    const uint8_t* bytes;
+    const uint64_t* off;
+    const uint32_t* len;
+    const uint32_t* seed;
+    uint16_t* out;
+    uint8_t* status;
+    uint64_t lo, hi;
+} job_t;
+
+static void* run_job(void* arg) {
+    job_t* j = (job_t*)arg;
+    for (uint64_t i = j->lo; i < j->hi; ++i) {
+        if (j->kind == 0) {
+            one_span(j->bytes, j->off, j->len, j->seed, j->out, i);
+        } else {
+            one_ipv4(j->bytes, j->off, j->len, j->out, j->status, i);
+        }
+    }
+    return 0;
+}
+
+/* Shard-per-core like Seastar's smp: contiguous index ranges per thread. */
+static void run_batch(job_t base, uint64_t n, int nthreads) {
+    if (nthreads <= 1 || n < 2) {
+        base.lo = 0;
+        base.hi = n;
+        run_job(&base);
+        return;
+    }
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    job_t jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t] = base;
+        jobs[t].lo = n * (uint64_t)t / (uint64_t)nthreads;
+        jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        pthread_create(&th[t], 0, run_job, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; ++t) {
+        pthread_join(th[t], 0);
+    }
+}
+
+void oracle_batch_spans(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+                        const uint32_t* seed, uint16_t* out, uint64_t n, int nthreads) {
+    job_t b = {0, bytes, off, len, seed, out, 0, 0, 0};
+    run_batch(b, n, nthreads);
+}
+
+void oracle_batch_ipv4(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+                       uint16_t* out2, uint8_t* status, uint64_t n, int nthreads) {
+    job_t b = {1, bytes, off, len, 0, out2, status, 0, 0};
+    run_batch(b, n, nthreads);
+}

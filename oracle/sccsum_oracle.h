@@ -1,0 +1,84 @@
+/*
+ * sccsum ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of Seastar's software Internet checksum and of the
+ * native-stack call sites that feed it.  It exists to CHECK the product (the
+ * HIP batch kernels behind include/sccsum.h) and to provide bench.py's
+ * cpu_baseline leg.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline may load it; the product library never links or calls it.
+ *
+ * Parity pinning: the reference's own build of src/net/ip_checksum.cc is not
+ * possible in this image (its TU includes seastar/net/net.hh, which needs the
+ * absent fmt library; making it compile would need a stand-in header).  The
+ * restatement is pinned instead by the known answers recorded in SURVEY.md
+ * §8(c) (outputs of the reference compiled during the survey session) and by
+ * the published RFC 1071 / RFC 791 example vectors: tests/golden/kat.json.
+ *
+ * Every function cites the reference file:line it restates
+ * (paths relative to scylladb/seastar).
+ */
+#ifndef SCCSUM_ORACLE_H
+#define SCCSUM_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* struct checksummer { __int128 csum = 0; bool odd = false; }
+ * include/seastar/net/ip_checksum.hh:35-37 */
+typedef struct oracle_checksummer {
+    __int128 csum;
+    int odd;
+} oracle_checksummer;
+
+void oracle_init(oracle_checksummer* c);
+/* checksummer::sum(const char*, size_t)   src/net/ip_checksum.cc:31-53 */
+void oracle_sum_bytes(oracle_checksummer* c, const uint8_t* data, size_t len);
+/* checksummer::sum(uint8_t/uint16_t/uint32_t)   ip_checksum.hh:40-63 */
+void oracle_sum_u8(oracle_checksummer* c, uint8_t v);
+void oracle_sum_u16(oracle_checksummer* c, uint16_t v);
+void oracle_sum_u32(oracle_checksummer* c, uint32_t v);
+/* checksummer::get() const   src/net/ip_checksum.cc:55-62 (network-order bytes in a uint16_t) */
+uint16_t oracle_get(const oracle_checksummer* c);
+/* checksummer::sum(const packet&)   src/net/ip_checksum.cc:64-68 (walks fragments) */
+void oracle_sum_fragments(oracle_checksummer* c, const uint8_t* const* bases,
+                          const size_t* sizes, size_t nfrag);
+/* ip_checksum(const void*, size_t)   src/net/ip_checksum.cc:70-74 */
+uint16_t oracle_ip_checksum(const uint8_t* data, size_t len);
+/* ipv4_traits::{tcp,udp}_pseudo_header_checksum   include/seastar/net/ip.hh:70-75
+ * src/dst are HOST-order addresses (ipv4_address.ip, ipv4_address.hh:42);
+ * len is uint16_t, so 65536 wraps to 0 exactly as the reference signature does. */
+void oracle_pseudo_header(oracle_checksummer* c, uint32_t src_host, uint32_t dst_host,
+                          uint8_t proto, uint16_t len);
+
+/* ---- batch drivers (the reference has none; these apply the per-packet
+ *      reference calls to an offset/length array, used as checker + CPU
+ *      baseline; nthreads <= 1 runs inline) ---- */
+
+/* out[i] = checksum of bytes[off[i], off[i]+len[i]) after seeding the
+ * checksummer with csum = seed[i] (seed may be NULL = 0).  A seed is what a
+ * checksummer holds after the pseudo-header, folded (oracle_fold_seed). */
+void oracle_batch_spans(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+                        const uint32_t* seed, uint16_t* out, uint64_t n, int nthreads);
+
+/* IPv4 frames starting at bytes+off[i] with len[i] bytes:
+ *   out[2i]   = IPv4 header checksum over exactly 20 B (ip.cc:121-127, 271-277)
+ *   out[2i+1] = L4 checksum of [4*ihl, ip_len) seeded with the pseudo-header
+ *               (tcp.hh:876-883 verify / udp.cc:184-195 generate)
+ *   status[i] bit0 = IP sum verifies (== 0), bit1 = L4 sum verifies,
+ *             bit2 = malformed (len < 20, len < ip_len, 4*ihl > ip_len)
+ *   (ip.cc:114-140 drop rules). status may be NULL. */
+void oracle_batch_ipv4(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+                       uint16_t* out2, uint8_t* status, uint64_t n, int nthreads);
+
+/* Fold a checksummer csum to a seed value (end-around carry, zero stays zero). */
+uint32_t oracle_fold_seed(const oracle_checksummer* c);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

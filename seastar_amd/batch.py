@@ -1,0 +1,119 @@
+"""Device-resident packet batches and the launch wrappers over the C-ABI.
+
+A batch is the layout the kernels consume (DESIGN.md "Data layout in HBM"):
+one byte buffer holding every packet back to back (any alignment), padded to
+a multiple of 16 bytes, plus an offset (u64) / length (u32) array.  torch
+tensors only hold the device memory and give the stream; the arithmetic is in
+libsccsum.so.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import native
+
+
+def _round16(n: int) -> int:
+    return (n + 15) & ~15
+
+
+@dataclass
+class PacketBatch:
+    data: torch.Tensor  # uint8, len >= round16(bytes_len), device
+    off: torch.Tensor  # int64 [n], device
+    length: torch.Tensor  # int32 [n], device
+    bytes_len: int
+    max_len: int
+
+    @property
+    def n(self) -> int:
+        return int(self.off.numel())
+
+    @property
+    def device(self) -> torch.device:
+        return self.data.device
+
+    @staticmethod
+    def from_host(buf: np.ndarray, off: np.ndarray, length: np.ndarray, device="cuda") -> "PacketBatch":
+        buf = np.ascontiguousarray(buf, dtype=np.uint8).ravel()
+        bytes_len = int(buf.size)
+        padded = np.zeros(_round16(bytes_len) or 16, dtype=np.uint8)
+        padded[:bytes_len] = buf
+        off = np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)
+        length = np.ascontiguousarray(length, dtype=np.uint32).view(np.int32)
+        max_len = int(length.view(np.uint32).max()) if length.size else 0
+        return PacketBatch(
+            data=torch.from_numpy(padded).to(device),
+            off=torch.from_numpy(off.copy()).to(device),
+            length=torch.from_numpy(length.copy()).to(device),
+            bytes_len=bytes_len,
+            max_len=max_len,
+        )
+
+
+def _ptr(t):
+    return None if t is None else ctypes_ptr(t)
+
+
+def ctypes_ptr(t: torch.Tensor) -> int:
+    if not t.is_cuda:
+        raise ValueError("sccsum kernels need device tensors")
+    return t.data_ptr()
+
+
+def _stream(stream) -> int | None:
+    s = torch.cuda.current_stream() if stream is None else stream
+    return s.cuda_stream
+
+
+def spans(batch: PacketBatch, seeds: torch.Tensor | None = None, out: torch.Tensor | None = None,
+          status: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """sccsum_spans: one network-order uint16 checksum per span (int16 tensor)."""
+    lib = native.load()
+    n = batch.n
+    if out is None:
+        out = torch.empty(max(n, 1), dtype=torch.int16, device=batch.device)
+    if seeds is not None:
+        assert seeds.dtype == torch.int32 and seeds.numel() >= n
+    code = lib.sccsum_spans(
+        ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length),
+        _ptr(seeds), ctypes_ptr(out), _ptr(status), n, batch.max_len, _stream(stream),
+    )
+    native.check(code, "sccsum_spans")
+    return out[:n]
+
+
+def ipv4_frames(batch: PacketBatch, out2: torch.Tensor | None = None, status: torch.Tensor | None = None,
+                stream=None) -> torch.Tensor:
+    """sccsum_ipv4_frames: [n, 2] int16 (IPv4 header checksum, L4 checksum)."""
+    lib = native.load()
+    n = batch.n
+    if out2 is None:
+        out2 = torch.empty(max(2 * n, 2), dtype=torch.int16, device=batch.device)
+    code = lib.sccsum_ipv4_frames(
+        ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length),
+        ctypes_ptr(out2), _ptr(status), n, batch.max_len, _stream(stream),
+    )
+    native.check(code, "sccsum_ipv4_frames")
+    return out2[: 2 * n].view(n, 2) if n else out2[:0].view(0, 2)
+
+
+def read_probe(buf: torch.Tensor, nbytes: int, sink: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """Stream-read nbytes of buf with the kernels' load shape (HBM ceiling probe)."""
+    lib = native.load()
+    if sink is None:
+        sink = torch.zeros(lib.sccsum_read_probe_blocks(), dtype=torch.int64, device=buf.device)
+    native.check(lib.sccsum_read_probe(ctypes_ptr(buf), nbytes & ~15, ctypes_ptr(sink), _stream(stream)),
+                 "sccsum_read_probe")
+    return sink
+
+
+def as_u16(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().numpy().view(np.uint16)
+
+
+def pseudo_seed(src_host: int, dst_host: int, proto: int, length: int) -> int:
+    return int(native.load().sccsum_pseudo_seed(src_host, dst_host, proto, length & 0xFFFF))

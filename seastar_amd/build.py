@@ -1,0 +1,34 @@
+"""Build libsccsum.so in-tree with hipcc for gfx950."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+from .native import LIB_PATH, PKG_DIR, REPO_DIR
+
+SOURCES = [
+    os.path.join(PKG_DIR, "csrc", "sccsum.hip"),
+    os.path.join(PKG_DIR, "csrc", "checksummer.cc"),
+]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def hipcc_cmd(out: str = LIB_PATH) -> list[str]:
+    return [
+        HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared",
+        "-Wall", "-Wno-unused-command-line-argument",
+        "-I", os.path.join(REPO_DIR, "include"),
+        *SOURCES, "-o", out,
+    ]
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+    newest = max(os.path.getmtime(p) for p in SOURCES + [os.path.join(REPO_DIR, "include", "sccsum.h")])
+    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= newest:
+        return LIB_PATH
+    cmd = hipcc_cmd()
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return LIB_PATH

@@ -1,0 +1,90 @@
+"""ctypes binding of the C-ABI in include/sccsum.h (libsccsum.so).
+
+There is no fallback: if the library is missing or fails to load, every entry
+point raises.  torch is imported before the library is opened so that both
+share one HIP runtime (torch ships its own libamdhip64.so.7; our library's
+NEEDED entry then resolves to the already-loaded copy).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libsccsum.so")
+HEADER_PATH = os.path.join(REPO_DIR, "include", "sccsum.h")
+
+SCCSUM_OK = 0
+SCCSUM_EINVAL = -1
+SCCSUM_ENODEV = -2
+ST_OK = 0x01
+ST_L4_OK = 0x02
+ST_MALFORMED = 0x04
+ST_RANGE = 0x08
+
+
+class SccsumError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        self.code = code
+        msg = what
+        try:
+            msg = f"{what}: {load().sccsum_strerror(code).decode()} ({code})"
+        except Exception:  # noqa: BLE001 - best effort message
+            msg = f"{what}: error {code}"
+        super().__init__(msg)
+
+
+_LIB = None
+
+_u64 = ctypes.c_uint64
+_u32 = ctypes.c_uint32
+_vp = ctypes.c_void_p
+
+_PROTOS = {
+    "sccsum_abi_version": (ctypes.c_int, []),
+    "sccsum_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "sccsum_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "sccsum_init": (ctypes.c_int, [ctypes.c_int]),
+    "sccsum_pseudo_seed": (_u32, [_u32, _u32, ctypes.c_uint8, ctypes.c_uint16]),
+    "sccsum_spans": (ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),
+    "sccsum_ipv4_frames": (ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),
+    "sccsum_sync": (ctypes.c_int, [_vp]),
+    "sccsum_read_probe": (ctypes.c_int, [_vp, _u64, _vp, _vp]),
+    "sccsum_read_probe_blocks": (ctypes.c_int, []),
+}
+
+
+def header_symbols() -> list[str]:
+    """Every function declared in include/sccsum.h."""
+    text = open(HEADER_PATH).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(sccsum_[a-z0-9_]+)\s*\(", text)))
+
+
+def load():
+    """Open libsccsum.so (raises if it is missing: there is no CPU fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    import torch  # noqa: F401  -- share torch's HIP runtime (see module doc)
+
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.sccsum_abi_version() != 1:
+        raise RuntimeError("libsccsum ABI version mismatch")
+    _LIB = lib
+    return lib
+
+
+def check(code: int, what: str) -> None:
+    if code != SCCSUM_OK:
+        raise SccsumError(code, what)

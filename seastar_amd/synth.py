@@ -1,0 +1,155 @@
+"""Synthetic packet batches shaped like the native stack's traffic.
+
+Frames are built byte-for-byte the way the reference builds them:
+  IPv4 header  src/net/ip.cc:249-269  (ver 4, ihl 5, dscp/ecn 0, total length,
+               id 0, frag 0, ttl 64, proto, csum 0, src, dst — network order)
+  UDP header   src/net/udp.cc:178-182 (ports, length = UDP header + payload,
+               cksum 0 from the value-initialised header, packet.hh:586-589)
+  TCP header   include/seastar/net/tcp.hh:1621-1651, written by tcp_hdr::write
+               (:261-282) with checksum 0 and data_offset = (20+options)/4.
+Payload bytes are random.  Everything is deterministic in `seed`.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+PROTO_TCP = 6
+PROTO_UDP = 17
+IPV4_HDR = 20
+UDP_HDR = 8
+TCP_HDR = 20
+
+
+def _rng(seed: int) -> np.random.Generator:
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def _put_be16(frames: np.ndarray, col: int, vals) -> None:
+    vals = np.asarray(vals, dtype=np.uint32)
+    frames[:, col] = (vals >> 8) & 0xFF
+    frames[:, col + 1] = vals & 0xFF
+
+
+def _put_be32(frames: np.ndarray, col: int, vals) -> None:
+    vals = np.asarray(vals, dtype=np.uint64)
+    for k in range(4):
+        frames[:, col + k] = (vals >> (24 - 8 * k)) & 0xFF
+
+
+def write_ipv4_header(frames: np.ndarray, total_len, proto: int, src, dst) -> None:
+    """ipv4::send's header (ip.cc:249-269) into frames[:, 0:20], csum = 0."""
+    frames[:, 0] = 0x45  # ver 4, ihl 5
+    frames[:, 1] = 0
+    _put_be16(frames, 2, total_len)
+    frames[:, 4:8] = 0  # id 0, frag 0
+    frames[:, 8] = 64
+    frames[:, 9] = proto
+    frames[:, 10:12] = 0
+    _put_be32(frames, 12, src)
+    _put_be32(frames, 16, dst)
+
+
+def udp_ipv4_frames(n: int, frame_len: int = 1500, seed: int = 0x5EA57A2C):
+    """n equal-length IPv4/UDP frames packed back to back; checksum fields 0.
+
+    Returns (buf, off, length, meta) with meta = dict(src, dst) host-order."""
+    assert frame_len >= IPV4_HDR + UDP_HDR
+    rng = _rng(seed)
+    frames = rng.integers(0, 256, size=(n, frame_len), dtype=np.uint8)
+    src = rng.integers(1, 2**32, size=n, dtype=np.uint64)
+    dst = rng.integers(1, 2**32, size=n, dtype=np.uint64)
+    write_ipv4_header(frames, frame_len, PROTO_UDP, src, dst)
+    _put_be16(frames, 20, rng.integers(1024, 65536, size=n))
+    _put_be16(frames, 22, rng.integers(1, 65536, size=n))
+    _put_be16(frames, 24, frame_len - IPV4_HDR)
+    frames[:, 26:28] = 0
+    off = np.arange(n, dtype=np.uint64) * frame_len
+    length = np.full(n, frame_len, dtype=np.uint32)
+    return frames.reshape(-1), off, length, {"src": src, "dst": dst}
+
+
+def tcp_segments(n: int, seg_len: int, seed: int = 0x5EA57A2C, options_len: int = 0):
+    """n TCP segments (header + options + payload, no IP header) packed back to
+    back, checksum 0; meta has the host-order addresses for the pseudo-header."""
+    assert seg_len >= TCP_HDR + options_len and options_len % 4 == 0
+    rng = _rng(seed)
+    segs = rng.integers(0, 256, size=(n, seg_len), dtype=np.uint8)
+    _put_be16(segs, 0, rng.integers(1, 65536, size=n))
+    _put_be16(segs, 2, rng.integers(1, 65536, size=n))
+    _put_be32(segs, 4, rng.integers(0, 2**32, size=n, dtype=np.uint64))
+    _put_be32(segs, 8, rng.integers(0, 2**32, size=n, dtype=np.uint64))
+    segs[:, 12] = ((TCP_HDR + options_len) // 4) << 4
+    segs[:, 13] = 0x10  # ACK
+    _put_be16(segs, 14, rng.integers(0, 65536, size=n))
+    segs[:, 16:18] = 0
+    segs[:, 18:20] = 0
+    if options_len:
+        segs[:, TCP_HDR:TCP_HDR + options_len] = 1  # NOP options
+    src = rng.integers(1, 2**32, size=n, dtype=np.uint64)
+    dst = rng.integers(1, 2**32, size=n, dtype=np.uint64)
+    off = np.arange(n, dtype=np.uint64) * seg_len
+    length = np.full(n, seg_len, dtype=np.uint32)
+    return segs.reshape(-1), off, length, {"src": src, "dst": dst}
+
+
+def zipf_lengths(n: int, seed: int, s: float = 1.2, lo: int = 64, hi: int = 9000) -> np.ndarray:
+    """L = lo-1+k, k ~ Zipf(s) on {1 .. hi-lo+1} (SURVEY.md §8(d) cfg 3)."""
+    rng = _rng(seed)
+    kmax = hi - lo + 1
+    k = np.arange(1, kmax + 1, dtype=np.float64)
+    p = k ** (-s)
+    p /= p.sum()
+    draw = rng.choice(kmax, size=n, p=p) + 1
+    return (lo - 1 + draw).astype(np.uint32)
+
+
+def pack(lengths: np.ndarray, align: int = 1, seed: int | None = None, max_gap: int = 0):
+    """Offsets for packing `lengths` back to back, each start rounded up to
+    `align`, optionally with random 0..max_gap byte gaps (odd starts)."""
+    lengths = np.asarray(lengths, dtype=np.uint64)
+    gaps = np.zeros(lengths.size, dtype=np.uint64)
+    if max_gap:
+        gaps = _rng(seed or 1).integers(0, max_gap + 1, size=lengths.size).astype(np.uint64)
+    off = np.empty(lengths.size, dtype=np.uint64)
+    pos = 0
+    a = int(align)
+    for i, (L, g) in enumerate(zip(lengths.tolist(), gaps.tolist())):
+        pos += g
+        pos = (pos + a - 1) // a * a
+        off[i] = pos
+        pos += L
+    return off, pos
+
+
+def mixed_udp_frames(n: int, seed: int = 0x5EA57A2C, align: int = 1, max_gap: int = 0,
+                     lengths: np.ndarray | None = None):
+    """IPv4/UDP frames with Zipf lengths 64..9000 (cfg 3), packed at `align`."""
+    rng = _rng(seed)
+    if lengths is None:
+        lengths = zipf_lengths(n, seed)
+    off, total = pack(lengths, align=align, seed=seed + 1, max_gap=max_gap)
+    buf = rng.integers(0, 256, size=int(total), dtype=np.uint8)
+    src = rng.integers(1, 2**32, size=n, dtype=np.uint64)
+    dst = rng.integers(1, 2**32, size=n, dtype=np.uint64)
+    sport = rng.integers(1024, 65536, size=n)
+    dport = rng.integers(1, 65536, size=n)
+    for i in range(n):
+        o, L = int(off[i]), int(lengths[i])
+        f = buf[o:o + L].reshape(1, L)
+        write_ipv4_header(f, [L], PROTO_UDP, [src[i]], [dst[i]])
+        _put_be16(f, 20, [sport[i]])
+        _put_be16(f, 22, [dport[i]])
+        _put_be16(f, 24, [L - IPV4_HDR])
+        f[:, 26:28] = 0
+    return buf, off, lengths.astype(np.uint32), {"src": src, "dst": dst}
+
+
+def store_ipv4_checksums(buf: np.ndarray, off: np.ndarray, out2: np.ndarray) -> None:
+    """Write computed (IP, L4) checksums into the frames' fields: IP +10,
+    UDP +20+6 or TCP +20+16 (ihl 5 frames; header proto picks the L4)."""
+    for i in range(off.size):
+        o = int(off[i])
+        buf[o + 10:o + 12] = np.frombuffer(np.uint16(out2[i, 0]).tobytes(), np.uint8)
+        proto = int(buf[o + 9])
+        pos = o + 20 + (16 if proto == PROTO_TCP else 6)
+        buf[pos:pos + 2] = np.frombuffer(np.uint16(out2[i, 1]).tobytes(), np.uint8)

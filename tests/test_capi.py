@@ -1,0 +1,67 @@
+"""The C-ABI library loads and exports every symbol include/sccsum.h declares,
+plus the kept C++ per-packet API symbols; host-only entry
+points behave (no compute calls: no GPU here)."""
+import subprocess
+
+import numpy as np
+
+import oracle
+from seastar_amd import native
+
+CXX_API_SYMBOLS = [
+    "_ZN7seastar3net11ip_checksumEPKvm",  # ip_checksum(void const*, unsigned long)
+    "_ZN7seastar3net11checksummer3sumEPKcm",  # checksummer::sum(char const*, unsigned long)
+    "_ZNK7seastar3net11checksummer3getEv",  # checksummer::get() const
+]
+
+
+def _exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", native.LIB_PATH], check=True, capture_output=True,
+                         text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_header_symbols_exported():
+    syms = native.header_symbols()
+    assert len(syms) >= 10
+    exported = _exported()
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+
+
+def test_cxx_api_symbols_exported():
+    exported = _exported()
+    assert all(s in exported for s in CXX_API_SYMBOLS)
+
+
+def test_library_loads_and_binds_every_symbol():
+    lib = native.load()
+    for s in native.header_symbols():
+        assert hasattr(lib, s)
+    assert lib.sccsum_abi_version() == 1
+    assert lib.sccsum_strerror(0) == b"success"
+    assert lib.sccsum_strerror(native.SCCSUM_EINVAL) == b"invalid argument"
+
+
+def test_pseudo_seed_matches_oracle():
+    rng = np.random.default_rng(0)
+    lib = native.load()
+    for _ in range(2000):
+        src, dst = (int(x) for x in rng.integers(0, 2**32, 2, dtype=np.uint64))
+        proto = int(rng.choice([6, 17, 1, 255]))
+        length = int(rng.integers(0, 65537))
+        assert lib.sccsum_pseudo_seed(src, dst, proto, length & 0xFFFF) == oracle.pseudo_seed(src, dst, proto,
+                                                                                              length)
+
+
+def test_argument_validation_without_device():
+    lib = native.load()
+    assert lib.sccsum_spans(None, 0, None, None, None, None, None, 0, 0, None) == 0
+    assert lib.sccsum_ipv4_frames(None, 0, None, None, None, None, 0, 0, None) == 0
+    assert lib.sccsum_spans(None, 64, None, None, None, None, None, 3, 0, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_frames(None, 64, None, None, None, None, 3, 0, None) == native.SCCSUM_EINVAL
+    # misaligned offset array
+    assert lib.sccsum_spans(16, 64, 0x1004, 0x2000, None, 0x3000, None, 3, 0, None) == native.SCCSUM_EINVAL
+    # misaligned out2 for frames (needs 4-byte alignment)
+    assert lib.sccsum_ipv4_frames(16, 64, 0x1000, 0x2000, 0x3002, None, 3, 0, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_read_probe(None, 16, None, None) == native.SCCSUM_EINVAL

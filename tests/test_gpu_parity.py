@@ -1,0 +1,226 @@
+"""Parity of the HIP kernels (through the C-ABI) with the oracle — bit-exact.
+
+Small cases compare every output with the oracle; the full-size cases
+(BASELINE.json configs at full scale) use size-independent properties:
+generate -> store -> verify round trips, exact failure sets after corruption,
+and oracle comparison on a random sample.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from seastar_amd import batch, native, synth
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _spans(dev, buf, off, length, seeds=None, with_status=False):
+    b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+    sd = None if seeds is None else torch.from_numpy(np.asarray(seeds, np.uint32).view(np.int32)).to(dev)
+    st = torch.empty(max(b.n, 1), dtype=torch.uint8, device=dev) if with_status else None
+    out = batch.spans(b, seeds=sd, status=st)
+    torch.cuda.synchronize()
+    got = batch.as_u16(out)
+    return (got, st[: b.n].cpu().numpy()) if with_status else got
+
+
+def _frames(dev, buf, off, length):
+    b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+    st = torch.empty(max(b.n, 1), dtype=torch.uint8, device=dev)
+    out = batch.ipv4_frames(b, status=st)
+    torch.cuda.synchronize()
+    return batch.as_u16(out), st[: b.n].cpu().numpy()
+
+
+def test_known_answers(dev):
+    kat = json.load(open(os.path.join(GOLDEN, "kat.json")))
+    cases = [c for c in kat["ip_checksum"]]
+    datas = [bytes.fromhex(c["hex"]) for c in cases]
+    buf = np.frombuffer(b"".join(datas), np.uint8) if any(datas) else np.zeros(0, np.uint8)
+    length = np.array([len(d) for d in datas], np.uint32)
+    off = np.concatenate([[0], np.cumsum(length)[:-1]]).astype(np.uint64)
+    got = _spans(dev, buf, off, length)
+    want = np.array([int.from_bytes(bytes.fromhex(c["result_bytes"]), "little") for c in cases], np.uint16)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("fill", ["random", "zeros", "ones"])
+def test_every_length_every_alignment(dev, fill):
+    """Lengths 0..2100 at all 16 start alignments (head/tail masking, odd starts)."""
+    rng = np.random.default_rng(11)
+    lens = np.tile(np.arange(0, 2101, dtype=np.uint32), 16)
+    heads = np.repeat(np.arange(16, dtype=np.uint64), 2101)
+    off = np.empty(lens.size, np.uint64)
+    pos = 0
+    for i, (L, h) in enumerate(zip(lens.tolist(), heads.tolist())):
+        pos = ((pos + 15) // 16) * 16 + h
+        off[i] = pos
+        pos += L
+    if fill == "random":
+        buf = rng.integers(0, 256, size=pos, dtype=np.uint8)
+    elif fill == "zeros":
+        buf = np.zeros(pos, np.uint8)
+    else:
+        buf = np.full(pos, 0xFF, np.uint8)
+    got = _spans(dev, buf, off, lens)
+    want = oracle.batch_spans(buf, off, lens)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"first mismatches (len, head): {[(int(lens[i]), int(heads[i])) for i in bad[:8]]}"
+
+
+def test_seeds_and_status(dev):
+    rng = np.random.default_rng(5)
+    n = 4000
+    lens = rng.integers(0, 9001, size=n).astype(np.uint32)
+    off, total = synth.pack(lens, seed=9, max_gap=15)
+    buf = rng.integers(0, 256, size=total, dtype=np.uint8)
+    seeds = rng.integers(0, 65536, size=n).astype(np.uint32)
+    seeds[:50] = 0
+    seeds[50:100] = 0xFFFF
+    got, st = _spans(dev, buf, off, lens, seeds, with_status=True)
+    want = oracle.batch_spans(buf, off, lens, seeds)
+    assert np.array_equal(got, want)
+    assert np.array_equal(st, (want == 0).astype(np.uint8))
+
+
+def test_zero_sum_edge(dev):
+    """fold(0)=0 vs 0xFFFF: all-zero data with zero seed -> 0xFFFF; zero data
+    with seed 0xFFFF -> 0x0000; ff ff -> 0."""
+    buf = np.zeros(4096, np.uint8)
+    buf[2048:2050] = 0xFF
+    off = np.array([0, 0, 100, 2048, 2048, 3000], np.uint64)
+    lens = np.array([0, 2000, 1, 2, 0, 96], np.uint32)
+    seeds = np.array([0, 0, 0xFFFF, 0, 0xFFFF, 0xFFFF], np.uint32)
+    got = _spans(dev, buf, off, lens, seeds)
+    want = oracle.batch_spans(buf, off, lens, seeds)
+    assert np.array_equal(got, want)
+    assert got[0] == 0xFFFF and got[1] == 0xFFFF and got[3] == 0
+
+
+def test_large_spans_tcp64k_pseudo_wrap(dev):
+    """64 KiB TCP segments: pseudo-header length 65536 truncates to 0
+    (ip.hh:70-75, tcp.hh:878); also 65535 and jumbo lengths."""
+    n = 64
+    buf, off, lens, meta = synth.tcp_segments(n, 65536, seed=21)
+    seeds = np.array([oracle.pseudo_seed(int(s), int(d), 6, 65536) for s, d in zip(meta["src"], meta["dst"])],
+                     np.uint32)
+    seeds_cabi = np.array([batch.pseudo_seed(int(s), int(d), 6, 65536) for s, d in zip(meta["src"], meta["dst"])],
+                          np.uint32)
+    assert np.array_equal(seeds, seeds_cabi)
+    got = _spans(dev, buf, off, lens, seeds)
+    want = oracle.batch_spans(buf, off, lens, seeds)
+    assert np.array_equal(got, want)
+    # 65535-byte variant at odd offsets
+    lens2 = np.full(16, 65535, np.uint32)
+    off2, total = synth.pack(lens2, seed=3, max_gap=5)
+    rb = np.random.default_rng(8).integers(0, 256, size=total, dtype=np.uint8)
+    got2 = _spans(dev, rb, off2, lens2)
+    assert np.array_equal(got2, oracle.batch_spans(rb, off2, lens2))
+
+
+def test_udp1500_generate_verify_roundtrip(dev):
+    n = 20000
+    buf, off, lens, _ = synth.udp_ipv4_frames(n, 1500, seed=42)
+    got, st = _frames(dev, buf, off, lens)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
+    assert np.array_equal(got, want)
+    assert np.array_equal(st, want_st)
+    rx = buf.copy()
+    synth.store_ipv4_checksums(rx, off, got)
+    got2, st2 = _frames(dev, rx, off, lens)
+    assert np.all(got2 == 0) and np.all(st2 == 3)
+    # corrupt 1 %: one payload byte each -> exactly those fail L4, IP still ok
+    rng = np.random.default_rng(4)
+    bad = rng.choice(n, size=n // 100, replace=False)
+    for i in bad:
+        rx[int(off[i]) + 100 + int(i % 1000)] ^= 0x5A
+    got3, st3 = _frames(dev, rx, off, lens)
+    fail = np.nonzero((st3 & 2) == 0)[0]
+    assert np.array_equal(np.sort(fail), np.sort(bad))
+    assert np.all(st3 & 1)
+    want3, want_st3 = oracle.batch_ipv4(rx, off, lens)
+    assert np.array_equal(got3, want3) and np.array_equal(st3, want_st3)
+
+
+@pytest.mark.parametrize("align,gap", [(1, 0), (1, 9), (64, 0)])
+def test_mixed_mtu_frames(dev, align, gap):
+    buf, off, lens, _ = synth.mixed_udp_frames(3000, seed=77, align=align, max_gap=gap)
+    got, st = _frames(dev, buf, off, lens)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
+    assert np.array_equal(got, want)
+    assert np.array_equal(st, want_st)
+
+
+def test_malformed_and_range(dev):
+    rng = np.random.default_rng(3)
+    buf, off, lens, _ = synth.udp_ipv4_frames(8, 200, seed=1)
+    buf = buf.copy()
+    # 0: short frame; 1: ip_len > len; 2: ihl 15 (options beyond ip_len 200? no: 60 < 200);
+    # 3: ihl 0 (L4 starts at 0 as in the reference); 4: ip_len < len (trim);
+    # 5: ihl*4 > ip_len; 6: out of range; 7: normal
+    lens = lens.copy()
+    off = off.copy()
+    lens[0] = 19
+    buf[int(off[1]) + 2:int(off[1]) + 4] = [0x01, 0x00]  # 256 > 200
+    buf[int(off[2])] = 0x4F
+    buf[int(off[3])] = 0x40
+    buf[int(off[4]) + 2:int(off[4]) + 4] = [0x00, 0x80]  # 128 < 200
+    buf[int(off[5])] = 0x4F
+    buf[int(off[5]) + 2:int(off[5]) + 4] = [0x00, 0x28]  # 40 < 60
+    off[6] = buf.size - 10
+    got, st = _frames(dev, buf, off, lens)
+    want, want_st = oracle.batch_ipv4(buf, off[:6].copy(), lens[:6].copy())
+    assert np.array_equal(got[:6], want)
+    assert np.array_equal(st[:6], want_st)
+    assert st[6] == native.ST_RANGE and np.all(got[6] == 0)
+    want7, want_st7 = oracle.batch_ipv4(buf, off[7:].copy(), lens[7:].copy())
+    assert np.array_equal(got[7:], want7) and np.array_equal(st[7:], want_st7)
+    assert st[0] == native.ST_MALFORMED and (st[1] & native.ST_MALFORMED) and (st[5] & native.ST_MALFORMED)
+    # spans: range errors never read
+    sg, ss = _spans(dev, rng.integers(0, 256, 100, dtype=np.uint8), np.array([0, 90, 200], np.uint64),
+                    np.array([100, 20, 0], np.uint32), with_status=True)
+    assert ss[1] == native.ST_RANGE and ss[2] == native.ST_RANGE and sg[1] == 0
+
+
+def test_cabi_errors(dev):
+    lib = native.load()
+    assert lib.sccsum_spans(None, 0, None, None, None, None, None, 0, 0, None) == 0  # n == 0 is a no-op
+    assert lib.sccsum_spans(None, 16, None, None, None, None, None, 5, 0, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_init(10_000) == native.SCCSUM_ENODEV
+
+
+def test_full_scale_udp1500(dev):
+    """BASELINE cfg 2 at full size: 1,048,576 x 1500 B, generate -> store ->
+    verify (all pass), 1 % corrupted fail exactly, oracle on a 8192 sample."""
+    n, L = 1 << 20, 1500
+    from seastar_amd import devsynth
+
+    tx = devsynth.udp_frames(n, L, seed=0x5EA57A2C, device=dev)
+    out = batch.ipv4_frames(tx)
+    rx = devsynth.store_checksums(tx, out)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    out_rx = batch.ipv4_frames(rx, status=st)
+    assert int((out_rx != 0).sum()) == 0 and int((st != 3).sum()) == 0
+    idx = torch.randperm(n, device=dev, generator=torch.Generator(device=dev).manual_seed(1))[: n // 100]
+    devsynth.corrupt(rx, idx, byte=777)
+    out_bad = batch.ipv4_frames(rx, status=st)
+    failed = torch.nonzero((st & 2) == 0).flatten()
+    assert torch.equal(torch.sort(failed).values, torch.sort(idx).values)
+    sample = np.sort(np.random.default_rng(0).choice(n, 8192, replace=False))
+    frames = rx.data[: n * L].view(n, L)[torch.from_numpy(sample).to(dev)].cpu().numpy().reshape(-1)
+    soff = np.arange(sample.size, dtype=np.uint64) * L
+    want, _ = oracle.batch_ipv4(frames, soff, np.full(sample.size, L, np.uint32))
+    assert np.array_equal(batch.as_u16(out_bad)[sample], want)
+
+
+def test_read_probe(dev):
+    buf = torch.randint(0, 256, (1 << 20,), dtype=torch.uint8, device=dev)
+    sink = batch.read_probe(buf, buf.numel())
+    torch.cuda.synchronize()
+    assert int(sink.sum()) > 0

@@ -1,0 +1,177 @@
+"""Pins the oracle (oracle/sccsum_oracle.c) before it is trusted as checker.
+
+1. Known answers: tests/golden/kat.json — outputs of the compiled reference
+   recorded in SURVEY.md §8(c) plus the RFC 1071 / RFC 791 published vectors.
+2. An independent formulation: the closed form of the reference's result
+   (SURVEY.md finding 4: htons(~fold(S)) with S the integer sum of big-endian
+   words, fold(0)=0, fold(S)=1+((S-1) mod 65535)), in pure Python.
+3. The stateful semantics of the inline members (ip_checksum.hh:40-69) and of
+   fragment walks (ip_checksum.cc:64-68), against a pure-Python model.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def closed_form(data: bytes, seed: int = 0) -> int:
+    """uint16 value (little-endian host) the reference returns."""
+    if len(data) % 2:
+        data = data + b"\0"
+    s = seed + sum(int.from_bytes(data[i:i + 2], "big") for i in range(0, len(data), 2))
+    f = 0 if s == 0 else 1 + (s - 1) % 65535
+    c = ~f & 0xFFFF
+    return ((c & 0xFF) << 8) | (c >> 8)
+
+
+class PyChecksummer:
+    """Pure-Python statement of struct checksummer (ip_checksum.hh:35-69)."""
+
+    def __init__(self):
+        self.csum = 0
+        self.odd = False
+
+    def u8(self, v):
+        self.csum += v if self.odd else v << 8
+        self.odd = not self.odd
+
+    def u16(self, v):
+        if self.odd:
+            self.u8(v >> 8)
+            self.u8(v & 0xFF)
+        else:
+            self.csum += v
+
+    def u32(self, v):
+        if self.odd:
+            self.u16(v & 0xFFFF)
+            self.u16(v >> 16)
+        else:
+            self.csum += v
+
+    def data(self, b: bytes):
+        for x in b:
+            self.u8(x)
+
+    def get(self):
+        s = self.csum
+        f = 0 if s == 0 else 1 + (s - 1) % 65535
+        c = ~f & 0xFFFF
+        return ((c & 0xFF) << 8) | (c >> 8)
+
+
+def test_kat():
+    kat = json.load(open(os.path.join(GOLDEN, "kat.json")))
+    for case in kat["ip_checksum"]:
+        data = bytes.fromhex(case["hex"])
+        want = int.from_bytes(bytes.fromhex(case["result_bytes"]), "little")
+        assert oracle.ip_checksum(data) == want, case["name"]
+        assert closed_form(data) == want, case["name"]
+
+
+def test_closed_form_random():
+    rng = np.random.default_rng(123)
+    for _ in range(3000):
+        n = int(rng.integers(0, 300))
+        kind = rng.integers(0, 4)
+        if kind == 0:
+            d = bytes(n)
+        elif kind == 1:
+            d = b"\xff" * n
+        else:
+            d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert oracle.ip_checksum(d) == closed_form(d), (n, kind)
+
+
+def test_closed_form_long():
+    rng = np.random.default_rng(7)
+    for n in (1500, 9000, 65535, 65536):
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert oracle.ip_checksum(d) == closed_form(d)
+
+
+def test_fragments_equal_contiguous():
+    """1501 random bytes split 7/1/333/1160 = contiguous;
+    plus the packet_test.cc fragment sizes 5/31/65/4096/4096."""
+    rng = np.random.default_rng(99)
+    for sizes in ([7, 1, 333, 1160], [5, 31, 65, 4096, 4096], [1] * 17, [3, 3, 3, 2, 9]):
+        total = sum(sizes)
+        d = rng.integers(0, 256, total, dtype=np.uint8).tobytes()
+        c = oracle.new()
+        pos = 0
+        for s in sizes:
+            oracle.sum_bytes(c, d[pos:pos + s])
+            pos += s
+        assert oracle.get(c) == oracle.ip_checksum(d) == closed_form(d)
+        # and the fragment-list entry point
+        arrs = [np.frombuffer(d[sum(sizes[:i]):sum(sizes[:i + 1])], np.uint8).copy() for i in range(len(sizes))]
+        bases = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+        szs = (ctypes.c_size_t * len(arrs))(*sizes)
+        c2 = oracle.new()
+        oracle.lib().oracle_sum_fragments(ctypes.byref(c2), bases, szs, len(arrs))
+        assert oracle.get(c2) == oracle.get(c)
+
+
+def test_inline_members_model():
+    rng = np.random.default_rng(5)
+    for _ in range(500):
+        c = oracle.new()
+        m = PyChecksummer()
+        for _ in range(int(rng.integers(1, 12))):
+            op = int(rng.integers(0, 4))
+            if op == 0:
+                v = int(rng.integers(0, 256))
+                oracle.lib().oracle_sum_u8(ctypes.byref(c), v)
+                m.u8(v)
+            elif op == 1:
+                v = int(rng.integers(0, 65536))
+                oracle.lib().oracle_sum_u16(ctypes.byref(c), v)
+                m.u16(v)
+            elif op == 2:
+                v = int(rng.integers(0, 2**32))
+                oracle.lib().oracle_sum_u32(ctypes.byref(c), v)
+                m.u32(v)
+            else:
+                d = rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8).tobytes()
+                oracle.sum_bytes(c, d)
+                m.data(d)
+            assert bool(c.odd) == m.odd
+        assert oracle.get(c) == m.get()
+
+
+def test_pseudo_header_len_wrap():
+    """len 65536 == len 0 (uint16_t parameter, ip.hh:70-75)."""
+    a = oracle.pseudo_seed(0xC0A80001, 0x0A000002, 6, 65536)
+    b = oracle.pseudo_seed(0xC0A80001, 0x0A000002, 6, 0)
+    assert a == b
+    m = PyChecksummer()
+    for v in (0xC0A80001, 0x0A000002):
+        m.u32(v)
+    m.u8(0)
+    m.u8(6)
+    m.u16(1480)
+    c = oracle.new()
+    oracle.lib().oracle_pseudo_header(ctypes.byref(c), 0xC0A80001, 0x0A000002, 6, 1480)
+    assert c.csum == m.csum
+
+
+@pytest.mark.parametrize("nthreads", [1, 4])
+def test_batch_drivers_match_single_calls(nthreads):
+    from seastar_amd import synth
+
+    buf, off, lens, meta = synth.udp_ipv4_frames(200, 1500, seed=3)
+    out2, st = oracle.batch_ipv4(buf, off, lens, nthreads=nthreads)
+    for i in range(0, 200, 17):
+        f = buf[int(off[i]):int(off[i]) + 1500].tobytes()
+        assert out2[i, 0] == closed_form(f[:20])
+        seed = int(meta["src"][i]) + int(meta["dst"][i]) + 17 + 1480
+        assert out2[i, 1] == closed_form(f[20:], seed)
+    assert np.all(st & 0x4 == 0)
+    spans = oracle.batch_spans(buf, off, lens, nthreads=nthreads)
+    assert spans[5] == closed_form(buf[int(off[5]):int(off[5]) + 1500].tobytes())
