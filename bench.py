@@ -219,7 +219,7 @@ def main():
     torch.cuda.synchronize()
     ceiling = (tx.bytes_len & ~15) * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
 
-    traffic, traffic_src = pmc_traffic(args.pmc, "csum_kernel")
+    traffic, traffic_src = pmc_traffic(args.pmc, "csum_batch_kernel")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -249,7 +249,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "csum_kernel<2,true> (sccsum_ipv4_frames)",
+                "kernel": "csum_batch_kernel<2,true,false,nt,hybrid> (sccsum_ipv4_frames)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",

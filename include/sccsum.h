@@ -35,7 +35,7 @@
  *     roundup(bytes_len, 16) (hipMalloc allocations always are).
  *   - A packet whose [off, off+len) is not inside [0, bytes_len) is not read:
  *     its outputs are 0 and its status has SCCSUM_ST_RANGE.
- *   - d_off must be 8-byte aligned, d_len/d_seed/d_out2 4-byte aligned,
+ *   - d_bytes must be 16-byte aligned, d_off 8-byte aligned, d_len/d_seed/d_out2 4-byte aligned,
  *     d_out 2-byte aligned.
  *   - Launches are asynchronous on `stream` (a hipStream_t; NULL = the
  *     device's null stream).  No allocation, no host synchronisation: the
@@ -108,6 +108,21 @@ int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len,
                        const uint64_t* d_off, const uint32_t* d_len,
                        uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len,
                        void* stream);
+
+/* Diagnostic: select the kernel family for later launches in this process
+ * (0 = default (6 up to 2 KiB packets, else 2), 1 = one-packet-per-wave
+ * loop, 2 = batch kernel, 3 = batch
+ * kernel with the next packet in flight, 4 / 5 = 2 / 3 with default cache
+ * policy instead of nontemporal loads, 6 / 7 = 2 / 3 with each packet's last
+ * 128-byte line loaded with the default policy).  All variants produce
+ * identical results; the knob exists for in-process A/B timing and for
+ * cross-checking two independent kernels.  SCCSUM_EINVAL for an unknown one. */
+int sccsum_set_kernel_variant(int variant);
+
+/* Diagnostic: cap the launch grid at `blocks` 256-thread workgroups per
+ * compute unit (default 8 = 32 waves/CU).  Occupancy A/B knob; results are
+ * unaffected.  Returns SCCSUM_EINVAL outside 1..32. */
+int sccsum_set_blocks_per_cu(int blocks);
 
 /* Wait for all work queued on `stream`. */
 int sccsum_sync(void* stream);

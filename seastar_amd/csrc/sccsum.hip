@@ -11,11 +11,17 @@
 // reorder and widen freely — it loads aligned 16-byte units.
 //
 // Layout: packets live anywhere inside one byte buffer behind an
-// offset (u64) / length (u32) array.  One wavefront owns one packet at a time:
-// lane i loads 16-byte units i, i+64, ... of the aligned span covering the
-// packet, masks the bytes outside it, accumulates 64-bit lane sums, and the
-// wave folds them with DPP row operations + 4 readlanes.  No LDS, no MFMA: a
-// byte reduction at the HBM read roofline.
+// offset (u64) / length (u32) array.  Default kernel (csum_batch_kernel): a
+// wavefront takes a tile of up to 64 packets, plans them one per lane, then
+// streams them one packet at a time — every lane loads 16-byte units of the
+// packet through a raw buffer descriptor sized to the packet's unit span
+// (lanes past it read zeros, no per-lane masking), sums them with v_sad_u16,
+// folds the 64 lanes with DPP row ops + 4 readlanes — and finally each lane
+// finishes one packet (edge-byte correction from units stashed in LDS, IPv4
+// header decode, pseudo-header, complement) with one coalesced store per
+// tile.  No MFMA: a byte reduction at the HBM read roofline.
+// csum_kernel is a deliberately plain second implementation (one packet per
+// wave, per-lane byte masks) kept for cross-checking.
 
 #include <hip/hip_runtime.h>
 
@@ -224,6 +230,337 @@ __global__ __launch_bounds__(kBlock) void csum_kernel(
     }
 }
 
+// ---------------------------------------------------------------- batch-kernel helpers
+
+// Keep bytes [lo, hi) of a 64-bit half unit (half-relative byte indices).
+__device__ __forceinline__ uint64_t keep_half(uint64_t q, int lo, int hi) {
+    const int a = min(max(lo, 0), 8);
+    const int b = min(max(hi, 0), 8);
+    const int w = b - a;
+    const int sh = w > 0 ? 64 - 8 * w : 0;
+    const uint64_t m = (~0ull >> sh) << (8 * (w > 0 ? a : 0));
+    return w > 0 ? (q & m) : 0ull;
+}
+
+// Sum the four dwords of a unit as 16-bit halves into a 32-bit accumulator
+// (v_sad_u16 with a zero operand: lo16 + hi16 + acc, one instruction per dword).
+__device__ __forceinline__ uint32_t sad4(const u32x4& v, uint32_t acc) {
+    acc = __builtin_amdgcn_sad_u16(v.x, 0u, acc);
+    acc = __builtin_amdgcn_sad_u16(v.y, 0u, acc);
+    acc = __builtin_amdgcn_sad_u16(v.z, 0u, acc);
+    return __builtin_amdgcn_sad_u16(v.w, 0u, acc);
+}
+
+// Masked unit (bytes [lo, hi) kept, unit-relative) summed like sad4.
+__device__ __forceinline__ uint32_t sad4_masked(const u32x4& v, int lo, int hi, uint32_t acc) {
+    const uint64_t k0 = keep_half(static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32), lo, hi);
+    const uint64_t k1 = keep_half(static_cast<uint64_t>(v.z) | (static_cast<uint64_t>(v.w) << 32), lo - 8, hi - 8);
+    acc = __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k0), 0u, acc);
+    acc = __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k0 >> 32), 0u, acc);
+    acc = __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k1), 0u, acc);
+    return __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k1 >> 32), 0u, acc);
+}
+
+constexpr int kRsrcFlags = 0x00020000;  // raw buffer, 32-bit data format (gfx950)
+constexpr int kNT = 2;                  // nontemporal: streamed once
+
+// Descriptor inputs pass through readfirstlane so the compiler can prove the
+// descriptor wave-uniform (otherwise it wraps every buffer op in a waterfall
+// loop: guide T20).  Callers only pass wave-uniform values.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* base, uint32_t bytes) {
+    const uint64_t b = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b >> 32));
+    const uint32_t nb = __builtin_amdgcn_readfirstlane(bytes);
+    void* p = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, static_cast<short>(0), static_cast<int>(nb), kRsrcFlags);
+}
+
+// ---------------------------------------------------------------- batch kernel (default)
+
+// Put a wave-uniform value into lane `k` of `v` (compare + select; gfx9's
+// v_writelane cannot read both a value and a lane select from SGPRs).
+__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t value, uint32_t k, uint32_t lane) {
+    return lane == k ? value : v;
+}
+
+// Sum of the bytes [lo, hi) of a 16-byte unit as little-endian 16-bit words
+// at their unit-relative positions (sad4 of the masked unit).
+__device__ __forceinline__ uint32_t unit_part(const u32x4& v, int lo, int hi) {
+    return sad4_masked(v, lo, hi, 0u);
+}
+
+constexpr uint32_t kStashUnits = 4;     // units 0..2 of a packet (IPv4 header) + its last unit
+constexpr uint32_t kStashStride = 80;   // bytes per packet row (5 x 16 B: conflict-free ds_read_b128)
+constexpr uint32_t kExactMax = 131072;  // fast path keeps exact 32-bit sums up to this length
+static_assert(kStashStride >= 16 * kStashUnits && kStashStride % 16 == 0, "stash row layout");
+
+// Exact folded sum (little-endian domain relative to a0) of [rs, re), one
+// wave, any length: the slow path for packets the batch pass cannot take.
+__device__ uint32_t exact_range_sum(const uint8_t* a0, uint64_t rs, uint64_t re, uint32_t lane) {
+    uint64_t acc = 0;
+    if (re > rs) {
+        const uint64_t c0 = rs >> 4, c1 = (re - 1) >> 4;
+        for (uint64_t c = c0; c <= c1; c += kWave) {
+            const uint64_t cu = c + lane;
+            u32x4 w = u32x4{0, 0, 0, 0};
+            if (cu <= c1) w = load_unit(a0 + 16 * cu);
+            const int64_t lo = static_cast<int64_t>(rs) - static_cast<int64_t>(16 * cu);
+            const int64_t hi = static_cast<int64_t>(re) - static_cast<int64_t>(16 * cu);
+            const int l = static_cast<int>(lo < -16 ? -16 : (lo > 32 ? 32 : lo));
+            const int h = static_cast<int>(hi < -16 ? -16 : (hi > 32 ? 32 : hi));
+            acc += sad4_masked(w, l, h, 0u);
+        }
+    }
+    return fold16(wave_sum(fold16(acc)));
+}
+
+// Batch kernel.  Wave w owns tiles t = w, w + W, ... of B consecutive packets.
+//  A: lane i takes packet i of the tile: offset, length, seed, unit span.
+//  B: per packet (wave-uniform loop): 3 readlanes, one raw buffer descriptor
+//     sized to the packet's 16-byte unit span (lanes past it read zeros),
+//     unmasked v_sad_u16 sums, DPP row sums + 4 readlanes -> exact 32-bit
+//     sum written into lane k; units 0..2 and the last unit are stashed in LDS.
+//  C: lane i finishes packet i: subtracts the stashed bytes outside the
+//     summed range, decodes the IPv4 header (frames), folds, adds the seed or
+//     pseudo-header, complements; one coalesced store for the tile.
+//  D: packets the fast path cannot take (frames with options or a trimmed
+//     IP length, spans longer than 128 KiB) are redone exactly, one wave each.
+template <int U, bool IPV4, bool PIPE, int AUX, bool HYB>
+__global__ __launch_bounds__(kBlock) void csum_batch_kernel(
+    const uint8_t* __restrict__ bytes, uint64_t bytes_len,
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
+    const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
+    uint8_t* __restrict__ status, uint64_t n, uint32_t B) {
+    __shared__ __attribute__((aligned(16))) uint8_t stash_all[kWavesPerBlock][kWave * kStashStride];
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    uint8_t* stash = stash_all[wv];
+    const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+    const uint64_t ntiles = (n + B - 1) / B;
+    const bool has_seed = !IPV4 && seed != nullptr;
+    const uint32_t vo = 16u * lane;  // this lane's byte offset inside a 1 KiB slice
+
+    for (uint64_t t = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv; t < ntiles; t += nwaves) {
+        // ---- A: per-lane packet plan
+        const uint64_t base = t * B;
+        const uint64_t left = n - base;
+        const uint32_t cnt = left < B ? static_cast<uint32_t>(left) : B;
+        const bool mine = lane < cnt;
+        const uint64_t q = base + (mine ? lane : 0);
+        const uint64_t o = off[q];
+        const uint32_t L = mine ? len[q] : 0u;
+        const uint32_t sd = has_seed ? seed[q] : 0u;
+        const bool range_bad = o > bytes_len || L > bytes_len - o;
+        const bool short_frame = IPV4 && L < 20;
+        const bool huge = L > kExactMax;
+        const uint8_t* ptr = bytes + (range_bad ? 0 : o);
+        const uint32_t head = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ptr) & 15u);
+        const uint64_t a0 = reinterpret_cast<uint64_t>(ptr - head);
+        const bool fast = mine && !range_bad && !short_frame && !huge;
+        const uint32_t nunits = (fast && L) ? (head + L + 15u) >> 4 : 0u;
+
+        // ---- B: one packet at a time
+        // HYB: the units of the packet's last 128-byte line (shared with the
+        // next packet when packets are packed back to back) are loaded with
+        // the default cache policy so the next packet's first line hits in
+        // L2; all other units stream nontemporally.
+        uint32_t res = 0;
+        struct PktLoad {
+            __amdgpu_buffer_rsrc_t r;  // units [0, s)
+            uint32_t nu, s;
+            u32x4 v[U];
+            u32x4 w;  // HYB: lane i <- unit s + i of the last line (i < 8)
+        };
+        auto issue = [&](uint32_t k, bool valid, PktLoad& P) {
+            P.nu = valid ? __builtin_amdgcn_readlane(nunits, k) : 0u;
+            const uint32_t alo = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0), k);
+            const uint32_t ahi = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0 >> 32), k);
+            const uint8_t* pa = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(ahi) << 32) | alo);
+            if (HYB) {
+                const uint32_t f = (alo >> 4) & 7u;  // first unit's slot in its 128-byte line
+                const uint32_t ls = P.nu ? ((f + P.nu - 1) & ~7u) : 0u;
+                P.s = ls > f ? ls - f : 0u;
+                const auto rw = rsrc(pa + 16u * P.s, 16u * (P.nu - P.s));
+                P.w = __builtin_amdgcn_raw_buffer_load_b128(rw, static_cast<int>(vo), 0, 0);
+            } else {
+                P.s = P.nu;
+                P.w = u32x4{0, 0, 0, 0};
+            }
+            P.r = rsrc(pa, 16u * P.s);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                P.v[u] = __builtin_amdgcn_raw_buffer_load_b128(P.r, static_cast<int>(vo + 1024u * u), 0, AUX);
+        };
+        auto body = [&](uint32_t k, PktLoad& P) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = sad4(P.v[u], acc);
+            if (HYB) acc = sad4(P.w, acc);
+            uint8_t* row = stash + k * kStashStride;
+            constexpr uint32_t kHead = IPV4 ? 3u : 1u;
+            if (lane < kHead && lane < P.s) *reinterpret_cast<u32x4*>(row + 16u * lane) = P.v[0];
+            if (HYB && lane + P.s < kHead) *reinterpret_cast<u32x4*>(row + 16u * (lane + P.s)) = P.w;
+            const uint32_t gu = static_cast<uint32_t>(U) * kWave;
+            for (uint32_t g = gu; g < P.s; g += gu) {
+                u32x4 w[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    w[u] = __builtin_amdgcn_raw_buffer_load_b128(P.r, static_cast<int>(16u * g + vo + 1024u * u), 0,
+                                                                 AUX);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    acc = sad4(w[u], acc);
+                    P.v[u] = w[u];
+                }
+            }
+            // last unit of the span -> stash slot 3
+            if (P.nu) {
+                const uint32_t last = P.nu - 1;
+                if (HYB) {
+                    if (lane + P.s == last) *reinterpret_cast<u32x4*>(row + 48) = P.w;
+                } else {
+                    const uint32_t slot = (last >> 6) % U;
+                    u32x4 lu = P.v[0];
+#pragma unroll
+                    for (int u = 1; u < U; ++u) lu = slot == static_cast<uint32_t>(u) ? P.v[u] : lu;
+                    if (lane == (last & 63u)) *reinterpret_cast<u32x4*>(row + 48) = lu;
+                }
+            }
+            const uint32_t S = wave_sum(acc);
+            res = writelane(res, S, k, lane);
+        };
+
+        if (!PIPE) {
+            for (uint32_t k = 0; k < cnt; ++k) {
+                PktLoad P;
+                issue(k, true, P);
+                body(k, P);
+            }
+        } else {
+            PktLoad P, P1;
+            issue(0, true, P);
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const bool more = k + 1 < cnt;
+                issue(more ? k + 1 : k, more, P1);
+                body(k, P);
+                P = P1;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): stash writes visible to this wave's reads
+        __builtin_amdgcn_wave_barrier();
+
+        // ---- C: lane i finishes packet i
+        const int rs0 = static_cast<int>(head) + (IPV4 ? 20 : 0);
+        const int re0 = static_cast<int>(head + L);
+        const uint8_t* row = stash + lane * kStashStride;
+        const u32x4 s0 = *reinterpret_cast<const u32x4*>(row);
+        const u32x4 s1 = *reinterpret_cast<const u32x4*>(row + 16);
+        const u32x4 s2 = *reinterpret_cast<const u32x4*>(row + 32);
+        const u32x4 s3 = *reinterpret_cast<const u32x4*>(row + 48);
+        const int lastu16 = 16 * (static_cast<int>(nunits) - 1);
+        uint32_t excl = unit_part(s0, 0, rs0);
+        if (IPV4) {
+            excl += unit_part(s1, 0, rs0 - 16) + unit_part(s2, 0, rs0 - 32);
+        }
+        excl += unit_part(s3, re0 - lastu16, 16);
+        // a unit that is both among 0..2 and the last one is excluded twice,
+        // but on disjoint byte ranges ([0, rs) and [re, 16)).
+        const uint32_t kept = nunits ? res - excl : 0u;
+        uint32_t S = fold16(kept);
+        if (head & 1u) S = swap16(S);
+        uint32_t word = 0, st = 0;
+        bool slow = huge && mine && !range_bad;
+        uint32_t ipc = 0, pseudo = 0;
+        int srs = 0, sre = 0;
+        if (IPV4) {
+            // header dwords at byte `head` of the stash row
+            const uint32_t* hw = reinterpret_cast<const uint32_t*>(row + (head & ~3u));
+            const uint32_t sh = head & 3u;
+            const uint32_t d0 = hw[0], d1 = hw[1], d2 = hw[2], d3 = hw[3], d4 = hw[4], d5 = hw[5];
+            const uint32_t h0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+            const uint32_t h1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            const uint32_t h2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+            const uint32_t h3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+            const uint32_t h4 = __builtin_amdgcn_alignbyte(d5, d4, sh);
+            ipc = ~fold16(static_cast<uint64_t>(h0) + h1 + h2 + h3 + h4) & 0xffffu;
+            const uint32_t ihl = h0 & 0xfu;
+            const uint32_t ip_len = swap16(h0 >> 16);
+            const uint32_t proto = (h2 >> 8) & 0xffu;
+            const uint32_t l4_off = 4u * ihl;
+            const uint32_t l4_end = ip_len < L ? ip_len : L;
+            uint32_t l4_len = 0;
+            if (L < ip_len) st |= SCCSUM_ST_MALFORMED;
+            if (l4_off > l4_end) {
+                st |= SCCSUM_ST_MALFORMED;
+            } else {
+                l4_len = l4_end - l4_off;
+            }
+            pseudo = fold16(static_cast<uint64_t>(h3 & 0xffffu) + (h3 >> 16) + (h4 & 0xffffu) + (h4 >> 16) +
+                            (proto << 8) + swap16(l4_len & 0xffffu));
+            slow = slow || (fast && (ihl != 5u || ip_len != L));
+            srs = static_cast<int>(head + l4_off);
+            sre = srs + static_cast<int>(l4_len);
+            const uint32_t r = ~fold16(static_cast<uint64_t>(S) + pseudo) & 0xffffu;
+            word = ipc | (r << 16);
+            st |= (ipc == 0 ? SCCSUM_ST_OK : 0u) | (r == 0 ? SCCSUM_ST_L4_OK : 0u);
+        } else {
+            const uint32_t r = ~fold16(static_cast<uint64_t>(S) + swap16(fold16(sd))) & 0xffffu;
+            word = r;
+            st = r == 0 ? SCCSUM_ST_OK : 0u;
+        }
+        if (range_bad) {
+            word = 0;
+            st = SCCSUM_ST_RANGE;
+        } else if (short_frame) {
+            word = 0;
+            st = SCCSUM_ST_MALFORMED;
+        }
+
+        // ---- D: exact redo of the packets the fast path could not take
+        uint64_t todo = __ballot(slow);
+        while (todo) {
+            const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            const uint32_t jlo = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0), j);
+            const uint32_t jhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0 >> 32), j);
+            const uint8_t* ja0 = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(jhi) << 32) | jlo);
+            const uint32_t jhead = __builtin_amdgcn_readlane(head, j);
+            uint64_t rs, re;
+            if (IPV4) {
+                rs = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(srs), j));
+                re = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(sre), j));
+            } else {
+                rs = jhead;
+                re = static_cast<uint64_t>(jhead) + __builtin_amdgcn_readlane(L, j);
+            }
+            uint32_t SJ = exact_range_sum(ja0, rs, re, lane);
+            if (jhead & 1u) SJ = swap16(SJ);
+            if (lane == j) {
+                if (IPV4) {
+                    const uint32_t r = ~fold16(static_cast<uint64_t>(SJ) + pseudo) & 0xffffu;
+                    word = ipc | (r << 16);
+                    st = (st & ~SCCSUM_ST_L4_OK) | (r == 0 ? SCCSUM_ST_L4_OK : 0u);
+                } else {
+                    const uint32_t r = ~fold16(static_cast<uint64_t>(SJ) + swap16(fold16(sd))) & 0xffffu;
+                    word = r;
+                    st = r == 0 ? SCCSUM_ST_OK : 0u;
+                }
+            }
+        }
+
+        if (mine) {
+            if (IPV4) {
+                reinterpret_cast<uint32_t*>(out)[base + lane] = word;
+            } else {
+                out[base + lane] = static_cast<uint16_t>(word);
+            }
+            if (status) status[base + lane] = static_cast<uint8_t>(st);
+        }
+        __builtin_amdgcn_wave_barrier();  // stash rows are rewritten by the next tile
+    }
+}
+
 // Plain stream-read of the same load shape (16 B per lane, nontemporal).
 __global__ __launch_bounds__(kBlock) void read_probe_kernel(const u32x4* __restrict__ src, uint64_t units,
                                                              uint64_t* __restrict__ sink) {
@@ -262,8 +599,10 @@ int cu_count() {
     return c;
 }
 
+std::atomic<int> g_blocks_per_cu{kBlocksPerCU};
+
 unsigned grid_for(uint64_t n) {
-    const uint64_t cap = static_cast<uint64_t>(cu_count()) * kBlocksPerCU;
+    const uint64_t cap = static_cast<uint64_t>(cu_count()) * g_blocks_per_cu.load(std::memory_order_relaxed);
     uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
     if (want > cap) want = cap;
     want = (want + 7) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
@@ -279,32 +618,85 @@ int units_class(uint32_t max_len) {
     return 8;
 }
 
+// Kernel variant: 0 = default (batch kernel: 6 for packets up to 2 KiB, else 2),
+// 1 = simple one-packet-per-wave loop (independent second implementation),
+// 2 = batch kernel, 3 = batch kernel with the next packet in flight (both
+// with nontemporal loads), 4 / 5 = 2 / 3 with default-policy loads,
+// 6 / 7 = 2 / 3 with each packet's last 128-byte line loaded default-policy.
+std::atomic<int> g_variant{0};
+
+template <int U, bool IPV4>
+void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
+              const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n) {
+    if (variant == 1) {
+        csum_kernel<U, IPV4>
+            <<<dim3(grid_for(n)), dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
+        return;
+    }
+    // batch kernel: tiles of B <= 64 packets, enough tiles to fill every wave slot
+    const uint64_t slots = static_cast<uint64_t>(cu_count()) * g_blocks_per_cu.load() * kWavesPerBlock;
+    uint64_t B = (n + slots - 1) / slots;
+    B = B < 1 ? 1 : (B > kWave ? kWave : B);
+    const dim3 grid(grid_for((n + B - 1) / B));
+    const uint32_t b32 = static_cast<uint32_t>(B);
+    // default: up to 2 KiB packets -> hybrid policy (last line cached for the
+    // neighbour), longer ones -> all nontemporal; no cross-packet prefetch
+    // (measured: it only adds issue work).
+    const int v = variant != 0 ? variant : (U <= 2 ? 6 : 2);
+    switch (v) {
+        case 6:
+            csum_batch_kernel<U, IPV4, false, kNT, true>
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+            break;
+        case 7:
+            csum_batch_kernel<U, IPV4, true, kNT, true>
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+            break;
+        case 2:
+            csum_batch_kernel<U, IPV4, false, kNT, false>
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+            break;
+        case 4:
+            csum_batch_kernel<U, IPV4, false, 0, false>
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+            break;
+        case 5:
+            csum_batch_kernel<U, IPV4, true, 0, false>
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+            break;
+        default:
+            csum_batch_kernel<U, IPV4, true, kNT, false>
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+            break;
+    }
+}
+
 template <bool IPV4>
 int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
            const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n, uint32_t max_len,
            void* stream) {
     if (n == 0) return SCCSUM_OK;
     if (!d_bytes || !d_off || !d_len || !d_out) return SCCSUM_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(d_off) & 7u) || (reinterpret_cast<uintptr_t>(d_len) & 3u) ||
-        (reinterpret_cast<uintptr_t>(d_seed) & 3u) ||
+    if ((reinterpret_cast<uintptr_t>(d_bytes) & 15u) || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
+        (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_seed) & 3u) ||
         (reinterpret_cast<uintptr_t>(d_out) & (IPV4 ? 3u : 1u))) {
         return SCCSUM_EINVAL;
     }
+    const int variant = g_variant.load(std::memory_order_relaxed);
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    const dim3 grid(grid_for(n)), block(kBlock);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
     switch (units_class(max_len)) {
         case 1:
-            csum_kernel<1, IPV4><<<grid, block, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
+            launch_u<1, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
             break;
         case 2:
-            csum_kernel<2, IPV4><<<grid, block, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
+            launch_u<2, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
             break;
         case 4:
-            csum_kernel<4, IPV4><<<grid, block, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
+            launch_u<4, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
             break;
         default:
-            csum_kernel<8, IPV4><<<grid, block, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
+            launch_u<8, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
             break;
     }
     return static_cast<int>(hipGetLastError());
@@ -359,6 +751,18 @@ int sccsum_spans(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off,
 int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
                        uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len, void* stream) {
     return sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len, stream);
+}
+
+int sccsum_set_kernel_variant(int variant) {
+    if (variant < 0 || variant > 7) return SCCSUM_EINVAL;
+    sccsum::g_variant.store(variant, std::memory_order_relaxed);
+    return SCCSUM_OK;
+}
+
+int sccsum_set_blocks_per_cu(int blocks) {
+    if (blocks < 1 || blocks > 32) return SCCSUM_EINVAL;
+    sccsum::g_blocks_per_cu.store(blocks, std::memory_order_relaxed);
+    return SCCSUM_OK;
 }
 
 int sccsum_sync(void* stream) { return static_cast<int>(hipStreamSynchronize(static_cast<hipStream_t>(stream))); }

@@ -20,6 +20,15 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7], ids=["simple", "batch", "batch_pipe", "batch_dflt", "batch_pipe_dflt", "batch_hyb", "batch_pipe_hyb"], autouse=True)
+def kernel_variant(request, dev):
+    """Every parity test runs against both kernel families."""
+    lib = native.load()
+    native.check(lib.sccsum_set_kernel_variant(request.param), "set variant")
+    yield request.param
+    native.check(lib.sccsum_set_kernel_variant(0), "reset variant")
+
+
 def _spans(dev, buf, off, length, seeds=None, with_status=False):
     b = batch.PacketBatch.from_host(buf, off, length, device=dev)
     sd = None if seeds is None else torch.from_numpy(np.asarray(seeds, np.uint32).view(np.int32)).to(dev)
@@ -224,3 +233,26 @@ def test_read_probe(dev):
     sink = batch.read_probe(buf, buf.numel())
     torch.cuda.synchronize()
     assert int(sink.sum()) > 0
+
+
+def test_zipf_large_spans_odd_offsets(dev):
+    """cfg 3 shape at scale: 200k Zipf(1.2) lengths 64..9000 packed with odd
+    gaps (the A/B tool's batch), with seeds, every packet vs the oracle."""
+    lens = synth.zipf_lengths(200_000, seed=3)
+    off, total = synth.pack(lens, seed=4, max_gap=3)
+    buf = np.random.default_rng(5).integers(0, 256, size=total, dtype=np.uint8)
+    seeds = np.random.default_rng(6).integers(0, 65536, size=lens.size).astype(np.uint32)
+    got = _spans(dev, buf, off, lens)
+    want = oracle.batch_spans(buf, off, lens, nthreads=8)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first (idx, len, off): " + str(
+        [(int(i), int(lens[i]), int(off[i])) for i in bad[:5]])
+    got = _spans(dev, buf, off, lens, seeds)
+    assert np.array_equal(got, oracle.batch_spans(buf, off, lens, seeds, nthreads=8))
+
+
+def test_zipf_large_frames(dev):
+    buf, off, lens, _ = synth.mixed_udp_frames(20_000, seed=12, max_gap=3)
+    got, st = _frames(dev, buf, off, lens)
+    want, want_st = oracle.batch_ipv4(buf, off, lens, nthreads=8)
+    assert np.array_equal(got, want) and np.array_equal(st, want_st)

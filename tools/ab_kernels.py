@@ -1,0 +1,91 @@
+"""In-process interleaved A/B of kernel variants (sccsum_set_kernel_variant)
+on the bench workload and on mixed / long packets.  Prints one JSON line per
+(case, variant) with median and min launch time and GB/s (algorithmic bytes).
+
+usage: python tools/ab_kernels.py [--rounds 10] [--variants 1,2]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from seastar_amd import batch, devsynth, native, synth  # noqa: E402
+
+
+def cases(dev):
+    n = 1 << 20
+    tx = devsynth.udp_frames(n, 1500, seed=1, device=dev)
+    yield "udp1500_frames", tx, "frames", n * (1500 + 12 + 4)
+    yield "udp1500_spans", tx, "spans", n * (1500 + 12 + 2)
+    lens = synth.zipf_lengths(200_000, seed=3)
+    off, total = synth.pack(lens, seed=4, max_gap=3)
+    buf = np.random.default_rng(5).integers(0, 256, size=total, dtype=np.uint8)
+    mb = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+    yield "zipf_spans", mb, "spans", int(lens.sum()) + lens.size * 14
+    n64 = 16384
+    seg = torch.randint(0, 256, (n64 * 65536,), dtype=torch.uint8, device=dev)
+    lb = batch.PacketBatch(data=seg, off=torch.arange(n64, device=dev, dtype=torch.int64) * 65536,
+                           length=torch.full((n64,), 65536, dtype=torch.int32, device=dev),
+                           bytes_len=n64 * 65536, max_len=65536)
+    yield "tcp64k_spans", lb, "spans", n64 * (65536 + 14)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--variants", default="1,2,3", help="comma list of variant[:blocks_per_cu]")
+    args = ap.parse_args()
+    variants = args.variants.split(",")
+    lib = native.load()
+    native.check(lib.sccsum_init(0), "init")
+    dev = torch.device("cuda:0")
+    for name, b, mode, alg in cases(dev):
+        outs = {}
+        times = {v: [] for v in variants}
+
+        def run(v):
+            var, _, bpc = v.partition(":")
+            native.check(lib.sccsum_set_kernel_variant(int(var)), "variant")
+            native.check(lib.sccsum_set_blocks_per_cu(int(bpc or 8)), "blocks_per_cu")
+            if mode == "frames":
+                return batch.ipv4_frames(b)
+            return batch.spans(b)
+
+        for v in variants:
+            outs[v] = run(v).clone()
+        torch.cuda.synchronize()
+        ref = outs[variants[0]]
+        for v in variants[1:]:
+            assert torch.equal(outs[v], ref), f"{name}: variant {v} differs from {variants[0]}"
+        for _ in range(args.rounds):
+            for v in variants:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                run(v)
+                e0.record()
+                for _ in range(args.reps):
+                    run(v)
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) / args.reps)
+        for v in variants:
+            t = np.array(times[v])
+            print(json.dumps({"case": name, "variant": v, "median_us": round(float(np.median(t)) * 1e3, 1),
+                              "min_us": round(float(t.min()) * 1e3, 1),
+                              "GBps_median": round(alg / (np.median(t) / 1e3) / 1e9, 1)}), flush=True)
+        del b
+        torch.cuda.empty_cache()
+    native.check(lib.sccsum_set_kernel_variant(0), "variant")
+    native.check(lib.sccsum_set_blocks_per_cu(8), "blocks_per_cu")
+
+
+if __name__ == "__main__":
+    main()
