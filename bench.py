@@ -98,7 +98,7 @@ def cpu_baseline(tx, budget_s: float):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # cpu_baseline leg only
 
-    n_sample = min(65536, tx.n)
+    n_sample = min(262144, tx.n)  # 393 MB: larger than the host L3, like the real stream
     host = tx.data[: n_sample * FRAME].cpu().numpy()
     off = np.arange(n_sample, dtype=np.uint64) * FRAME
     length = np.full(n_sample, FRAME, dtype=np.uint32)
