@@ -1,0 +1,90 @@
+// seastar/net/ip_checksum_batch.hh — C++ batch interface to the MI355X
+// checksum engine (libsccsum, C-ABI in <sccsum.h>), in Seastar's vocabulary.
+//
+// The per-packet API (<seastar/net/ip_checksum.hh>) stays synchronous and on
+// the reactor thread.  This header is what a shard uses to hand a burst of
+// packets to its GPU: one launch checksums every packet of the burst.
+//
+//   per-packet reference call                          batch equivalent
+//   ------------------------------------------------   --------------------------------
+//   ip_checksum(data, len)           ip_checksum.cc:70-74     sum_spans(batch, nullptr, ...)
+//   checksummer + *_pseudo_header_checksum + sum + get        sum_spans(batch, seeds, ...)
+//       udp.cc:184-195, tcp.hh:1656-1694, tcp.hh:1004-1016
+//   ip.cc:121-127 (IPv4 verify) + tcp.hh:876-883 (TCP verify) ipv4_frames(batch, ...)
+//   ip.cc:271-277 (IPv4 generate) + udp/tcp generate          ipv4_frames(batch, ...) on zeroed fields
+//
+// Results are network-order uint16 values, exactly what checksummer::get()
+// returns; a verify passes when the value is 0.  Errors throw
+// std::runtime_error (the C-ABI underneath never throws).
+#pragma once
+
+#include <sccsum.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace seastar {
+
+namespace net {
+
+// Packets resident in device memory: one byte buffer plus offset/length
+// arrays (see <sccsum.h> "Memory contract").
+struct device_packet_batch {
+    const void* bytes = nullptr;   // 16-byte aligned device pointer
+    uint64_t bytes_len = 0;        // valid bytes at `bytes`
+    const uint64_t* off = nullptr; // device, n entries
+    const uint32_t* len = nullptr; // device, n entries
+    uint64_t n = 0;
+    uint32_t max_len = 0;          // upper bound of len[] (0 = unknown); tunes the launch only
+};
+
+enum class checksum_status : uint8_t {
+    ok = SCCSUM_ST_OK,               // spans: result 0; frames: IPv4 header verifies
+    l4_ok = SCCSUM_ST_L4_OK,         // frames: TCP/UDP checksum verifies
+    malformed = SCCSUM_ST_MALFORMED, // frames: shorter than 20 B / than the IP length, bad ihl
+    out_of_range = SCCSUM_ST_RANGE,  // span outside the byte buffer (not read)
+};
+
+class batch_checksummer {
+    int _device;
+
+    static void check(int rc, const char* what) {
+        if (rc != SCCSUM_OK) {
+            throw std::runtime_error(std::string(what) + ": " + sccsum_strerror(rc));
+        }
+    }
+
+public:
+    // Binds the calling thread (the shard's reactor thread) to `device`.
+    explicit batch_checksummer(int device) : _device(device) { check(sccsum_init(device), "sccsum_init"); }
+
+    int device() const noexcept { return _device; }
+
+    // The pseudo-header partial sum ipv4_traits::{tcp,udp}_pseudo_header_checksum
+    // leaves in a fresh checksummer (ip.hh:70-75); host-order addresses, len
+    // truncated to 16 bits exactly like the reference's uint16_t parameter.
+    static uint32_t pseudo_header_seed(uint32_t src_host, uint32_t dst_host, uint8_t proto, uint16_t len) noexcept {
+        return sccsum_pseudo_seed(src_host, dst_host, proto, len);
+    }
+
+    // out[i] = checksum of span i, seeded with seeds[i] when seeds != nullptr.
+    void sum_spans(const device_packet_batch& b, const uint32_t* d_seeds, uint16_t* d_out, uint8_t* d_status,
+                   void* stream) const {
+        check(sccsum_spans(b.bytes, b.bytes_len, b.off, b.len, d_seeds, d_out, d_status, b.n, b.max_len, stream),
+              "sccsum_spans");
+    }
+
+    // out2[2i] = IPv4 header checksum, out2[2i+1] = TCP/UDP checksum of frame i.
+    void ipv4_frames(const device_packet_batch& b, uint16_t* d_out2, uint8_t* d_status, void* stream) const {
+        check(sccsum_ipv4_frames(b.bytes, b.bytes_len, b.off, b.len, d_out2, d_status, b.n, b.max_len, stream),
+              "sccsum_ipv4_frames");
+    }
+
+    void sync(void* stream) const { check(sccsum_sync(stream), "sccsum_sync"); }
+};
+
+}  // namespace net
+
+}  // namespace seastar
