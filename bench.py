@@ -46,22 +46,31 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc", default=None, help="PMC summary JSON for roofline.traffic (default: newest in profiles/)")
+    ap.add_argument("--config", default="udp1500", choices=["udp1500", "mixed", "tcp64k", "e2e"],
+                    help="udp1500 = the metric's config (cfg 2, default); mixed = cfg 3; tcp64k = cfg 4 "
+                         "(per-GPU shard); e2e = cfg 5 (pinned host mbufs, PCIe-inclusive)")
     return ap.parse_args()
+
+
+BACKEND = os.environ.get("SCCSUM_DIST_BACKEND", "nccl")  # gloo: rehearse N ranks on fewer GPUs
 
 
 def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    dev = local % max(ndev, 1)
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    native.check(native.load().sccsum_init(local), "sccsum_init")
-    return world, rank, local
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(BACKEND)
+    native.check(native.load().sccsum_init(dev), "sccsum_init")
+    return world, rank, dev
 
 
 def barrier(world):
@@ -76,7 +85,7 @@ def max_over_ranks(x: float, world: int) -> float:
         return x
     import torch.distributed as dist
 
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if BACKEND == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -147,10 +156,142 @@ def pmc_traffic(path: str | None, kernel_substr: str):
     return None, None
 
 
+def timed(step, steps, warmup, world, stream):
+    """Warm up, then time `steps` calls bracketed by barrier + sync; returns
+    (max-over-ranks wall seconds, mean seconds per launch from HIP events)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e in evs:
+        e[0].record(stream)
+        step()
+        e[1].record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    return wall, float(np.mean([a.elapsed_time(b) for a, b in evs])) / 1e3
+
+
+def line(metric, value, unit, args, world, wall, dtype, config, roofline=None, cpu=None, extra=None):
+    d = {"metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": world, "steps": args.steps,
+         "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+         "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic", "config": config,
+         "roofline": roofline, "cpu_baseline": cpu}
+    if extra:
+        d.update(extra)
+    print(json.dumps(d), flush=True)
+
+
+def run_tcp64k(args, world, rank, dev):
+    """cfg 4: 64 KiB TCP segments with pseudo-header seeds (len 65536 wraps to
+    0, tcp.hh:878), this rank's independent shard of the 16 M-segment job."""
+    n = args.packets if args.packets != (1 << 20) else 2 * 1024 * 1024  # 16 M / 8 GPUs per rank
+    seg = 65536
+    b, seeds = devsynth.tcp_segments(n, seg, seed=SEED + 104729 * rank, device=dev)
+    out = torch.empty(n, dtype=torch.int16, device=dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    batch.spans(b, seeds=seeds, out=out)  # generate
+    devsynth.store_tcp_checksums(b, out)
+    batch.spans(b, seeds=seeds, out=out, status=st)  # verify: every segment must pass
+    torch.cuda.synchronize()
+    assert int((st != 1).sum()) == 0, "tcp64k verify failed"
+    stream = torch.cuda.current_stream()
+    wall, launch_s = timed(lambda: batch.spans(b, seeds=seeds, out=out, status=st, stream=stream),
+                           args.steps, args.warmup, world, stream)
+    alg = n * (seg + 12 + 4 + 2 + 1)
+    if rank == 0:
+        line("GiB/s device-resident Internet checksum, 64 KiB TCP segments (cfg 4)",
+             world * n * seg * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
+             {"workload": "cfg4: 65536 B TCP segments + pseudo-header seed per segment, verify pass",
+              "segments_per_gpu": n, "segment_bytes": seg, "parallelism": f"{world} independent shards"},
+             {"bound": "hbm", "achieved": round(alg / launch_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+              "frac": round(alg / launch_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+              "avg_launch_us": round(launch_s * 1e6, 2)})
+
+
+def run_mixed(args, world, rank, dev):
+    """cfg 3: Zipf(1.2) frame lengths 64..9000 B, contiguous packing (odd
+    offsets), ~1.5 GB per GPU, IPv4 + UDP checksums per frame."""
+    from seastar_amd import synth
+
+    n = args.packets if args.packets != (1 << 20) else 3_400_000
+    lens = synth.zipf_lengths(n, seed=SEED + rank)
+    b = devsynth.mixed_frames(lens, seed=SEED + 31 * rank, device=dev)
+    out = torch.empty(2 * n, dtype=torch.int16, device=dev)
+    stream = torch.cuda.current_stream()
+    wall, launch_s = timed(lambda: batch.ipv4_frames(b, out2=out, stream=stream), args.steps, args.warmup, world,
+                           stream)
+    total = int(lens.sum())
+    alg = total + n * (12 + 4)
+    if rank == 0:
+        line("GiB/s device-resident Internet checksum, mixed-MTU Zipf batches (cfg 3)",
+             world * total * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
+             {"workload": "cfg3: Zipf(s=1.2) IPv4/UDP frames 64..9000 B, packed back to back (odd offsets)",
+              "packets_per_gpu": n, "bytes_per_gpu": total, "mean_len": round(total / n, 1),
+              "parallelism": f"{world} independent shards"},
+             {"bound": "hbm", "achieved": round(alg / launch_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+              "frac": round(alg / launch_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+              "avg_launch_us": round(launch_s * 1e6, 2)})
+
+
+def run_e2e(args, world, rank, dev):
+    """cfg 5: frames in a pinned, DPDK-mbuf-shaped host pool (2304-B slots,
+    data at +256); chunks H2D on a copy stream, kernel on a compute stream,
+    results D2H, 3 chunks in flight.  A = slots copied as they lie; B =
+    packets gathered into pinned staging first (only packet bytes cross PCIe)."""
+    from seastar_amd import pipeline
+
+    n = args.packets
+    tx = devsynth.udp_frames(n, FRAME, seed=SEED + rank, device=dev)
+    want = batch.ipv4_frames(tx).cpu().numpy().view(np.uint16).reshape(n, 2)
+    pool = pipeline.pinned_empty(n * pipeline.MBUF_SLOT)
+    pv = pool.reshape(n, pipeline.MBUF_SLOT)
+    pv[:, :pipeline.MBUF_DATA_OFF] = 0
+    pv[:, pipeline.MBUF_DATA_OFF:pipeline.MBUF_DATA_OFF + FRAME] = tx.data[: n * FRAME].view(n, FRAME).cpu().numpy()
+    off = np.arange(n, dtype=np.uint64) * pipeline.MBUF_SLOT + pipeline.MBUF_DATA_OFF
+    length = np.full(n, FRAME, dtype=np.uint32)
+    del tx
+    torch.cuda.empty_cache()
+    res = {}
+    for name, gather, chunk_bytes in (("A_slots_as_is", False, 65536 * pipeline.MBUF_SLOT),
+                                      ("B_gathered", True, 65536 * FRAME)):
+        pl = pipeline.HostPipeline(dev.index or 0, chunk_bytes=chunk_bytes, chunk_packets=65536, depth=3)
+        got = pl.run(native.PIPE_IPV4, pool, off, length, gather=gather, max_len=FRAME)
+        assert np.array_equal(got, want), f"e2e {name} mismatch vs device-resident results"
+        times = []
+        for _ in range(max(1, args.steps // 4)):
+            t0 = time.perf_counter()
+            pl.run(native.PIPE_IPV4, pool, off, length, gather=gather, max_len=FRAME)
+            times.append(time.perf_counter() - t0)
+        pl.close()
+        t = float(np.median(times))
+        pcie = n * (pipeline.MBUF_SLOT if not gather else FRAME) + n * (12 + 4)
+        res[name] = {"GiBps_packet_bytes": round(n * FRAME / t / 2**30, 2), "ms_per_batch": round(t * 1e3, 2),
+                     "pcie_GBps_h2d_plus_d2h": round(pcie / t / 1e9, 2)}
+    if rank == 0:
+        best = max(res.values(), key=lambda r: r["GiBps_packet_bytes"])
+        line("GiB/s Internet checksum incl. PCIe: pinned mbuf-shaped host buffers -> HBM -> host (cfg 5)",
+             world * best["GiBps_packet_bytes"], "GiB/s", args, world, best["ms_per_batch"] / 1e3 * args.steps, "u8",
+             {"workload": "cfg5: 1,048,576 x 1500 B IPv4/UDP frames in 2304-B mbuf slots (pinned), "
+                          "H2D + kernel + D2H of 4 B/frame, 3-deep pipeline, 64Ki-frame chunks",
+              "parallelism": f"{world} independent shards"}, extra={"variants": res})
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup()
     dev = torch.device("cuda", local)
+    if args.config != "udp1500":
+        {"tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e}[args.config](args, world, rank, dev)
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.destroy_process_group()
+        return
     n = args.packets
 
     tx = devsynth.udp_frames(n, FRAME, seed=SEED + 7919 * rank, device=dev)

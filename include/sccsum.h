@@ -134,6 +134,41 @@ int sccsum_sync(void* stream);
 int sccsum_read_probe(const void* d_src, uint64_t bytes, uint64_t* d_sink, void* stream);
 int sccsum_read_probe_blocks(void);
 
+/* ---------------------------------------------------------------------------
+ * Host pipeline: batches that live in HOST memory (DPDK mbuf pools, socket
+ * buffers).  The batch is cut into chunks of at most chunk_packets packets /
+ * chunk_bytes bytes; each chunk is copied to HBM on a copy stream
+ * (hipMemcpyAsync, pinned staging), checksummed on a compute stream and its
+ * results copied back, with `depth` chunks in flight so the copies overlap
+ * the kernels.  The device work is the same sccsum_spans / sccsum_ipv4_frames.
+ * ------------------------------------------------------------------------- */
+typedef struct sccsum_pipeline sccsum_pipeline;
+
+#define SCCSUM_PIPE_SPANS 0
+#define SCCSUM_PIPE_IPV4  1
+
+/* Allocate device buffers and pinned staging for `depth` chunks on `device`. */
+int sccsum_pipeline_create(int device, uint64_t chunk_bytes, uint32_t chunk_packets, int depth,
+                           sccsum_pipeline** out);
+
+/* Checksum n packets at host_bytes[host_off[i] .. +host_len[i]) (all HOST
+ * pointers; host_bytes should be pinned — sccsum_host_alloc — when gather is
+ * 0).  gather = 0: each chunk's covering byte range is copied as it lies
+ * (e.g. whole mbuf slots, headers and headroom included); gather = 1: the
+ * packets are first packed into pinned staging on the host (only packet bytes
+ * cross PCIe).  mode = SCCSUM_PIPE_SPANS (host_seed optional, host_out[n]) or
+ * SCCSUM_PIPE_IPV4 (host_out[2n]); host_status optional.  Returns when all
+ * results are in host_out.  host_len is the size of the host_bytes area. */
+int sccsum_pipeline_run(sccsum_pipeline* p, int mode, int gather, const void* host_bytes, uint64_t host_len,
+                        const uint64_t* host_off, const uint32_t* host_lens, const uint32_t* host_seed,
+                        uint64_t n, uint32_t max_len, uint16_t* host_out, uint8_t* host_status);
+
+int sccsum_pipeline_destroy(sccsum_pipeline* p);
+
+/* Pinned (page-locked) host memory for packet pools. */
+int sccsum_host_alloc(void** p, uint64_t bytes);
+int sccsum_host_free(void* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,6 +9,7 @@ from .native import LIB_PATH, PKG_DIR, REPO_DIR
 SOURCES = [
     os.path.join(PKG_DIR, "csrc", "sccsum.hip"),
     os.path.join(PKG_DIR, "csrc", "checksummer.cc"),
+    os.path.join(PKG_DIR, "csrc", "pipeline.cc"),
 ]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 

@@ -15,6 +15,16 @@ def _round16(n: int) -> int:
     return (n + 15) & ~15
 
 
+def random_bytes(nbytes: int, g: torch.Generator, device, chunk: int = 1 << 30) -> torch.Tensor:
+    """nbytes random bytes in HBM, generated in 1 GiB pieces (torch's RNG
+    kernels are happiest below 2^31 elements)."""
+    data = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    for s in range(0, nbytes, chunk):
+        e = min(nbytes, s + chunk)
+        data[s:e].random_(0, 256, generator=g)
+    return data
+
+
 def _be16(x: torch.Tensor) -> torch.Tensor:
     return torch.stack([(x >> 8) & 0xFF, x & 0xFF], dim=1).to(torch.uint8)
 
@@ -69,3 +79,69 @@ def corrupt(b: PacketBatch, idx: torch.Tensor, byte: int) -> None:
     """Flip bits of payload byte `byte` in frames idx (in place)."""
     f = _frame_view(b)
     f[idx, byte] ^= 0x5A
+
+
+def tcp_segments(n: int, seg_len: int, seed: int, device):
+    """n TCP segments (20 B header, checksum 0, payload random) back to back;
+    returns (batch, seeds): seeds = pseudo-header partial sums exactly as
+    tcp_pseudo_header_checksum leaves them (ip.hh:70-75, len as uint16_t),
+    folded to 16 bits."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    total = n * seg_len
+    data = random_bytes(_round16(total), g, device)
+    f = data[:total].view(n, seg_len)
+    f[:, 12] = (20 // 4) << 4
+    f[:, 13] = 0x10
+    f[:, 16:18] = 0
+    src = torch.randint(1, 2**31, (n,), dtype=torch.int64, device=device, generator=g)
+    dst = torch.randint(1, 2**31, (n,), dtype=torch.int64, device=device, generator=g)
+    s = src + dst + 6 + (seg_len & 0xFFFF)
+    for _ in range(3):
+        s = (s & 0xFFFF) + (s >> 16)
+    off = torch.arange(n, dtype=torch.int64, device=device) * seg_len
+    length = torch.full((n,), seg_len, dtype=torch.int32, device=device)
+    b = PacketBatch(data=data, off=off, length=length, bytes_len=total, max_len=seg_len)
+    return b, s.to(torch.int32)
+
+
+def store_tcp_checksums(b: PacketBatch, out: torch.Tensor) -> None:
+    """tcp_hdr::write_nbo_checksum (tcp.hh:283-285) for every segment, in place."""
+    f = _frame_view(b)
+    f[:, 16:18] = out.contiguous().view(torch.uint8).view(b.n, 2)
+
+
+def mixed_frames(lengths, seed: int, device) -> PacketBatch:
+    """IPv4/UDP frames of the given lengths packed back to back (odd offsets
+    included), built in HBM: random payload, headers per ip.cc:249-269."""
+    import numpy as np
+
+    lengths = np.asarray(lengths, dtype=np.int64)
+    n = lengths.size
+    off = np.concatenate([[0], np.cumsum(lengths)[:-1]])
+    total = int(lengths.sum())
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    data = torch.randint(0, 256, (_round16(total),), dtype=torch.uint8, device=device, generator=g)
+    o = torch.from_numpy(off).to(device)
+    L = torch.from_numpy(lengths).to(device)
+
+    def put(k: int, vals):
+        data[o + k] = vals.to(torch.uint8) if torch.is_tensor(vals) else torch.full_like(o, vals, dtype=torch.uint8)
+
+    src = torch.randint(1, 2**31, (n,), dtype=torch.int64, device=device, generator=g)
+    dst = torch.randint(1, 2**31, (n,), dtype=torch.int64, device=device, generator=g)
+    put(0, 0x45)
+    put(1, 0)
+    put(2, (L >> 8) & 0xFF)
+    put(3, L & 0xFF)
+    for k in (4, 5, 6, 7, 10, 11, 26, 27):
+        put(k, 0)
+    put(8, 64)
+    put(9, 17)
+    for i in range(4):
+        put(12 + i, (src >> (24 - 8 * i)) & 0xFF)
+        put(16 + i, (dst >> (24 - 8 * i)) & 0xFF)
+    put(24, ((L - 20) >> 8) & 0xFF)
+    put(25, (L - 20) & 0xFF)
+    return PacketBatch(data=data, off=o, length=L.to(torch.int32), bytes_len=total, max_len=int(lengths.max()))

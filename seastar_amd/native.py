@@ -55,7 +55,15 @@ _PROTOS = {
     "sccsum_set_blocks_per_cu": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_read_probe": (ctypes.c_int, [_vp, _u64, _vp, _vp]),
     "sccsum_read_probe_blocks": (ctypes.c_int, []),
+    "sccsum_pipeline_create": (ctypes.c_int, [ctypes.c_int, _u64, _u32, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "sccsum_pipeline_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, _u64, _vp, _vp, _vp, _u64, _u32,
+                                           _vp, _vp]),
+    "sccsum_pipeline_destroy": (ctypes.c_int, [_vp]),
+    "sccsum_host_alloc": (ctypes.c_int, [ctypes.POINTER(_vp), _u64]),
+    "sccsum_host_free": (ctypes.c_int, [_vp]),
 }
+PIPE_SPANS = 0
+PIPE_IPV4 = 1
 
 
 def header_symbols() -> list[str]:

@@ -1,0 +1,75 @@
+"""Host-memory batches through the GPU (sccsum_pipeline_* in include/sccsum.h):
+the end-to-end path of BASELINE cfg 5 — DPDK-mbuf-shaped pinned host buffers,
+hipMemcpyAsync in and out on side streams, overlapped with the kernels."""
+from __future__ import annotations
+
+import ctypes
+import weakref
+
+import numpy as np
+
+from . import native
+
+MBUF_SLOT = 128 + 128 + 2048  # rte_mbuf + headroom + data room (src/net/dpdk.cc:139-156)
+MBUF_DATA_OFF = 256
+
+
+def pinned_empty(nbytes: int) -> np.ndarray:
+    """uint8 array in page-locked host memory (freed with the array)."""
+    lib = native.load()
+    p = ctypes.c_void_p()
+    native.check(lib.sccsum_host_alloc(ctypes.byref(p), max(int(nbytes), 1)), "sccsum_host_alloc")
+    arr = np.ctypeslib.as_array((ctypes.c_uint8 * max(int(nbytes), 1)).from_address(p.value))[: int(nbytes)]
+    weakref.finalize(arr, lib.sccsum_host_free, p.value)
+    return arr
+
+
+def mbuf_pool(frames: np.ndarray, lengths: np.ndarray, offsets: np.ndarray):
+    """Place each packet in its own mbuf-shaped slot of a pinned pool: packet i
+    at slot i + 256 (after the rte_mbuf header and headroom).  Returns
+    (pool, off, len)."""
+    n = lengths.size
+    pool = pinned_empty(n * MBUF_SLOT)
+    pool[:] = 0
+    off = np.arange(n, dtype=np.uint64) * MBUF_SLOT + MBUF_DATA_OFF
+    for i in range(n):
+        L = int(lengths[i])
+        o = int(offsets[i])
+        pool[int(off[i]):int(off[i]) + L] = frames[o:o + L]
+    return pool, off, lengths.astype(np.uint32)
+
+
+class HostPipeline:
+    def __init__(self, device: int = 0, chunk_bytes: int = 64 << 20, chunk_packets: int = 1 << 16, depth: int = 3):
+        self._lib = native.load()
+        h = ctypes.c_void_p()
+        native.check(self._lib.sccsum_pipeline_create(device, chunk_bytes, chunk_packets, depth, ctypes.byref(h)),
+                     "sccsum_pipeline_create")
+        self._h = h
+
+    def run(self, mode: int, buf: np.ndarray, off: np.ndarray, length: np.ndarray, seeds: np.ndarray | None = None,
+            status: bool = False, gather: bool = False, max_len: int = 0):
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        n = off.size
+        width = 2 if mode == native.PIPE_IPV4 else 1
+        out = np.empty((n, width) if width == 2 else n, dtype=np.uint16)
+        st = np.empty(n, dtype=np.uint8) if status else None
+        sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+        code = self._lib.sccsum_pipeline_run(
+            self._h, mode, int(gather), buf.ctypes.data if buf.size else None, buf.size, off.ctypes.data,
+            length.ctypes.data, None if sd is None else sd.ctypes.data, n, max_len,
+            out.ctypes.data, None if st is None else st.ctypes.data)
+        native.check(code, "sccsum_pipeline_run")
+        return (out, st) if status else out
+
+    def close(self):
+        if self._h:
+            self._lib.sccsum_pipeline_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

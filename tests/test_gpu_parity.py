@@ -256,3 +256,23 @@ def test_zipf_large_frames(dev):
     got, st = _frames(dev, buf, off, lens)
     want, want_st = oracle.batch_ipv4(buf, off, lens, nthreads=8)
     assert np.array_equal(got, want) and np.array_equal(st, want_st)
+
+
+@pytest.mark.parametrize("gather", [False, True])
+def test_host_pipeline_mbuf_pool(dev, gather, kernel_variant):
+    """cfg 5 path: frames in an mbuf-shaped pinned pool, chunked through the
+    GPU with async copies; small chunks force many stage recycles."""
+    if kernel_variant != 1 and kernel_variant != 6:
+        pytest.skip("pipeline exercised with two kernel families")
+    from seastar_amd import pipeline
+
+    buf, off, lens, _ = synth.mixed_udp_frames(2500, seed=31, max_gap=5)
+    pool, poff, plen = pipeline.mbuf_pool(buf, lens, off)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
+    pl = pipeline.HostPipeline(0, chunk_bytes=1 << 20, chunk_packets=300, depth=3)
+    got, st = pl.run(native.PIPE_IPV4, pool, poff, plen, status=True, gather=gather, max_len=9000)
+    assert np.array_equal(got, want) and np.array_equal(st, want_st)
+    seeds = np.random.default_rng(2).integers(0, 65536, lens.size).astype(np.uint32)
+    got2 = pl.run(native.PIPE_SPANS, pool, poff, plen, seeds=seeds, gather=gather)
+    assert np.array_equal(got2, oracle.batch_spans(pool, poff, plen, seeds))
+    pl.close()
