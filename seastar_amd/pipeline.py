@@ -29,6 +29,8 @@ def mbuf_pool(frames: np.ndarray, lengths: np.ndarray, offsets: np.ndarray):
     at slot i + 256 (after the rte_mbuf header and headroom).  Returns
     (pool, off, len)."""
     n = lengths.size
+    if n and int(np.max(lengths)) > MBUF_SLOT - MBUF_DATA_OFF:
+        raise ValueError("a packet longer than one mbuf data room (2048 B) needs a segment chain")
     pool = pinned_empty(n * MBUF_SLOT)
     pool[:] = 0
     off = np.arange(n, dtype=np.uint64) * MBUF_SLOT + MBUF_DATA_OFF
