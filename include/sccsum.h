@@ -110,7 +110,7 @@ int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len,
                        void* stream);
 
 /* Diagnostic: select the kernel family for later launches in this process
- * (0 = default (6 up to 2 KiB packets, else 2), 1 = one-packet-per-wave
+ * (0 = default (6 when max_len <= 2048, else 2), 1 = one-packet-per-wave
  * loop, 2 = batch kernel, 3 = batch
  * kernel with the next packet in flight, 4 / 5 = 2 / 3 with default cache
  * policy instead of nontemporal loads, 6 / 7 = 2 / 3 with each packet's last
@@ -123,6 +123,10 @@ int sccsum_set_kernel_variant(int variant);
  * compute unit (default 8 = 32 waves/CU).  Occupancy A/B knob; results are
  * unaffected.  Returns SCCSUM_EINVAL outside 1..32. */
 int sccsum_set_blocks_per_cu(int blocks);
+
+/* Diagnostic: force U, the 16-byte units each lane loads per step of a packet
+ * (1, 2, 4 or 8; 0 = choose from max_len).  Results are unaffected. */
+int sccsum_set_group_units(int units);
 
 /* Wait for all work queued on `stream`. */
 int sccsum_sync(void* stream);

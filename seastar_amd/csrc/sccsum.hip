@@ -293,6 +293,10 @@ __device__ __forceinline__ uint32_t unit_part(const u32x4& v, int lo, int hi) {
 constexpr uint32_t kStashUnits = 4;     // units 0..2 of a packet (IPv4 header) + its last unit
 constexpr uint32_t kStashStride = 80;   // bytes per packet row (5 x 16 B: conflict-free ds_read_b128)
 constexpr uint32_t kExactMax = 131072;  // fast path keeps exact 32-bit sums up to this length
+#ifndef SCCSUM_LONG_GROUPS
+#define SCCSUM_LONG_GROUPS 3
+#endif
+constexpr int kLongGroups = SCCSUM_LONG_GROUPS;  // groups in flight per step of a long packet
 static_assert(kStashStride >= 16 * kStashUnits && kStashStride % 16 == 0, "stash row layout");
 
 // Exact folded sum (little-endian domain relative to a0) of [rs, re), one
@@ -402,7 +406,24 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(
             if (lane < kHead && lane < P.s) *reinterpret_cast<u32x4*>(row + 16u * lane) = P.v[0];
             if (HYB && lane + P.s < kHead) *reinterpret_cast<u32x4*>(row + 16u * (lane + P.s)) = P.w;
             const uint32_t gu = static_cast<uint32_t>(U) * kWave;
-            for (uint32_t g = gu; g < P.s; g += gu) {
+            uint32_t g = gu;
+            // long packets: kLongGroups groups of loads in flight per step;
+            // the final group always goes through the single-group loop below
+            // so P.v ends up holding it (tail stash)
+            for (; g + kLongGroups * gu < P.s; g += kLongGroups * gu) {
+                u32x4 w[kLongGroups][U];
+#pragma unroll
+                for (int q = 0; q < kLongGroups; ++q)
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        w[q][u] = __builtin_amdgcn_raw_buffer_load_b128(
+                            P.r, static_cast<int>(16u * (g + q * gu) + vo + 1024u * u), 0, AUX);
+#pragma unroll
+                for (int q = 0; q < kLongGroups; ++q)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) acc = sad4(w[q][u], acc);
+            }
+            for (; g < P.s; g += gu) {
                 u32x4 w[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u)
@@ -609,7 +630,11 @@ unsigned grid_for(uint64_t n) {
     return static_cast<unsigned>(want);
 }
 
+std::atomic<int> g_group_units{0};  // diagnostic override of U (0 = by max_len)
+
 int units_class(uint32_t max_len) {
+    const int forced = g_group_units.load(std::memory_order_relaxed);
+    if (forced) return forced;
     if (max_len == 0) return 4;
     const uint64_t units = (static_cast<uint64_t>(max_len) + 30) / 16;  // worst-case head of 15
     if (units <= 64) return 1;
@@ -618,7 +643,9 @@ int units_class(uint32_t max_len) {
     return 8;
 }
 
-// Kernel variant: 0 = default (batch kernel: 6 for packets up to 2 KiB, else 2),
+// Kernel variant: 0 = default (batch kernel: 6 when max_len <= 2 KiB, else 2;
+// measured: the hybrid policy pays for packed MTU-size frames, all-nontemporal
+// for mixed and long packets; cross-packet prefetch (3, 5, 7) only adds issue work),
 // 1 = simple one-packet-per-wave loop (independent second implementation),
 // 2 = batch kernel, 3 = batch kernel with the next packet in flight (both
 // with nontemporal loads), 4 / 5 = 2 / 3 with default-policy loads,
@@ -639,11 +666,7 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     B = B < 1 ? 1 : (B > kWave ? kWave : B);
     const dim3 grid(grid_for((n + B - 1) / B));
     const uint32_t b32 = static_cast<uint32_t>(B);
-    // default: up to 2 KiB packets -> hybrid policy (last line cached for the
-    // neighbour), longer ones -> all nontemporal; no cross-packet prefetch
-    // (measured: it only adds issue work).
-    const int v = variant != 0 ? variant : (U <= 2 ? 6 : 2);
-    switch (v) {
+    switch (variant) {
         case 6:
             csum_batch_kernel<U, IPV4, false, kNT, true>
                 <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
@@ -682,10 +705,15 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
         (reinterpret_cast<uintptr_t>(d_out) & (IPV4 ? 3u : 1u))) {
         return SCCSUM_EINVAL;
     }
-    const int variant = g_variant.load(std::memory_order_relaxed);
+    int variant = g_variant.load(std::memory_order_relaxed);
+    if (variant == 0) variant = (max_len != 0 && max_len <= 2048) ? 6 : 2;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
-    switch (units_class(max_len)) {
+    // batch kernel: U = 2 for every size (long packets keep 4 groups in flight
+    // in their loop); the simple kernel sizes U by max_len.
+    const int forced = g_group_units.load(std::memory_order_relaxed);
+    const int uc = variant == 1 ? units_class(max_len) : (forced ? forced : 2);
+    switch (uc) {
         case 1:
             launch_u<1, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
             break;
@@ -762,6 +790,12 @@ int sccsum_set_kernel_variant(int variant) {
 int sccsum_set_blocks_per_cu(int blocks) {
     if (blocks < 1 || blocks > 32) return SCCSUM_EINVAL;
     sccsum::g_blocks_per_cu.store(blocks, std::memory_order_relaxed);
+    return SCCSUM_OK;
+}
+
+int sccsum_set_group_units(int units) {
+    if (units != 0 && units != 1 && units != 2 && units != 4 && units != 8) return SCCSUM_EINVAL;
+    sccsum::g_group_units.store(units, std::memory_order_relaxed);
     return SCCSUM_OK;
 }
 

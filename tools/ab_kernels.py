@@ -42,20 +42,25 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="1,2,3", help="comma list of variant[:blocks_per_cu]")
+    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U]]")
+    ap.add_argument("--cases", default="udp1500_frames,udp1500_spans,zipf_spans,tcp64k_spans")
     args = ap.parse_args()
     variants = args.variants.split(",")
     lib = native.load()
     native.check(lib.sccsum_init(0), "init")
     dev = torch.device("cuda:0")
+    wanted = set(args.cases.split(","))
     for name, b, mode, alg in cases(dev):
+        if name not in wanted:
+            continue
         outs = {}
         times = {v: [] for v in variants}
 
         def run(v):
-            var, _, bpc = v.partition(":")
-            native.check(lib.sccsum_set_kernel_variant(int(var)), "variant")
-            native.check(lib.sccsum_set_blocks_per_cu(int(bpc or 8)), "blocks_per_cu")
+            parts = (v.split(":") + ["", ""])[:3]
+            native.check(lib.sccsum_set_kernel_variant(int(parts[0])), "variant")
+            native.check(lib.sccsum_set_blocks_per_cu(int(parts[1] or 8)), "blocks_per_cu")
+            native.check(lib.sccsum_set_group_units(int(parts[2] or 0)), "group_units")
             if mode == "frames":
                 return batch.ipv4_frames(b)
             return batch.spans(b)
@@ -85,6 +90,7 @@ def main():
         torch.cuda.empty_cache()
     native.check(lib.sccsum_set_kernel_variant(0), "variant")
     native.check(lib.sccsum_set_blocks_per_cu(8), "blocks_per_cu")
+    native.check(lib.sccsum_set_group_units(0), "group_units")
 
 
 if __name__ == "__main__":
