@@ -114,7 +114,8 @@ int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len,
  * loop, 2 = batch kernel, 3 = batch
  * kernel with the next packet in flight, 4 / 5 = 2 / 3 with default cache
  * policy instead of nontemporal loads, 6 / 7 = 2 / 3 with each packet's last
- * 128-byte line loaded with the default policy).  All variants produce
+ * 128-byte line loaded with the default policy, 8 / 9 = 2 / 6 with short
+ * packets sharing passes: 4 per pass on 16 lanes each or 2 on 32).  All variants produce
  * identical results; the knob exists for in-process A/B timing and for
  * cross-checking two independent kernels.  SCCSUM_EINVAL for an unknown one. */
 int sccsum_set_kernel_variant(int variant);

@@ -27,6 +27,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <type_traits>
 
 #include "sccsum.h"
 
@@ -330,7 +331,7 @@ __device__ uint32_t exact_range_sum(const uint8_t* a0, uint64_t rs, uint64_t re,
 //     pseudo-header, complements; one coalesced store for the tile.
 //  D: packets the fast path cannot take (frames with options or a trimmed
 //     IP length, spans longer than 128 KiB) are redone exactly, one wave each.
-template <int U, bool IPV4, bool PIPE, int AUX, bool HYB>
+template <int U, bool IPV4, bool PIPE, int AUX, bool HYB, bool MULTI>
 __global__ __launch_bounds__(kBlock) void csum_batch_kernel(
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
@@ -410,16 +411,17 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(
             // long packets: kLongGroups groups of loads in flight per step;
             // the final group always goes through the single-group loop below
             // so P.v ends up holding it (tail stash)
-            for (; g + kLongGroups * gu < P.s; g += kLongGroups * gu) {
-                u32x4 w[kLongGroups][U];
+            constexpr int kLG = PIPE ? 2 : kLongGroups;  // the ping-pong loop holds two load sets
+            for (; g + kLG * gu < P.s; g += kLG * gu) {
+                u32x4 w[kLG][U];
 #pragma unroll
-                for (int q = 0; q < kLongGroups; ++q)
+                for (int q = 0; q < kLG; ++q)
 #pragma unroll
                     for (int u = 0; u < U; ++u)
                         w[q][u] = __builtin_amdgcn_raw_buffer_load_b128(
                             P.r, static_cast<int>(16u * (g + q * gu) + vo + 1024u * u), 0, AUX);
 #pragma unroll
-                for (int q = 0; q < kLongGroups; ++q)
+                for (int q = 0; q < kLG; ++q)
 #pragma unroll
                     for (int u = 0; u < U; ++u) acc = sad4(w[q][u], acc);
             }
@@ -452,20 +454,94 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(
             res = writelane(res, S, k, lane);
         };
 
-        if (!PIPE) {
+        // MULTI: several short packets share one pass — NP packets x (64/NP)
+        // lanes x U units; per-lane packet addresses come from the plan lanes by
+        // ds_bpermute and 16-lane DPP row sums give one total per packet, so
+        // the per-pass issue work is divided by NP.
+        auto multi = [&](auto npc, uint32_t k) {
+            constexpr uint32_t NP = decltype(npc)::value;
+            constexpr uint32_t SL = kWave / NP;  // lanes per packet (32 or 16)
+            constexpr uint32_t kHead = IPV4 ? 3u : 1u;
+            const uint32_t seg = lane / SL, j = lane % SL;
+            const int src = static_cast<int>(k + seg);
+            const uint32_t qlo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(a0)), src));
+            const uint32_t qhi = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(a0 >> 32)), src));
+            const uint32_t qnu = static_cast<uint32_t>(__shfl(static_cast<int>(nunits), src));
+            const uint8_t* qa = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(qhi) << 32) | qlo);
+            u32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = j + SL * u;
+                v[u] = u32x4{0, 0, 0, 0};
+                if (c < qnu) v[u] = load_unit(qa + 16u * c);
+            }
+            uint32_t acc = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = sad4(v[u], acc);
+            uint8_t* row = stash + static_cast<uint32_t>(src) * kStashStride;
+            if (j < kHead) *reinterpret_cast<u32x4*>(row + 16u * j) = v[0];
+            if (qnu) {
+                const uint32_t last = qnu - 1;
+                u32x4 lu = v[0];
+#pragma unroll
+                for (int u = 1; u < U; ++u) lu = last / SL == static_cast<uint32_t>(u) ? v[u] : lu;
+                if (j == last % SL) *reinterpret_cast<u32x4*>(row + 48) = lu;
+            }
+            // 16-lane row sums
+            acc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc), 0xB1, 0xF, 0xF, false));
+            acc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc), 0x4E, 0xF, 0xF, false));
+            acc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc), 0x124, 0xF, 0xF, false));
+            acc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc), 0x128, 0xF, 0xF, false));
+            const uint32_t r0 = __builtin_amdgcn_readlane(acc, 0), r1 = __builtin_amdgcn_readlane(acc, 16);
+            const uint32_t r2 = __builtin_amdgcn_readlane(acc, 32), r3 = __builtin_amdgcn_readlane(acc, 48);
+            if (NP == 4) {
+                res = writelane(res, r0, k, lane);
+                res = writelane(res, r1, k + 1, lane);
+                res = writelane(res, r2, k + 2, lane);
+                res = writelane(res, r3, k + 3, lane);
+            } else {
+                res = writelane(res, r0 + r1, k, lane);
+                res = writelane(res, r2 + r3, k + 1, lane);
+            }
+        };
+
+        if (MULTI) {
+            const uint64_t quad_ok = __ballot(nunits <= 16u * U);
+            const uint64_t pair_ok = __ballot(nunits <= 32u * U);
+            uint32_t k = 0;
+            while (k < cnt) {
+                if (k + 4 <= cnt && ((quad_ok >> k) & 0xFull) == 0xFull) {
+                    multi(std::integral_constant<uint32_t, 4>{}, k);
+                    k += 4;
+                } else if (k + 2 <= cnt && ((pair_ok >> k) & 0x3ull) == 0x3ull) {
+                    multi(std::integral_constant<uint32_t, 2>{}, k);
+                    k += 2;
+                } else {
+                    PktLoad P;
+                    issue(k, true, P);
+                    body(k, P);
+                    k += 1;
+                }
+            }
+        } else if (!PIPE) {
             for (uint32_t k = 0; k < cnt; ++k) {
                 PktLoad P;
                 issue(k, true, P);
                 body(k, P);
             }
         } else {
-            PktLoad P, P1;
-            issue(0, true, P);
-            for (uint32_t k = 0; k < cnt; ++k) {
-                const bool more = k + 1 < cnt;
-                issue(more ? k + 1 : k, more, P1);
-                body(k, P);
-                P = P1;
+            // ping-pong: packet k+1's loads are in flight while packet k is
+            // summed; two named load sets, no register copies (copying an
+            // in-flight load's destination would force a full vmcnt(0) wait)
+            PktLoad PA, PB;
+            issue(0, true, PA);
+            for (uint32_t k = 0; k < cnt; k += 2) {
+                const bool m1 = k + 1 < cnt;
+                issue(m1 ? k + 1 : k, m1, PB);
+                body(k, PA);
+                const bool m2 = k + 2 < cnt;
+                issue(m2 ? k + 2 : k, m2, PA);
+                if (m1) body(k + 1, PB);
             }
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): stash writes visible to this wave's reads
@@ -649,7 +725,8 @@ int units_class(uint32_t max_len) {
 // 1 = simple one-packet-per-wave loop (independent second implementation),
 // 2 = batch kernel, 3 = batch kernel with the next packet in flight (both
 // with nontemporal loads), 4 / 5 = 2 / 3 with default-policy loads,
-// 6 / 7 = 2 / 3 with each packet's last 128-byte line loaded default-policy.
+// 6 / 7 = 2 / 3 with each packet's last 128-byte line loaded default-policy,
+// 8 / 9 = 2 / 6 with short packets sharing passes (4 x 16 or 2 x 32 lanes).
 std::atomic<int> g_variant{0};
 
 template <int U, bool IPV4>
@@ -667,28 +744,36 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     const dim3 grid(grid_for((n + B - 1) / B));
     const uint32_t b32 = static_cast<uint32_t>(B);
     switch (variant) {
+        case 8:
+            csum_batch_kernel<U, IPV4, false, kNT, false, true>
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+            break;
+        case 9:
+            csum_batch_kernel<U, IPV4, false, kNT, true, true>
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+            break;
         case 6:
-            csum_batch_kernel<U, IPV4, false, kNT, true>
+            csum_batch_kernel<U, IPV4, false, kNT, true, false>
                 <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
             break;
         case 7:
-            csum_batch_kernel<U, IPV4, true, kNT, true>
+            csum_batch_kernel<U, IPV4, true, kNT, true, false>
                 <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
             break;
         case 2:
-            csum_batch_kernel<U, IPV4, false, kNT, false>
+            csum_batch_kernel<U, IPV4, false, kNT, false, false>
                 <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
             break;
         case 4:
-            csum_batch_kernel<U, IPV4, false, 0, false>
+            csum_batch_kernel<U, IPV4, false, 0, false, false>
                 <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
             break;
         case 5:
-            csum_batch_kernel<U, IPV4, true, 0, false>
+            csum_batch_kernel<U, IPV4, true, 0, false, false>
                 <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
             break;
         default:
-            csum_batch_kernel<U, IPV4, true, kNT, false>
+            csum_batch_kernel<U, IPV4, true, kNT, false, false>
                 <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
             break;
     }
@@ -782,7 +867,7 @@ int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len, const uint64_t* 
 }
 
 int sccsum_set_kernel_variant(int variant) {
-    if (variant < 0 || variant > 7) return SCCSUM_EINVAL;
+    if (variant < 0 || variant > 9) return SCCSUM_EINVAL;
     sccsum::g_variant.store(variant, std::memory_order_relaxed);
     return SCCSUM_OK;
 }

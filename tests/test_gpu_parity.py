@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7], ids=["simple", "batch", "batch_pipe", "batch_dflt", "batch_pipe_dflt", "batch_hyb", "batch_pipe_hyb"], autouse=True)
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9], ids=["simple", "batch", "batch_pipe", "batch_dflt", "batch_pipe_dflt", "batch_hyb", "batch_pipe_hyb", "batch_multi", "batch_hyb_multi"], autouse=True)
 def kernel_variant(request, dev):
     """Every parity test runs against both kernel families."""
     lib = native.load()

@@ -30,6 +30,10 @@ def cases(dev):
     buf = np.random.default_rng(5).integers(0, 256, size=total, dtype=np.uint8)
     mb = batch.PacketBatch.from_host(buf, off, lens, device=dev)
     yield "zipf_spans", mb, "spans", int(lens.sum()) + lens.size * 14
+    del mb
+    big = synth.zipf_lengths(3_400_000, seed=6)
+    fb = devsynth.mixed_frames(big, seed=7, device=dev)
+    yield "cfg3_zipf_frames", fb, "frames", int(big.sum()) + big.size * 16
     n64 = 16384
     seg = torch.randint(0, 256, (n64 * 65536,), dtype=torch.uint8, device=dev)
     lb = batch.PacketBatch(data=seg, off=torch.arange(n64, device=dev, dtype=torch.int64) * 65536,
@@ -43,7 +47,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U]]")
-    ap.add_argument("--cases", default="udp1500_frames,udp1500_spans,zipf_spans,tcp64k_spans")
+    ap.add_argument("--cases", default="udp1500_frames,udp1500_spans,zipf_spans,cfg3_zipf_frames,tcp64k_spans")
     args = ap.parse_args()
     variants = args.variants.split(",")
     lib = native.load()
