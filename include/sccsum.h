@@ -38,8 +38,10 @@
  *   - d_bytes must be 16-byte aligned, d_off 8-byte aligned, d_len/d_seed/d_out2 4-byte aligned,
  *     d_out 2-byte aligned.
  *   - Launches are asynchronous on `stream` (a hipStream_t; NULL = the
- *     device's null stream).  No allocation, no host synchronisation: the
- *     calls are safe inside hipStreamBeginCapture.
+ *     device's null stream), one kernel each.  No allocation, no host
+ *     synchronisation: the calls are safe inside hipStreamBeginCapture.  At
+ *     most 256 launches may be in flight per device at once (the ring of tile
+ *     counters they dequeue from).
  *
  * Threading: one host thread per device (Seastar's shard-per-core model).
  * Calls are re-entrant per stream.
@@ -75,8 +77,11 @@ const char* sccsum_strerror(int err);
 /* Number of visible HIP devices. */
 int sccsum_device_count(int* count);
 
-/* Bind the calling host thread to `device` (hipSetDevice) and cache its
- * compute-unit count for launch sizing. */
+/* Bind the calling host thread to `device` (hipSetDevice), cache its
+ * compute-unit count for launch sizing and allocate (once per device) the
+ * small ring of tile counters the batch kernel dequeues from.  Call it on
+ * every thread that launches; launches made without it fall back to static
+ * tile order. */
 int sccsum_init(int device);
 
 /* Pseudo-header partial sum exactly as ipv4_traits::*_pseudo_header_checksum
@@ -128,6 +133,14 @@ int sccsum_set_blocks_per_cu(int blocks);
 /* Diagnostic: force U, the 16-byte units each lane loads per step of a packet
  * (1, 2, 4 or 8; 0 = choose from max_len).  Results are unaffected. */
 int sccsum_set_group_units(int units);
+
+/* Diagnostic: cap the batch kernel's tile (packets a wave plans at once) at
+ * 1..64 (default 64).  Results are unaffected. */
+int sccsum_set_tile_packets(int packets);
+
+/* Diagnostic: batch-kernel tiles dequeued from per-XCD counters (1, the
+ * default) or dealt round robin (0).  Results are unaffected. */
+int sccsum_set_dynamic_tiles(int on);
 
 /* Wait for all work queued on `stream`. */
 int sccsum_sync(void* stream);

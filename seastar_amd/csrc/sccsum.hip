@@ -294,6 +294,10 @@ __device__ __forceinline__ uint32_t unit_part(const u32x4& v, int lo, int hi) {
 constexpr uint32_t kStashUnits = 4;     // units 0..2 of a packet (IPv4 header) + its last unit
 constexpr uint32_t kStashStride = 80;   // bytes per packet row (5 x 16 B: conflict-free ds_read_b128)
 constexpr uint32_t kExactMax = 131072;  // fast path keeps exact 32-bit sums up to this length
+// tile-head counters: each on its own 256-byte line (atomics to one line
+// serialise at the memory side: ~12 ns each chip-wide)
+constexpr uint32_t kHeadStride = 64;                      // uint32 words between counters
+constexpr uint32_t kHeadSlotWords = 9 * kHeadStride;      // one launch's 8 heads + exit counter
 #ifndef SCCSUM_LONG_GROUPS
 #define SCCSUM_LONG_GROUPS 3
 #endif
@@ -336,7 +340,7 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
     const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
-    uint8_t* __restrict__ status, uint64_t n, uint32_t B) {
+    uint8_t* __restrict__ status, uint64_t n, uint32_t B, uint32_t* __restrict__ heads) {
     __shared__ __attribute__((aligned(16))) uint8_t stash_all[kWavesPerBlock][kWave * kStashStride];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -346,7 +350,22 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(
     const bool has_seed = !IPV4 && seed != nullptr;
     const uint32_t vo = 16u * lane;  // this lane's byte offset inside a 1 KiB slice
 
-    for (uint64_t t = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv; t < ntiles; t += nwaves) {
+    // Tile order: with `heads` (8 zeroed counters) a wave dequeues its next
+    // tile from its workgroup's XCD group (blockIdx % 8 — placement only
+    // affects speed): tile = x + 8 * atomicAdd(heads[x], 1); so waves that
+    // drew short tiles take more (Zipf batches).  Without: static round robin.
+    const uint32_t xg = blockIdx.x & 7u;
+    auto next_tile = [&](uint64_t prev) -> uint64_t {
+        if (heads == nullptr) return prev + nwaves;
+        uint32_t d = 0;
+        if (lane == 0)
+            d = __hip_atomic_fetch_add(heads + xg * kHeadStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        d = __builtin_amdgcn_readfirstlane(d);
+        return static_cast<uint64_t>(xg) + 8ull * d;
+    };
+    uint64_t t0 = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
+    if (heads != nullptr) t0 = next_tile(0);
+    for (uint64_t t = t0; t < ntiles; t = next_tile(t)) {
         // ---- A: per-lane packet plan
         const uint64_t base = t * B;
         const uint64_t left = n - base;
@@ -656,6 +675,20 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(
         }
         __builtin_amdgcn_wave_barrier();  // stash rows are rewritten by the next tile
     }
+    // Self-resetting tile heads: every wave counts itself out on the slot's
+    // exit word (its own line, after the 8 heads); the last one out has seen
+    // every dequeue of this launch return, so it zeroes the heads and the exit
+    // word for the launch that reuses the slot kHeadSlots launches later.
+    if (heads != nullptr && lane == 0) {
+        uint32_t* exitw = heads + 8 * kHeadStride;
+        const uint32_t total = gridDim.x * kWavesPerBlock;
+        if (__hip_atomic_fetch_add(exitw, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+            for (uint32_t x = 0; x < 8; ++x) {
+                __hip_atomic_store(heads + x * kHeadStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __hip_atomic_store(exitw, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // Plain stream-read of the same load shape (16 B per lane, nontemporal).
@@ -707,6 +740,37 @@ unsigned grid_for(uint64_t n) {
 }
 
 std::atomic<int> g_group_units{0};  // diagnostic override of U (0 = by max_len)
+std::atomic<int> g_tile_packets{kWave};  // max packets per batch-kernel tile
+std::atomic<int> g_dynamic{1};           // batch kernel: dequeue tiles (1) or static round robin (0)
+
+// Per-device ring of tile-head slots (8 heads + 1 exit counter, each on its
+// own line), allocated and zeroed once in sccsum_init; each launch takes the
+// next slot and its last wave leaves it zeroed again, so launches need no
+// memset and launches on different streams do not share counters (up to
+// kHeadSlots launches in flight per device).
+constexpr int kHeadSlots = 256;
+uint32_t* g_heads[kMaxDevices];
+std::atomic<uint32_t> g_head_next[kMaxDevices];
+
+int ensure_heads(int dev) {
+    if (dev < 0 || dev >= kMaxDevices) return SCCSUM_ENODEV;
+    if (g_heads[dev] != nullptr) return SCCSUM_OK;
+    void* p = nullptr;
+    const size_t bytes = size_t(kHeadSlots) * kHeadSlotWords * sizeof(uint32_t);
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return static_cast<int>(e);
+    e = hipMemset(p, 0, bytes);  // once: from here on every launch leaves its slot zeroed
+    if (e != hipSuccess) return static_cast<int>(e);
+    g_heads[dev] = static_cast<uint32_t*>(p);
+    return SCCSUM_OK;
+}
+
+uint32_t* next_heads() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices || g_heads[dev] == nullptr) return nullptr;
+    const uint32_t slot = g_head_next[dev].fetch_add(1, std::memory_order_relaxed) % kHeadSlots;
+    return g_heads[dev] + kHeadSlotWords * slot;
+}
 
 int units_class(uint32_t max_len) {
     const int forced = g_group_units.load(std::memory_order_relaxed);
@@ -739,42 +803,45 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     }
     // batch kernel: tiles of B <= 64 packets, enough tiles to fill every wave slot
     const uint64_t slots = static_cast<uint64_t>(cu_count()) * g_blocks_per_cu.load() * kWavesPerBlock;
+    const uint64_t bmax = static_cast<uint64_t>(g_tile_packets.load(std::memory_order_relaxed));
     uint64_t B = (n + slots - 1) / slots;
-    B = B < 1 ? 1 : (B > kWave ? kWave : B);
+    B = B < 1 ? 1 : (B > bmax ? bmax : B);
     const dim3 grid(grid_for((n + B - 1) / B));
     const uint32_t b32 = static_cast<uint32_t>(B);
+    uint32_t* heads = nullptr;
+    if (g_dynamic.load(std::memory_order_relaxed)) heads = next_heads();
     switch (variant) {
         case 8:
             csum_batch_kernel<U, IPV4, false, kNT, false, true>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
             break;
         case 9:
             csum_batch_kernel<U, IPV4, false, kNT, true, true>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
             break;
         case 6:
             csum_batch_kernel<U, IPV4, false, kNT, true, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
             break;
         case 7:
             csum_batch_kernel<U, IPV4, true, kNT, true, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
             break;
         case 2:
             csum_batch_kernel<U, IPV4, false, kNT, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
             break;
         case 4:
             csum_batch_kernel<U, IPV4, false, 0, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
             break;
         case 5:
             csum_batch_kernel<U, IPV4, true, 0, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
             break;
         default:
             csum_batch_kernel<U, IPV4, true, kNT, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
             break;
     }
 }
@@ -843,7 +910,7 @@ int sccsum_init(int device) {
     const hipError_t e2 = hipSetDevice(device);
     if (e2 != hipSuccess) return static_cast<int>(e2);
     (void)sccsum::cu_count();
-    return SCCSUM_OK;
+    return sccsum::ensure_heads(device);
 }
 
 // ip.hh:70-75 via checksummer::sum_many(uint32 src, uint32 dst, uint8 0,
@@ -881,6 +948,18 @@ int sccsum_set_blocks_per_cu(int blocks) {
 int sccsum_set_group_units(int units) {
     if (units != 0 && units != 1 && units != 2 && units != 4 && units != 8) return SCCSUM_EINVAL;
     sccsum::g_group_units.store(units, std::memory_order_relaxed);
+    return SCCSUM_OK;
+}
+
+int sccsum_set_tile_packets(int packets) {
+    if (packets < 1 || packets > sccsum::kWave) return SCCSUM_EINVAL;
+    sccsum::g_tile_packets.store(packets, std::memory_order_relaxed);
+    return SCCSUM_OK;
+}
+
+int sccsum_set_dynamic_tiles(int on) {
+    if (on != 0 && on != 1) return SCCSUM_EINVAL;
+    sccsum::g_dynamic.store(on, std::memory_order_relaxed);
     return SCCSUM_OK;
 }
 

@@ -46,7 +46,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U]]")
+    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn]]]]")
     ap.add_argument("--cases", default="udp1500_frames,udp1500_spans,zipf_spans,cfg3_zipf_frames,tcp64k_spans")
     args = ap.parse_args()
     variants = args.variants.split(",")
@@ -61,10 +61,12 @@ def main():
         times = {v: [] for v in variants}
 
         def run(v):
-            parts = (v.split(":") + ["", ""])[:3]
+            parts = (v.split(":") + ["", "", "", ""])[:5]
             native.check(lib.sccsum_set_kernel_variant(int(parts[0])), "variant")
             native.check(lib.sccsum_set_blocks_per_cu(int(parts[1] or 8)), "blocks_per_cu")
             native.check(lib.sccsum_set_group_units(int(parts[2] or 0)), "group_units")
+            native.check(lib.sccsum_set_tile_packets(int(parts[3] or 64)), "tile_packets")
+            native.check(lib.sccsum_set_dynamic_tiles(int(parts[4] or 1)), "dynamic")
             if mode == "frames":
                 return batch.ipv4_frames(b)
             return batch.spans(b)
@@ -95,6 +97,8 @@ def main():
     native.check(lib.sccsum_set_kernel_variant(0), "variant")
     native.check(lib.sccsum_set_blocks_per_cu(8), "blocks_per_cu")
     native.check(lib.sccsum_set_group_units(0), "group_units")
+    native.check(lib.sccsum_set_tile_packets(64), "tile_packets")
+    native.check(lib.sccsum_set_dynamic_tiles(1), "dynamic")
 
 
 if __name__ == "__main__":
