@@ -115,7 +115,7 @@ int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len,
                        void* stream);
 
 /* Diagnostic: select the kernel family for later launches in this process
- * (0 = default (6 when max_len <= 2048, else 2), 1 = one-packet-per-wave
+ * (0 = default (6 when max_len <= 2048, else 8), 1 = one-packet-per-wave
  * loop, 2 = batch kernel, 3 = batch
  * kernel with the next packet in flight, 4 / 5 = 2 / 3 with default cache
  * policy instead of nontemporal loads, 6 / 7 = 2 / 3 with each packet's last

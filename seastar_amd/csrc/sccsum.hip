@@ -297,11 +297,15 @@ constexpr uint32_t kExactMax = 131072;  // fast path keeps exact 32-bit sums up 
 // tile-head counters: each on its own 256-byte line (atomics to one line
 // serialise at the memory side: ~12 ns each chip-wide)
 constexpr uint32_t kHeadStride = 64;                      // uint32 words between counters
-constexpr uint32_t kHeadSlotWords = 9 * kHeadStride;      // one launch's 8 heads + exit counter
+constexpr uint32_t kGroups = 64;                            // tile-dequeue counters per launch
+constexpr uint32_t kHeadSlotWords = kGroups * kHeadStride;  // one launch's counters
 #ifndef SCCSUM_LONG_GROUPS
 #define SCCSUM_LONG_GROUPS 3
 #endif
 constexpr int kLongGroups = SCCSUM_LONG_GROUPS;  // groups in flight per step of a long packet
+#ifndef SCCSUM_BATCH_MIN_WAVES
+#define SCCSUM_BATCH_MIN_WAVES 1  // __launch_bounds__ waves per SIMD floor (8 = cap VGPRs at 64)
+#endif
 static_assert(kStashStride >= 16 * kStashUnits && kStashStride % 16 == 0, "stash row layout");
 
 // Exact folded sum (little-endian domain relative to a0) of [rs, re), one
@@ -336,7 +340,7 @@ __device__ uint32_t exact_range_sum(const uint8_t* a0, uint64_t rs, uint64_t re,
 //  D: packets the fast path cannot take (frames with options or a trimmed
 //     IP length, spans longer than 128 KiB) are redone exactly, one wave each.
 template <int U, bool IPV4, bool PIPE, int AUX, bool HYB, bool MULTI>
-__global__ __launch_bounds__(kBlock) void csum_batch_kernel(
+__global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_kernel(
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
     const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
@@ -350,22 +354,37 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(
     const bool has_seed = !IPV4 && seed != nullptr;
     const uint32_t vo = 16u * lane;  // this lane's byte offset inside a 1 KiB slice
 
-    // Tile order: with `heads` (8 zeroed counters) a wave dequeues its next
-    // tile from its workgroup's XCD group (blockIdx % 8 — placement only
-    // affects speed): tile = x + 8 * atomicAdd(heads[x], 1); so waves that
-    // drew short tiles take more (Zipf batches).  Without: static round robin.
-    const uint32_t xg = blockIdx.x & 7u;
+    // Tile order.  Wave w first takes tile w (static: no start-up contention).
+    // With `heads`, the remaining tiles [W, ntiles) are split over kGroups
+    // counters (each on its own line) and dequeued: wave w pulls
+    // tile W + g + kGroups * atomicAdd(heads[g], 1) with g = w % kGroups, so
+    // waves that drew short tiles take more (Zipf batches).  Each group's
+    // dequeue count is known — one per remaining tile of the group plus one
+    // failing dequeue per wave of the group — so the wave that draws the last
+    // number zeroes the counter for the next launch on this slot (no memset,
+    // graph-replay safe).  Without `heads`: static round robin.
+    const uint64_t wglob = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
+    const uint32_t grp = static_cast<uint32_t>(wglob % kGroups);
+    const uint64_t rest = ntiles > nwaves ? ntiles - nwaves : 0;
+    const uint32_t tiles_g = rest > grp ? static_cast<uint32_t>((rest - grp + kGroups - 1) / kGroups) : 0u;
+    const uint32_t waves_g = static_cast<uint32_t>(nwaves / kGroups);  // host keeps nwaves % kGroups == 0
     auto next_tile = [&](uint64_t prev) -> uint64_t {
         if (heads == nullptr) return prev + nwaves;
         uint32_t d = 0;
-        if (lane == 0)
-            d = __hip_atomic_fetch_add(heads + xg * kHeadStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) {
+            uint32_t* h = heads + grp * kHeadStride;
+            d = __hip_atomic_fetch_add(h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (d == tiles_g + waves_g - 1) __hip_atomic_store(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         d = __builtin_amdgcn_readfirstlane(d);
-        return static_cast<uint64_t>(xg) + 8ull * d;
+        return d < tiles_g ? nwaves + grp + static_cast<uint64_t>(kGroups) * d : ntiles;
     };
-    uint64_t t0 = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
-    if (heads != nullptr) t0 = next_tile(0);
-    for (uint64_t t = t0; t < ntiles; t = next_tile(t)) {
+    // the next tile is dequeued when a tile starts, so the atomic's round trip
+    // hides under the tile's loads; a wave stops after its one failing dequeue
+    uint64_t t = wglob;
+    if (t >= ntiles && heads != nullptr) t = next_tile(t);
+    while (t < ntiles) {
+        const uint64_t t_next = next_tile(t);
         // ---- A: per-lane packet plan
         const uint64_t base = t * B;
         const uint64_t left = n - base;
@@ -430,7 +449,7 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(
             // long packets: kLongGroups groups of loads in flight per step;
             // the final group always goes through the single-group loop below
             // so P.v ends up holding it (tail stash)
-            constexpr int kLG = PIPE ? 2 : kLongGroups;  // the ping-pong loop holds two load sets
+            constexpr int kLG = (PIPE || MULTI) ? 2 : kLongGroups;  // leave registers for the second load set / shared passes
             for (; g + kLG * gu < P.s; g += kLG * gu) {
                 u32x4 w[kLG][U];
 #pragma unroll
@@ -674,20 +693,7 @@ __global__ __launch_bounds__(kBlock) void csum_batch_kernel(
             if (status) status[base + lane] = static_cast<uint8_t>(st);
         }
         __builtin_amdgcn_wave_barrier();  // stash rows are rewritten by the next tile
-    }
-    // Self-resetting tile heads: every wave counts itself out on the slot's
-    // exit word (its own line, after the 8 heads); the last one out has seen
-    // every dequeue of this launch return, so it zeroes the heads and the exit
-    // word for the launch that reuses the slot kHeadSlots launches later.
-    if (heads != nullptr && lane == 0) {
-        uint32_t* exitw = heads + 8 * kHeadStride;
-        const uint32_t total = gridDim.x * kWavesPerBlock;
-        if (__hip_atomic_fetch_add(exitw, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
-            for (uint32_t x = 0; x < 8; ++x) {
-                __hip_atomic_store(heads + x * kHeadStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __hip_atomic_store(exitw, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        t = t_next;
     }
 }
 
@@ -743,11 +749,11 @@ std::atomic<int> g_group_units{0};  // diagnostic override of U (0 = by max_len)
 std::atomic<int> g_tile_packets{kWave};  // max packets per batch-kernel tile
 std::atomic<int> g_dynamic{1};           // batch kernel: dequeue tiles (1) or static round robin (0)
 
-// Per-device ring of tile-head slots (8 heads + 1 exit counter, each on its
-// own line), allocated and zeroed once in sccsum_init; each launch takes the
-// next slot and its last wave leaves it zeroed again, so launches need no
-// memset and launches on different streams do not share counters (up to
-// kHeadSlots launches in flight per device).
+// Per-device ring of tile-head slots (kGroups heads, each on its own line),
+// allocated and zeroed once in sccsum_init; each launch takes the next slot
+// and leaves it zeroed again (the last dequeue of each group resets it), so
+// launches need no memset and launches on different streams do not share
+// counters (up to kHeadSlots launches in flight per device).
 constexpr int kHeadSlots = 256;
 uint32_t* g_heads[kMaxDevices];
 std::atomic<uint32_t> g_head_next[kMaxDevices];
@@ -783,9 +789,10 @@ int units_class(uint32_t max_len) {
     return 8;
 }
 
-// Kernel variant: 0 = default (batch kernel: 6 when max_len <= 2 KiB, else 2;
-// measured: the hybrid policy pays for packed MTU-size frames, all-nontemporal
-// for mixed and long packets; cross-packet prefetch (3, 5, 7) only adds issue work),
+// Kernel variant: 0 = default (batch kernel: 6 when max_len <= 2 KiB, else 8;
+// measured: the hybrid policy pays for packed MTU-size frames, shared passes
+// for short packets + all-nontemporal for mixed and long ones; cross-packet
+// prefetch (3, 5, 7) only adds issue work),
 // 1 = simple one-packet-per-wave loop (independent second implementation),
 // 2 = batch kernel, 3 = batch kernel with the next packet in flight (both
 // with nontemporal loads), 4 / 5 = 2 / 3 with default-policy loads,
@@ -806,7 +813,8 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     const uint64_t bmax = static_cast<uint64_t>(g_tile_packets.load(std::memory_order_relaxed));
     uint64_t B = (n + slots - 1) / slots;
     B = B < 1 ? 1 : (B > bmax ? bmax : B);
-    const dim3 grid(grid_for((n + B - 1) / B));
+    // grid: multiple of 16 workgroups so the wave count divides into kGroups
+    const dim3 grid((grid_for((n + B - 1) / B) + 15u) & ~15u);
     const uint32_t b32 = static_cast<uint32_t>(B);
     uint32_t* heads = nullptr;
     if (g_dynamic.load(std::memory_order_relaxed)) heads = next_heads();
@@ -858,7 +866,7 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
         return SCCSUM_EINVAL;
     }
     int variant = g_variant.load(std::memory_order_relaxed);
-    if (variant == 0) variant = (max_len != 0 && max_len <= 2048) ? 6 : 2;
+    if (variant == 0) variant = (max_len != 0 && max_len <= 2048) ? 6 : 8;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
     // batch kernel: U = 2 for every size (long packets keep 4 groups in flight
