@@ -19,6 +19,8 @@
  *                             src/net/ip.cc:121-127, 271-277;
  *                             length checks / trim / strip 4*ihl  src/net/ip.cc:128-140, 220-225;
  *                             L4 pseudo-header + segment  include/seastar/net/tcp.hh:876-883 }
+ *   sccsum_fragments    N x checksummer::sum(const packet&)  src/net/ip_checksum.cc:64-68
+ *                       (fragment lists with the odd-byte carry) + get()
  *   sccsum_pseudo_seed  ipv4_traits::{tcp,udp}_pseudo_header_checksum
  *                       include/seastar/net/ip.hh:70-75 (host arithmetic, O(1))
  *
@@ -113,6 +115,24 @@ int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len,
                        const uint64_t* d_off, const uint32_t* d_len,
                        uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len,
                        void* stream);
+
+/* Checksum n packets that are FRAGMENT LISTS, like checksummer::sum(const
+ * packet&) (src/net/ip_checksum.cc:64-68): packet i is the concatenation of
+ * fragments d_pkt_first[i] .. d_pkt_first[i+1]-1, fragment j being
+ * d_bytes[d_frag_off[j] .. +d_frag_len[j]) (any order, any alignment; DPDK
+ * multi-segment mbufs, virtio mergeable buffers).  A fragment that starts at
+ * an odd offset of its packet contributes byte-swapped, exactly the
+ * reference's `odd` carry.  d_pkt_first has n+1 nondecreasing entries ending
+ * at nfrag; d_seed / d_status optional as for sccsum_spans.  d_workspace:
+ * device scratch of sccsum_fragments_workspace(nfrag) bytes, 16-byte aligned.
+ * A packet with a fragment outside the buffer (or a bad d_pkt_first range)
+ * gets 0 and SCCSUM_ST_RANGE. */
+int sccsum_fragments(const void* d_bytes, uint64_t bytes_len,
+                     const uint64_t* d_frag_off, const uint32_t* d_frag_len, uint64_t nfrag,
+                     const uint32_t* d_pkt_first, const uint32_t* d_seed,
+                     uint16_t* d_out, uint8_t* d_status, uint64_t n, uint32_t max_frag_len,
+                     void* d_workspace, void* stream);
+uint64_t sccsum_fragments_workspace(uint64_t nfrag);
 
 /* Diagnostic: select the kernel family for later launches in this process
  * (0 = default (6 when max_len <= 2048, else 8), 1 = one-packet-per-wave

@@ -51,6 +51,7 @@ def lib():
             "oracle_fold_seed": (ctypes.c_uint32, [cs]),
             "oracle_batch_spans": (None, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int]),
             "oracle_batch_ipv4": (None, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int]),
+            "oracle_batch_fragments": (None, [_P, _P, _P, _P, _P, _P, ctypes.c_uint64]),
         }
         for name, (res, args) in protos.items():
             fn = getattr(L, name)
@@ -114,3 +115,16 @@ def batch_ipv4(buf: np.ndarray, off: np.ndarray, length: np.ndarray, nthreads: i
     status = np.empty(off.size, dtype=np.uint8)
     lib().oracle_batch_ipv4(_addr(buf), _addr(off), _addr(length), _addr(out2), _addr(status), off.size, nthreads)
     return out2, status
+
+
+def batch_fragments(buf, frag_off, frag_len, pkt_first, seeds=None) -> np.ndarray:
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    frag_off = np.ascontiguousarray(frag_off, dtype=np.uint64)
+    frag_len = np.ascontiguousarray(frag_len, dtype=np.uint32)
+    pkt_first = np.ascontiguousarray(pkt_first, dtype=np.uint32)
+    seeds = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    n = pkt_first.size - 1
+    out = np.empty(n, dtype=np.uint16)
+    lib().oracle_batch_fragments(_addr(buf), _addr(frag_off), _addr(frag_len), _addr(pkt_first), _addr(seeds),
+                                 _addr(out), n)
+    return out

@@ -247,3 +247,19 @@ void oracle_batch_ipv4(const uint8_t* bytes, const uint64_t* off, const uint32_t
     job_t b = {1, bytes, off, len, 0, out2, status, 0, 0};
     run_batch(b, n, nthreads);
 }
+
+/* src/net/ip_checksum.cc:64-68 applied per packet of a fragment-list batch */
+void oracle_batch_fragments(const uint8_t* bytes, const uint64_t* frag_off, const uint32_t* frag_len,
+                            const uint32_t* pkt_first, const uint32_t* seed, uint16_t* out, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i) {
+        oracle_checksummer c;
+        oracle_init(&c);
+        if (seed) {
+            c.csum = seed[i];
+        }
+        for (uint32_t j = pkt_first[i]; j < pkt_first[i + 1]; ++j) {
+            oracle_sum_bytes(&c, bytes + frag_off[j], frag_len[j]);
+        }
+        out[i] = oracle_get(&c);
+    }
+}

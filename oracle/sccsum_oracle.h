@@ -74,6 +74,12 @@ void oracle_batch_spans(const uint8_t* bytes, const uint64_t* off, const uint32_
 void oracle_batch_ipv4(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                        uint16_t* out2, uint8_t* status, uint64_t n, int nthreads);
 
+/* Fragment lists: packet i = fragments pkt_first[i] .. pkt_first[i+1]-1, each
+ * bytes[frag_off[j] .. +frag_len[j]); seeded like oracle_batch_spans, then
+ * checksummer::sum(const packet&) (ip_checksum.cc:64-68) + get(). */
+void oracle_batch_fragments(const uint8_t* bytes, const uint64_t* frag_off, const uint32_t* frag_len,
+                            const uint32_t* pkt_first, const uint32_t* seed, uint16_t* out, uint64_t n);
+
 /* Fold a checksummer csum to a seed value (end-around carry, zero stays zero). */
 uint32_t oracle_fold_seed(const oracle_checksummer* c);
 

@@ -101,6 +101,23 @@ def ipv4_frames(batch: PacketBatch, out2: torch.Tensor | None = None, status: to
     return out2[: 2 * n].view(n, 2) if n else out2[:0].view(0, 2)
 
 
+def fragments(data: torch.Tensor, bytes_len: int, frag_off: torch.Tensor, frag_len: torch.Tensor,
+              pkt_first: torch.Tensor, seeds: torch.Tensor | None = None, out: torch.Tensor | None = None,
+              status: torch.Tensor | None = None, max_frag_len: int = 0, stream=None) -> torch.Tensor:
+    """sccsum_fragments: one checksum per fragment-list packet (int16 tensor)."""
+    lib = native.load()
+    n = int(pkt_first.numel()) - 1
+    nfrag = int(frag_off.numel())
+    if out is None:
+        out = torch.empty(max(n, 1), dtype=torch.int16, device=data.device)
+    ws = torch.empty(int(lib.sccsum_fragments_workspace(nfrag)), dtype=torch.uint8, device=data.device)
+    code = lib.sccsum_fragments(
+        ctypes_ptr(data), bytes_len, ctypes_ptr(frag_off), ctypes_ptr(frag_len), nfrag, ctypes_ptr(pkt_first),
+        _ptr(seeds), ctypes_ptr(out), _ptr(status), n, max_frag_len, ctypes_ptr(ws), _stream(stream))
+    native.check(code, "sccsum_fragments")
+    return out[:n]
+
+
 def read_probe(buf: torch.Tensor, nbytes: int, sink: torch.Tensor | None = None, stream=None) -> torch.Tensor:
     """Stream-read nbytes of buf with the kernels' load shape (HBM ceiling probe)."""
     lib = native.load()

@@ -39,6 +39,7 @@ constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kBlocksPerCU = 8;  // 32 waves/CU: needs <= 64 VGPRs
 constexpr int kMaxDevices = 64;
+constexpr uint32_t kFlagRaw = 1;  // spans: output the folded span-relative sum (no seed, no complement)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -110,7 +111,8 @@ __global__ __launch_bounds__(kBlock) void csum_kernel(
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
     const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
-    uint8_t* __restrict__ status, uint64_t n) {
+    uint8_t* __restrict__ status, uint64_t n, uint32_t flags) {
+    const bool raw = !IPV4 && (flags & kFlagRaw);
     const int lane = static_cast<int>(threadIdx.x & (kWave - 1));
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
@@ -213,10 +215,10 @@ __global__ __launch_bounds__(kBlock) void csum_kernel(
         if (addr & 1u) S = swap16(S);  // span starts at an odd address (4*ihl is even)
         if (IPV4) {
             S = fold16(static_cast<uint64_t>(S) + pseudo);
-        } else if (seed) {
+        } else if (seed && !raw) {
             S = fold16(static_cast<uint64_t>(S) + swap16(fold16(seed[p])));
         }
-        const uint32_t r = ~S & 0xffffu;
+        const uint32_t r = raw ? S : ~S & 0xffffu;
         if (lane == 0) {
             if (IPV4) {
                 reinterpret_cast<uint32_t*>(out)[p] = ipc | (r << 16);
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void csum_kernel(
                 }
             } else {
                 out[p] = static_cast<uint16_t>(r);
-                if (status) status[p] = r == 0 ? SCCSUM_ST_OK : 0u;
+                if (status) status[p] = (!raw && r == 0) ? SCCSUM_ST_OK : 0u;
             }
         }
     }
@@ -344,7 +346,8 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
     const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
-    uint8_t* __restrict__ status, uint64_t n, uint32_t B, uint32_t* __restrict__ heads) {
+    uint8_t* __restrict__ status, uint64_t n, uint32_t B, uint32_t* __restrict__ heads, uint32_t flags) {
+    const bool raw = !IPV4 && (flags & kFlagRaw);
     __shared__ __attribute__((aligned(16))) uint8_t stash_all[kWavesPerBlock][kWave * kStashStride];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -640,9 +643,9 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
             word = ipc | (r << 16);
             st |= (ipc == 0 ? SCCSUM_ST_OK : 0u) | (r == 0 ? SCCSUM_ST_L4_OK : 0u);
         } else {
-            const uint32_t r = ~fold16(static_cast<uint64_t>(S) + swap16(fold16(sd))) & 0xffffu;
+            const uint32_t r = raw ? S : ~fold16(static_cast<uint64_t>(S) + swap16(fold16(sd))) & 0xffffu;
             word = r;
-            st = r == 0 ? SCCSUM_ST_OK : 0u;
+            st = (!raw && r == 0) ? SCCSUM_ST_OK : 0u;
         }
         if (range_bad) {
             word = 0;
@@ -677,9 +680,9 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
                     word = ipc | (r << 16);
                     st = (st & ~SCCSUM_ST_L4_OK) | (r == 0 ? SCCSUM_ST_L4_OK : 0u);
                 } else {
-                    const uint32_t r = ~fold16(static_cast<uint64_t>(SJ) + swap16(fold16(sd))) & 0xffffu;
+                    const uint32_t r = raw ? SJ : ~fold16(static_cast<uint64_t>(SJ) + swap16(fold16(sd))) & 0xffffu;
                     word = r;
-                    st = r == 0 ? SCCSUM_ST_OK : 0u;
+                    st = (!raw && r == 0) ? SCCSUM_ST_OK : 0u;
                 }
             }
         }
@@ -695,6 +698,36 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
         __builtin_amdgcn_wave_barrier();  // stash rows are rewritten by the next tile
         t = t_next;
     }
+}
+
+// Fragment lists (checksummer::sum(const packet&), src/net/ip_checksum.cc:64-68):
+// stage 1 = the span kernel in raw mode gives every fragment's folded sum
+// relative to the fragment's own start; here one thread per packet walks its
+// fragments in order and byte-swaps each sum whose fragment starts at an odd
+// packet-relative offset — the reference's `odd` carry (ip_checksum.cc:33-36,
+// 52) — then adds the seed and complements.
+__global__ __launch_bounds__(kBlock) void frag_combine_kernel(const uint32_t* __restrict__ frag_len, uint64_t nfrag,
+                                                               const uint32_t* __restrict__ pkt_first,
+                                                               const uint16_t* __restrict__ raw,
+                                                               const uint8_t* __restrict__ raw_status,
+                                                               const uint32_t* __restrict__ seed,
+                                                               uint16_t* __restrict__ out,
+                                                               uint8_t* __restrict__ status, uint64_t n) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t f0 = pkt_first[i], f1 = pkt_first[i + 1];
+    bool bad = f1 < f0 || f1 > nfrag;
+    uint64_t S = 0;
+    uint32_t par = 0;
+    for (uint64_t j = f0; !bad && j < f1; ++j) {
+        const uint32_t t = raw[j];
+        bad = (raw_status[j] & SCCSUM_ST_RANGE) != 0;
+        S += par ? swap16(t) : t;
+        par ^= frag_len[j] & 1u;
+    }
+    const uint32_t r = ~fold16(fold16(S) + static_cast<uint64_t>(swap16(fold16(seed ? seed[i] : 0u)))) & 0xffffu;
+    out[i] = bad ? uint16_t(0) : static_cast<uint16_t>(r);
+    if (status) status[i] = bad ? SCCSUM_ST_RANGE : (r == 0 ? SCCSUM_ST_OK : 0u);
 }
 
 // Plain stream-read of the same load shape (16 B per lane, nontemporal).
@@ -802,10 +835,11 @@ std::atomic<int> g_variant{0};
 
 template <int U, bool IPV4>
 void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
-              const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n) {
+              const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
+              uint32_t flags) {
     if (variant == 1) {
         csum_kernel<U, IPV4>
-            <<<dim3(grid_for(n)), dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
+            <<<dim3(grid_for(n)), dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
         return;
     }
     // batch kernel: tiles of B <= 64 packets, enough tiles to fill every wave slot
@@ -821,35 +855,35 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     switch (variant) {
         case 8:
             csum_batch_kernel<U, IPV4, false, kNT, false, true>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
             break;
         case 9:
             csum_batch_kernel<U, IPV4, false, kNT, true, true>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
             break;
         case 6:
             csum_batch_kernel<U, IPV4, false, kNT, true, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
             break;
         case 7:
             csum_batch_kernel<U, IPV4, true, kNT, true, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
             break;
         case 2:
             csum_batch_kernel<U, IPV4, false, kNT, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
             break;
         case 4:
             csum_batch_kernel<U, IPV4, false, 0, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
             break;
         case 5:
             csum_batch_kernel<U, IPV4, true, 0, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
             break;
         default:
             csum_batch_kernel<U, IPV4, true, kNT, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads);
+                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
             break;
     }
 }
@@ -857,7 +891,7 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
 template <bool IPV4>
 int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
            const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n, uint32_t max_len,
-           void* stream) {
+           void* stream, uint32_t flags = 0) {
     if (n == 0) return SCCSUM_OK;
     if (!d_bytes || !d_off || !d_len || !d_out) return SCCSUM_EINVAL;
     if ((reinterpret_cast<uintptr_t>(d_bytes) & 15u) || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
@@ -875,16 +909,16 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
     const int uc = variant == 1 ? units_class(max_len) : (forced ? forced : 2);
     switch (uc) {
         case 1:
-            launch_u<1, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
+            launch_u<1, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
             break;
         case 2:
-            launch_u<2, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
+            launch_u<2, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
             break;
         case 4:
-            launch_u<4, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
+            launch_u<4, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
             break;
         default:
-            launch_u<8, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n);
+            launch_u<8, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
             break;
     }
     return static_cast<int>(hipGetLastError());
@@ -939,6 +973,30 @@ int sccsum_spans(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off,
 int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
                        uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len, void* stream) {
     return sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len, stream);
+}
+
+uint64_t sccsum_fragments_workspace(uint64_t nfrag) { return ((2 * nfrag + 15) & ~uint64_t(15)) + nfrag + 16; }
+
+int sccsum_fragments(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_frag_off, const uint32_t* d_frag_len,
+                     uint64_t nfrag, const uint32_t* d_pkt_first, const uint32_t* d_seed, uint16_t* d_out,
+                     uint8_t* d_status, uint64_t n, uint32_t max_frag_len, void* d_workspace, void* stream) {
+    if (n == 0) return SCCSUM_OK;
+    if (!d_pkt_first || !d_out || (nfrag && (!d_workspace || !d_frag_off || !d_frag_len)) ||
+        (reinterpret_cast<uintptr_t>(d_workspace) & 15u) || (reinterpret_cast<uintptr_t>(d_pkt_first) & 3u) ||
+        (reinterpret_cast<uintptr_t>(d_seed) & 3u) || (reinterpret_cast<uintptr_t>(d_out) & 1u)) {
+        return SCCSUM_EINVAL;
+    }
+    auto* raw = static_cast<uint16_t*>(d_workspace);
+    auto* raw_st = static_cast<uint8_t*>(d_workspace) + ((2 * nfrag + 15) & ~uint64_t(15));
+    if (nfrag) {
+        const int rc = sccsum::launch<false>(d_bytes, bytes_len, d_frag_off, d_frag_len, nullptr, raw, raw_st, nfrag,
+                                             max_frag_len, stream, sccsum::kFlagRaw);
+        if (rc != SCCSUM_OK) return rc;
+    }
+    const unsigned grid = static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock);
+    sccsum::frag_combine_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, static_cast<hipStream_t>(stream)>>>(
+        d_frag_len, nfrag, d_pkt_first, raw, raw_st, d_seed, d_out, d_status, n);
+    return static_cast<int>(hipGetLastError());
 }
 
 int sccsum_set_kernel_variant(int variant) {

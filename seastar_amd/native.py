@@ -51,6 +51,8 @@ _PROTOS = {
     "sccsum_spans": (ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),
     "sccsum_ipv4_frames": (ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),
     "sccsum_sync": (ctypes.c_int, [_vp]),
+    "sccsum_fragments": (ctypes.c_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _u32, _vp, _vp]),
+    "sccsum_fragments_workspace": (_u64, [_u64]),
     "sccsum_set_kernel_variant": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_blocks_per_cu": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_group_units": (ctypes.c_int, [ctypes.c_int]),

@@ -65,3 +65,11 @@ def test_argument_validation_without_device():
     # misaligned out2 for frames (needs 4-byte alignment)
     assert lib.sccsum_ipv4_frames(16, 64, 0x1000, 0x2000, 0x3002, None, 3, 0, None) == native.SCCSUM_EINVAL
     assert lib.sccsum_read_probe(None, 16, None, None) == native.SCCSUM_EINVAL
+    # fragment lists: empty is a no-op; missing workspace / misaligned workspace rejected
+    assert lib.sccsum_fragments(None, 0, None, None, 0, None, None, None, None, 0, 0, None, None) == 0
+    assert lib.sccsum_fragments(16, 64, 0x1000, 0x2000, 4, 0x3000, None, 0x4000, None, 2, 0, None, None) \
+        == native.SCCSUM_EINVAL
+    assert lib.sccsum_fragments(16, 64, 0x1000, 0x2000, 4, 0x3000, None, 0x4000, None, 2, 0, 0x5008, None) \
+        == native.SCCSUM_EINVAL
+    assert lib.sccsum_fragments_workspace(0) >= 16
+    assert lib.sccsum_fragments_workspace(1000) >= 3 * 1000

@@ -278,3 +278,76 @@ def test_host_pipeline_mbuf_pool(dev, gather, kernel_variant):
     got2 = pl.run(native.PIPE_SPANS, pool, poff, plen, seeds=seeds, gather=gather)
     assert np.array_equal(got2, oracle.batch_spans(pool, poff, plen, seeds))
     pl.close()
+
+
+def _frag_batch(rng, n, sizes_fn, scatter=True):
+    """n packets as fragment lists; fragments placed at random (odd included)
+    offsets of one buffer, in shuffled order when scatter."""
+    frag_len = []
+    pkt_first = [0]
+    for i in range(n):
+        sizes = sizes_fn(i)
+        frag_len.extend(sizes)
+        pkt_first.append(len(frag_len))
+    frag_len = np.array(frag_len, np.uint32)
+    order = rng.permutation(frag_len.size) if scatter else np.arange(frag_len.size)
+    off = np.empty(frag_len.size, np.uint64)
+    pos = 0
+    for j in order:
+        pos += int(rng.integers(0, 4))
+        off[j] = pos
+        pos += int(frag_len[j])
+    buf = rng.integers(0, 256, size=pos + 1, dtype=np.uint8)
+    return buf, off, frag_len, np.array(pkt_first, np.uint32)
+
+
+@pytest.mark.parametrize("shape", ["packet_test", "odd_chains", "dpdk_segments", "single"])
+def test_fragment_lists(dev, shape):
+    """GPU checksummer::sum(const packet&): odd carries across fragments."""
+    rng = np.random.default_rng({"packet_test": 1, "odd_chains": 2, "dpdk_segments": 3, "single": 4}[shape])
+    if shape == "packet_test":  # tests/unit/packet_test.cc:32-84 sizes, with trims
+        base = [[5, 31, 65, 4096, 4096], [4, 25, 36, 3072, 4096], [1, 31, 65], [5], [0, 7]]
+        fn = lambda i: base[i % len(base)]
+    elif shape == "odd_chains":
+        fn = lambda i: list(rng.integers(0, 40, size=int(rng.integers(1, 9))))
+    elif shape == "dpdk_segments":  # jumbo frames in 2048-B data rooms (dpdk.cc:147-156)
+        fn = lambda i: ([2048] * (int(L) // 2048) + [int(L) % 2048]) if (L := rng.integers(64, 9001)) else [0]
+    else:
+        fn = lambda i: [int(rng.integers(0, 3000))]
+    n = 700
+    buf, off, flen, first = _frag_batch(rng, n, fn)
+    seeds = rng.integers(0, 65536, size=n).astype(np.uint32)
+    d = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    got = batch.fragments(d, buf.size, torch.from_numpy(off.view(np.int64)).to(dev),
+                          torch.from_numpy(flen.view(np.int32)).to(dev), torch.from_numpy(first.view(np.int32)).to(dev),
+                          seeds=torch.from_numpy(seeds.view(np.int32)).to(dev), status=st, max_frag_len=4096)
+    torch.cuda.synchronize()
+    want = oracle.batch_fragments(buf, off, flen, first, seeds)
+    assert np.array_equal(batch.as_u16(got), want)
+    assert np.array_equal(st.cpu().numpy(), (want == 0).astype(np.uint8))
+    # fragments of a contiguous packet == the contiguous span
+    if shape == "odd_chains":
+        got2 = batch.fragments(d, buf.size, torch.from_numpy(off.view(np.int64)).to(dev),
+                               torch.from_numpy(flen.view(np.int32)).to(dev),
+                               torch.from_numpy(first.view(np.int32)).to(dev))
+        assert np.array_equal(batch.as_u16(got2), oracle.batch_fragments(buf, off, flen, first))
+
+
+def test_fragment_lists_range(dev):
+    """A fragment past bytes_len (or a bad pkt_first) marks only its packet RANGE."""
+    rng = np.random.default_rng(9)
+    buf, off, flen, first = _frag_batch(rng, 64, lambda i: [3, 1500, 7], scatter=False)
+    off = off.copy()
+    off[3 * 10 + 1] = buf.size - 100  # packet 10's middle fragment overruns
+    d = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(dev)
+    st = torch.empty(64, dtype=torch.uint8, device=dev)
+    got = batch.as_u16(batch.fragments(d, buf.size, torch.from_numpy(off.view(np.int64)).to(dev),
+                                       torch.from_numpy(flen.view(np.int32)).to(dev),
+                                       torch.from_numpy(first.view(np.int32)).to(dev), status=st))
+    stn = st.cpu().numpy()
+    assert stn[10] == 8 and got[10] == 0
+    ok = np.arange(64) != 10
+    want = oracle.batch_fragments(buf, off, flen, first)
+    assert np.array_equal(got[ok], want[ok])
+    assert np.all(stn[ok] & 8 == 0)
