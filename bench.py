@@ -46,9 +46,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc", default=None, help="PMC summary JSON for roofline.traffic (default: newest in profiles/)")
-    ap.add_argument("--config", default="udp1500", choices=["udp1500", "mixed", "tcp64k", "e2e"],
+    ap.add_argument("--config", default="udp1500", choices=["udp1500", "mixed", "tcp64k", "e2e", "fill"],
                     help="udp1500 = the metric's config (cfg 2, default); mixed = cfg 3; tcp64k = cfg 4 "
-                         "(per-GPU shard); e2e = cfg 5 (pinned host mbufs, PCIe-inclusive)")
+                         "(per-GPU shard); e2e = cfg 5 (pinned host mbufs, PCIe-inclusive); fill = cfg 2 tx "
+                         "generate with in-place write-back (sccsum_ipv4_fill)")
     return ap.parse_args()
 
 
@@ -238,6 +239,32 @@ def run_mixed(args, world, rank, dev):
               "avg_launch_us": round(launch_s * 1e6, 2)})
 
 
+def run_fill(args, world, rank, dev):
+    """cfg 2 tx side with in-place write-back: IPv4 header +
+    UDP checksums generated and stored into the frames (wire-ready), every
+    step over the same 1 M x 1500 B batch (generate ignores the fields' old
+    contents, so repeated steps are identical work)."""
+    n = args.packets
+    b = devsynth.udp_frames(n, FRAME, seed=SEED + 7 * rank, device=dev)
+    mode = native.FILL_IP | native.FILL_L4
+    batch.ipv4_fill(b, mode)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    batch.ipv4_frames(b, status=st)
+    torch.cuda.synchronize()
+    assert int((st != 3).sum()) == 0, "filled frames do not verify"
+    stream = torch.cuda.current_stream()
+    wall, launch_s = timed(lambda: batch.ipv4_fill(b, mode, stream=stream), args.steps, args.warmup, world, stream)
+    alg = n * (FRAME + META_BYTES + 4)  # read every byte + metadata, write the two 2-byte fields
+    if rank == 0:
+        line("GiB/s device-resident Internet checksum, 1500B-packet batches, in-place generate (cfg 2 tx)",
+             world * n * FRAME * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
+             {"workload": "cfg2 tx: 1500 B IPv4/UDP frames, IP + UDP checksums generated and stored in place",
+              "packets_per_gpu": n, "parallelism": f"{world} independent shards"},
+             {"bound": "hbm", "achieved": round(alg / launch_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+              "frac": round(alg / launch_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+              "avg_launch_us": round(launch_s * 1e6, 2)})
+
+
 def run_e2e(args, world, rank, dev):
     """cfg 5: frames in a pinned, DPDK-mbuf-shaped host pool (2304-B slots,
     data at +256); chunks H2D on a copy stream, kernel on a compute stream,
@@ -286,7 +313,7 @@ def main():
     world, rank, local = dist_setup()
     dev = torch.device("cuda", local)
     if args.config != "udp1500":
-        {"tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e}[args.config](args, world, rank, dev)
+        {"tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e, "fill": run_fill}[args.config](args, world, rank, dev)
         if world > 1:
             import torch.distributed as dist
 

@@ -134,6 +134,34 @@ int sccsum_fragments(const void* d_bytes, uint64_t bytes_len,
                      void* d_workspace, void* stream);
 uint64_t sccsum_fragments_workspace(uint64_t nfrag);
 
+/* sccsum_ipv4_fill modes */
+#define SCCSUM_FILL_IP        0x01u /* IPv4 header checksum, field at +10 (ip.cc:266-278) */
+#define SCCSUM_FILL_L4        0x02u /* full TCP/UDP checksum: pseudo-header + segment (udp.cc:190-192,
+                                       tcp.hh:1691-1692 without tx offload) */
+#define SCCSUM_FILL_L4_PSEUDO 0x04u /* tx-offload partial: the folded pseudo-header alone, i.e. the
+                                       reference's `~csum.get()` (udp.cc:188-189, tcp.hh:1688-1689) */
+#define SCCSUM_FILL_TSO       0x08u /* with L4_PSEUDO: TCP pseudo-header length 0 (tcp.hh:1674-1676) */
+
+/* GENERATE checksums for n IPv4 frames and STORE them in the frames, in
+ * place: wire-ready frames, the tx half of the native stack.  Each checksum
+ * is computed as if its own field were zero, as the reference does (fresh
+ * headers are value-initialised, packet.hh:586-589; ip.cc:270), so the
+ * fields' current contents do not matter.  The L4 field is UDP +6 / TCP +16
+ * after 4*ihl; other protocols' L4 is left alone, as is any frame that is
+ * malformed (as in sccsum_ipv4_frames) or too short to hold the field.
+ *   mode: SCCSUM_FILL_IP and/or one of SCCSUM_FILL_L4 / SCCSUM_FILL_L4_PSEUDO
+ *         (| SCCSUM_FILL_TSO).  FILL_L4 reads every byte (batch kernel);
+ *         the others read only the 20-byte header.
+ *   d_out2[2i] / [2i+1] = the IP / L4 values stored (0 where nothing was
+ *         stored); may be NULL.
+ *   d_status[i] = SCCSUM_ST_OK if the IP field was written, SCCSUM_ST_L4_OK
+ *         if the L4 field was written, plus MALFORMED / RANGE; may be NULL.
+ * Frames must not overlap each other. */
+int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len,
+                     const uint64_t* d_off, const uint32_t* d_len,
+                     uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len,
+                     uint32_t mode, void* stream);
+
 /* Diagnostic: select the kernel family for later launches in this process
  * (0 = default (6 when max_len <= 2048, else 8), 1 = one-packet-per-wave
  * loop, 2 = batch kernel, 3 = batch

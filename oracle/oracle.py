@@ -52,6 +52,7 @@ def lib():
             "oracle_batch_spans": (None, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int]),
             "oracle_batch_ipv4": (None, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int]),
             "oracle_batch_fragments": (None, [_P, _P, _P, _P, _P, _P, ctypes.c_uint64]),
+            "oracle_batch_ipv4_fill": (None, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_uint32]),
         }
         for name, (res, args) in protos.items():
             fn = getattr(L, name)
@@ -128,3 +129,15 @@ def batch_fragments(buf, frag_off, frag_len, pkt_first, seeds=None) -> np.ndarra
     lib().oracle_batch_fragments(_addr(buf), _addr(frag_off), _addr(frag_len), _addr(pkt_first), _addr(seeds),
                                  _addr(out), n)
     return out
+
+
+def batch_ipv4_fill(buf, off, length, mode):
+    """Tx generate in place on a COPY of buf: returns (frames, out2 [n,2], status)."""
+    buf = np.array(buf, dtype=np.uint8, copy=True)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    n = off.size
+    out2 = np.empty(2 * n, dtype=np.uint16)
+    st = np.empty(n, dtype=np.uint8)
+    lib().oracle_batch_ipv4_fill(_addr(buf), _addr(off), _addr(length), _addr(out2), _addr(st), n, mode)
+    return buf, out2.reshape(n, 2), st

@@ -263,3 +263,59 @@ void oracle_batch_fragments(const uint8_t* bytes, const uint64_t* frag_off, cons
         out[i] = oracle_get(&c);
     }
 }
+
+/* Tx generate in place (see the header for the reference lines). */
+void oracle_batch_ipv4_fill(uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+                            uint16_t* out2, uint8_t* status, uint64_t n, uint32_t mode) {
+    for (uint64_t i = 0; i < n; ++i) {
+        uint8_t* p = bytes + off[i];
+        uint32_t L = len[i];
+        uint16_t ipw = 0, l4w = 0;
+        uint8_t st = 0;
+        if (L < 20) {
+            st = 4;
+        } else {
+            uint32_t ihl = p[0] & 0xf;
+            uint32_t ip_len = ((uint32_t)p[2] << 8) | p[3];
+            uint8_t proto = p[9];
+            uint32_t l4_off = 4 * ihl;
+            uint32_t l4_end = ip_len < L ? ip_len : L;
+            uint32_t l4_len = 0;
+            if (L < ip_len) st |= 4;
+            if (l4_off > l4_end) {
+                st |= 4;
+            } else {
+                l4_len = l4_end - l4_off;
+            }
+            if (mode & 1) {
+                p[10] = p[11] = 0;
+                ipw = oracle_ip_checksum(p, 20);
+                memcpy(p + 10, &ipw, 2);
+                st |= 1;
+            }
+            uint32_t fo = proto == 17 ? 6 : (proto == 6 ? 16 : 0);
+            if ((mode & 6) && fo && l4_len >= fo + 2 && !(st & 4)) {
+                uint8_t* field = p + l4_off + fo;
+                oracle_checksummer c;
+                oracle_init(&c);
+                if (mode & 2) {
+                    field[0] = field[1] = 0;
+                    oracle_pseudo_header(&c, rd_be32(p + 12), rd_be32(p + 16), proto, (uint16_t)l4_len);
+                    oracle_sum_bytes(&c, p + l4_off, l4_len);
+                    l4w = oracle_get(&c);
+                } else {
+                    uint32_t plen = ((mode & 8) && proto == 6) ? 0 : l4_len;
+                    oracle_pseudo_header(&c, rd_be32(p + 12), rd_be32(p + 16), proto, (uint16_t)plen);
+                    l4w = (uint16_t)~oracle_get(&c);
+                }
+                memcpy(field, &l4w, 2);
+                st |= 2;
+            }
+        }
+        if (out2) {
+            out2[2 * i] = ipw;
+            out2[2 * i + 1] = l4w;
+        }
+        if (status) status[i] = st;
+    }
+}

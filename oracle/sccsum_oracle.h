@@ -80,6 +80,19 @@ void oracle_batch_ipv4(const uint8_t* bytes, const uint64_t* off, const uint32_t
 void oracle_batch_fragments(const uint8_t* bytes, const uint64_t* frag_off, const uint32_t* frag_len,
                             const uint32_t* pkt_first, const uint32_t* seed, uint16_t* out, uint64_t n);
 
+/* Tx generate, in place, for IPv4 frames (the writers the reference runs on
+ * fresh, zero-checksum headers):
+ *   mode & 1: iph->csum = 0; csum.sum(iph, 20); iph->csum = get()      ip.cc:270-276
+ *   mode & 2: L4 field = 0; pseudo-header + csum.sum(segment); get()    udp.cc:186,192-193 / tcp.hh:1683,1691-1694
+ *   mode & 4: L4 field = ~get() of the pseudo-header alone (tx offload) udp.cc:188-189 / tcp.hh:1688-1689
+ *   mode & 8: with 4, TCP pseudo-header length 0 (TSO)                  tcp.hh:1674-1676
+ * L4 field: UDP +6, TCP +16 after 4*ihl; written only for proto 17/6, when
+ * the frame is not malformed (as oracle_batch_ipv4) and the segment holds the
+ * field.  out2 (may be NULL) gets the values stored (0 = none); status bit0 =
+ * IP stored, bit1 = L4 stored, bit2 malformed, bit3 never (no range checks). */
+void oracle_batch_ipv4_fill(uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+                            uint16_t* out2, uint8_t* status, uint64_t n, uint32_t mode);
+
 /* Fold a checksummer csum to a seed value (end-around carry, zero stays zero). */
 uint32_t oracle_fold_seed(const oracle_checksummer* c);
 

@@ -101,6 +101,20 @@ def ipv4_frames(batch: PacketBatch, out2: torch.Tensor | None = None, status: to
     return out2[: 2 * n].view(n, 2) if n else out2[:0].view(0, 2)
 
 
+def ipv4_fill(batch: PacketBatch, mode: int = native.FILL_IP | native.FILL_L4, out2: torch.Tensor | None = None,
+              status: torch.Tensor | None = None, stream=None) -> torch.Tensor | None:
+    """sccsum_ipv4_fill: generate checksums and store them in batch.data in place.
+    Returns the [n, 2] values stored when out2 is given (else None)."""
+    lib = native.load()
+    n = batch.n
+    code = lib.sccsum_ipv4_fill(
+        ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length),
+        _ptr(out2), _ptr(status), n, batch.max_len, mode, _stream(stream),
+    )
+    native.check(code, "sccsum_ipv4_fill")
+    return None if out2 is None else out2[: 2 * n].view(n, 2)
+
+
 def fragments(data: torch.Tensor, bytes_len: int, frag_off: torch.Tensor, frag_len: torch.Tensor,
               pkt_first: torch.Tensor, seeds: torch.Tensor | None = None, out: torch.Tensor | None = None,
               status: torch.Tensor | None = None, max_frag_len: int = 0, stream=None) -> torch.Tensor:

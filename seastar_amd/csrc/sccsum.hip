@@ -39,7 +39,9 @@ constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kBlocksPerCU = 8;  // 32 waves/CU: needs <= 64 VGPRs
 constexpr int kMaxDevices = 64;
-constexpr uint32_t kFlagRaw = 1;  // spans: output the folded span-relative sum (no seed, no complement)
+constexpr uint32_t kFlagRaw = 1;     // spans: output the folded span-relative sum (no seed, no complement)
+constexpr uint32_t kFlagFillL4 = 2;  // frames: generate the TCP/UDP checksum and store it in the frame
+constexpr uint32_t kFlagFillIp = 4;  // frames (with kFlagFillL4): also generate + store the IPv4 header checksum
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -293,7 +295,9 @@ __device__ __forceinline__ uint32_t unit_part(const u32x4& v, int lo, int hi) {
     return sad4_masked(v, lo, hi, 0u);
 }
 
-constexpr uint32_t kStashUnits = 4;     // units 0..2 of a packet (IPv4 header) + its last unit
+constexpr uint32_t kStashHead = 4;      // frames: units 0..3 (IPv4 header + the TCP/UDP checksum field)
+constexpr uint32_t kStashLast = 64;     // byte offset of the packet's last unit in its row
+constexpr uint32_t kStashUnits = 5;     // head units + the last unit
 constexpr uint32_t kStashStride = 80;   // bytes per packet row (5 x 16 B: conflict-free ds_read_b128)
 constexpr uint32_t kExactMax = 131072;  // fast path keeps exact 32-bit sums up to this length
 // tile-head counters: each on its own 256-byte line (atomics to one line
@@ -341,13 +345,16 @@ __device__ uint32_t exact_range_sum(const uint8_t* a0, uint64_t rs, uint64_t re,
 //     pseudo-header, complements; one coalesced store for the tile.
 //  D: packets the fast path cannot take (frames with options or a trimmed
 //     IP length, spans longer than 128 KiB) are redone exactly, one wave each.
-template <int U, bool IPV4, bool PIPE, int AUX, bool HYB, bool MULTI>
+template <int U, bool IPV4, bool PIPE, int AUX, bool HYB, bool MULTI, bool FILL = false>
 __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_kernel(
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
     const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
     uint8_t* __restrict__ status, uint64_t n, uint32_t B, uint32_t* __restrict__ heads, uint32_t flags) {
     const bool raw = !IPV4 && (flags & kFlagRaw);
+    static_assert(!FILL || IPV4, "in-place generate is a frames mode");
+    constexpr bool fill = FILL;                          // generate L4 checksums and store them in place
+    const bool fill_ip = FILL && (flags & kFlagFillIp);  // ... and the IPv4 header checksum
     __shared__ __attribute__((aligned(16))) uint8_t stash_all[kWavesPerBlock][kWave * kStashStride];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -444,7 +451,7 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
             for (int u = 0; u < U; ++u) acc = sad4(P.v[u], acc);
             if (HYB) acc = sad4(P.w, acc);
             uint8_t* row = stash + k * kStashStride;
-            constexpr uint32_t kHead = IPV4 ? 3u : 1u;
+            constexpr uint32_t kHead = FILL ? kStashHead : (IPV4 ? 3u : 1u);
             if (lane < kHead && lane < P.s) *reinterpret_cast<u32x4*>(row + 16u * lane) = P.v[0];
             if (HYB && lane + P.s < kHead) *reinterpret_cast<u32x4*>(row + 16u * (lane + P.s)) = P.w;
             const uint32_t gu = static_cast<uint32_t>(U) * kWave;
@@ -478,17 +485,17 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
                     P.v[u] = w[u];
                 }
             }
-            // last unit of the span -> stash slot 3
+            // last unit of the span -> the row's last slot
             if (P.nu) {
                 const uint32_t last = P.nu - 1;
                 if (HYB) {
-                    if (lane + P.s == last) *reinterpret_cast<u32x4*>(row + 48) = P.w;
+                    if (lane + P.s == last) *reinterpret_cast<u32x4*>(row + kStashLast) = P.w;
                 } else {
                     const uint32_t slot = (last >> 6) % U;
                     u32x4 lu = P.v[0];
 #pragma unroll
                     for (int u = 1; u < U; ++u) lu = slot == static_cast<uint32_t>(u) ? P.v[u] : lu;
-                    if (lane == (last & 63u)) *reinterpret_cast<u32x4*>(row + 48) = lu;
+                    if (lane == (last & 63u)) *reinterpret_cast<u32x4*>(row + kStashLast) = lu;
                 }
             }
             const uint32_t S = wave_sum(acc);
@@ -502,7 +509,7 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
         auto multi = [&](auto npc, uint32_t k) {
             constexpr uint32_t NP = decltype(npc)::value;
             constexpr uint32_t SL = kWave / NP;  // lanes per packet (32 or 16)
-            constexpr uint32_t kHead = IPV4 ? 3u : 1u;
+            constexpr uint32_t kHead = FILL ? kStashHead : (IPV4 ? 3u : 1u);
             const uint32_t seg = lane / SL, j = lane % SL;
             const int src = static_cast<int>(k + seg);
             const uint32_t qlo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(a0)), src));
@@ -526,7 +533,7 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
                 u32x4 lu = v[0];
 #pragma unroll
                 for (int u = 1; u < U; ++u) lu = last / SL == static_cast<uint32_t>(u) ? v[u] : lu;
-                if (j == last % SL) *reinterpret_cast<u32x4*>(row + 48) = lu;
+                if (j == last % SL) *reinterpret_cast<u32x4*>(row + kStashLast) = lu;
             }
             // 16-lane row sums
             acc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc), 0xB1, 0xF, 0xF, false));
@@ -595,21 +602,22 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
         const u32x4 s0 = *reinterpret_cast<const u32x4*>(row);
         const u32x4 s1 = *reinterpret_cast<const u32x4*>(row + 16);
         const u32x4 s2 = *reinterpret_cast<const u32x4*>(row + 32);
-        const u32x4 s3 = *reinterpret_cast<const u32x4*>(row + 48);
+        const u32x4 s3 = *reinterpret_cast<const u32x4*>(row + kStashLast);
         const int lastu16 = 16 * (static_cast<int>(nunits) - 1);
         uint32_t excl = unit_part(s0, 0, rs0);
         if (IPV4) {
             excl += unit_part(s1, 0, rs0 - 16) + unit_part(s2, 0, rs0 - 32);
         }
         excl += unit_part(s3, re0 - lastu16, 16);
-        // a unit that is both among 0..2 and the last one is excluded twice,
+        // a unit that is both a head unit and the last one is excluded twice,
         // but on disjoint byte ranges ([0, rs) and [re, 16)).
         const uint32_t kept = nunits ? res - excl : 0u;
         uint32_t S = fold16(kept);
         if (head & 1u) S = swap16(S);
         uint32_t word = 0, st = 0;
         bool slow = huge && mine && !range_bad;
-        uint32_t ipc = 0, pseudo = 0;
+        uint32_t ipc = 0, pseudo = 0, fo = 0;
+        bool has_field = false;
         int srs = 0, sre = 0;
         if (IPV4) {
             // header dwords at byte `head` of the stash row
@@ -621,7 +629,8 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
             const uint32_t h2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
             const uint32_t h3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
             const uint32_t h4 = __builtin_amdgcn_alignbyte(d5, d4, sh);
-            ipc = ~fold16(static_cast<uint64_t>(h0) + h1 + h2 + h3 + h4) & 0xffffu;
+            // generate (fill) treats the header checksum field (bytes 10-11) as zero (ip.cc:270-276)
+            ipc = ~fold16(static_cast<uint64_t>(h0) + h1 + (fill ? h2 & 0xffffu : h2) + h3 + h4) & 0xffffu;
             const uint32_t ihl = h0 & 0xfu;
             const uint32_t ip_len = swap16(h0 >> 16);
             const uint32_t proto = (h2 >> 8) & 0xffu;
@@ -639,9 +648,25 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
             slow = slow || (fast && (ihl != 5u || ip_len != L));
             srs = static_cast<int>(head + l4_off);
             sre = srs + static_cast<int>(l4_len);
-            const uint32_t r = ~fold16(static_cast<uint64_t>(S) + pseudo) & 0xffffu;
-            word = ipc | (r << 16);
-            st |= (ipc == 0 ? SCCSUM_ST_OK : 0u) | (r == 0 ? SCCSUM_ST_L4_OK : 0u);
+            if (fill) {
+                // the L4 checksum field (UDP +6, udp.cc:184-195; TCP +16, tcp.hh:283-285) counts as
+                // zero: subtract its current value (ones' complement: add ~field).  The pseudo-header
+                // is never zero, so the fold lands in [1, 0xffff] exactly like the reference's.
+                fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
+                has_field = fo != 0u && l4_len >= fo + 2u && (st & SCCSUM_ST_MALFORMED) == 0u;
+                uint32_t fv = 0;
+                if (has_field && !slow) {
+                    const uint32_t fb = head + 20u + fo;  // ihl == 5 here: inside head units 0..3
+                    fv = static_cast<uint32_t>(row[fb]) | (static_cast<uint32_t>(row[fb + 1]) << 8);
+                }
+                const uint32_t r = ~fold16(static_cast<uint64_t>(S) + pseudo + (~fv & 0xffffu)) & 0xffffu;
+                word = (fill_ip ? ipc : 0u) | (has_field ? r << 16 : 0u);
+                st |= (fill_ip ? SCCSUM_ST_OK : 0u) | (has_field ? SCCSUM_ST_L4_OK : 0u);
+            } else {
+                const uint32_t r = ~fold16(static_cast<uint64_t>(S) + pseudo) & 0xffffu;
+                word = ipc | (r << 16);
+                st |= (ipc == 0 ? SCCSUM_ST_OK : 0u) | (r == 0 ? SCCSUM_ST_L4_OK : 0u);
+            }
         } else {
             const uint32_t r = raw ? S : ~fold16(static_cast<uint64_t>(S) + swap16(fold16(sd))) & 0xffffu;
             word = r;
@@ -675,7 +700,14 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
             uint32_t SJ = exact_range_sum(ja0, rs, re, lane);
             if (jhead & 1u) SJ = swap16(SJ);
             if (lane == j) {
-                if (IPV4) {
+                if (IPV4 && fill) {
+                    if (has_field) {
+                        const uint8_t* fp = ja0 + rs + fo;
+                        const uint32_t fv = static_cast<uint32_t>(fp[0]) | (static_cast<uint32_t>(fp[1]) << 8);
+                        const uint32_t r = ~fold16(static_cast<uint64_t>(SJ) + pseudo + (~fv & 0xffffu)) & 0xffffu;
+                        word = (word & 0xffffu) | (r << 16);
+                    }
+                } else if (IPV4) {
                     const uint32_t r = ~fold16(static_cast<uint64_t>(SJ) + pseudo) & 0xffffu;
                     word = ipc | (r << 16);
                     st = (st & ~SCCSUM_ST_L4_OK) | (r == 0 ? SCCSUM_ST_L4_OK : 0u);
@@ -687,9 +719,22 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
             }
         }
 
+        if (fill && mine && !range_bad && !short_frame) {
+            // in-place write-back: wire-ready frames (network-order bytes = the LE store of the sum)
+            uint8_t* wp = const_cast<uint8_t*>(ptr);
+            if (fill_ip) {
+                wp[10] = static_cast<uint8_t>(word);
+                wp[11] = static_cast<uint8_t>(word >> 8);
+            }
+            if (has_field) {
+                const uint32_t fb = static_cast<uint32_t>(srs) - head + fo;
+                wp[fb] = static_cast<uint8_t>(word >> 16);
+                wp[fb + 1] = static_cast<uint8_t>(word >> 24);
+            }
+        }
         if (mine) {
             if (IPV4) {
-                reinterpret_cast<uint32_t*>(out)[base + lane] = word;
+                if (out) reinterpret_cast<uint32_t*>(out)[base + lane] = word;
             } else {
                 out[base + lane] = static_cast<uint16_t>(word);
             }
@@ -728,6 +773,67 @@ __global__ __launch_bounds__(kBlock) void frag_combine_kernel(const uint32_t* __
     const uint32_t r = ~fold16(fold16(S) + static_cast<uint64_t>(swap16(fold16(seed ? seed[i] : 0u)))) & 0xffffu;
     out[i] = bad ? uint16_t(0) : static_cast<uint16_t>(r);
     if (status) status[i] = bad ? SCCSUM_ST_RANGE : (r == 0 ? SCCSUM_ST_OK : 0u);
+}
+
+// Header-only generate (no payload bytes read): the IPv4 header checksum
+// (ip.cc:266-278) and/or the tx-offload partial that a NIC completes — the
+// folded pseudo-header stored in the L4 field (udp.cc:188-189, tcp.hh:1688-1689,
+// `~csum.get()` of the pseudo-header alone; TSO: length 0 for TCP).
+// One thread per frame.
+__global__ __launch_bounds__(kBlock) void fill_header_kernel(uint8_t* __restrict__ bytes, uint64_t bytes_len,
+                                                             const uint64_t* __restrict__ off,
+                                                             const uint32_t* __restrict__ len,
+                                                             uint32_t* __restrict__ out2,
+                                                             uint8_t* __restrict__ status, uint64_t n, uint32_t mode) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t o = off[i];
+    const uint32_t L = len[i];
+    uint32_t word = 0, st = 0;
+    if (o > bytes_len || L > bytes_len - o) {
+        st = SCCSUM_ST_RANGE;
+    } else if (L < 20u) {
+        st = SCCSUM_ST_MALFORMED;
+    } else {
+        uint8_t* p = bytes + o;
+        uint32_t h[10];  // little-endian 16-bit words of the 20-byte header
+#pragma unroll
+        for (int k = 0; k < 10; ++k) h[k] = static_cast<uint32_t>(p[2 * k]) | (static_cast<uint32_t>(p[2 * k + 1]) << 8);
+        const uint32_t ihl = p[0] & 0xfu;
+        const uint32_t ip_len = (static_cast<uint32_t>(p[2]) << 8) | p[3];
+        const uint32_t proto = p[9];
+        const uint32_t l4_off = 4u * ihl;
+        const uint32_t l4_end = ip_len < L ? ip_len : L;
+        uint32_t l4_len = 0;
+        if (L < ip_len) st |= SCCSUM_ST_MALFORMED;
+        if (l4_off > l4_end) {
+            st |= SCCSUM_ST_MALFORMED;
+        } else {
+            l4_len = l4_end - l4_off;
+        }
+        if (mode & SCCSUM_FILL_IP) {
+            const uint32_t ipc =
+                ~fold16(static_cast<uint64_t>(h[0]) + h[1] + h[2] + h[3] + h[4] + h[6] + h[7] + h[8] + h[9]) & 0xffffu;
+            p[10] = static_cast<uint8_t>(ipc);
+            p[11] = static_cast<uint8_t>(ipc >> 8);
+            word |= ipc;
+            st |= SCCSUM_ST_OK;
+        }
+        if (mode & SCCSUM_FILL_L4_PSEUDO) {
+            const uint32_t fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
+            if (fo != 0u && l4_len >= fo + 2u && (st & SCCSUM_ST_MALFORMED) == 0u) {
+                const uint32_t plen = ((mode & SCCSUM_FILL_TSO) && proto == 6u) ? 0u : l4_len;
+                const uint32_t ps = fold16(static_cast<uint64_t>(h[6]) + h[7] + h[8] + h[9] + (proto << 8) +
+                                           swap16(plen & 0xffffu));
+                p[l4_off + fo] = static_cast<uint8_t>(ps);
+                p[l4_off + fo + 1] = static_cast<uint8_t>(ps >> 8);
+                word |= ps << 16;
+                st |= SCCSUM_ST_L4_OK;
+            }
+        }
+    }
+    if (out2) out2[i] = word;
+    if (status) status[i] = static_cast<uint8_t>(st);
 }
 
 // Plain stream-read of the same load shape (16 B per lane, nontemporal).
@@ -852,6 +958,18 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     const uint32_t b32 = static_cast<uint32_t>(B);
     uint32_t* heads = nullptr;
     if (g_dynamic.load(std::memory_order_relaxed)) heads = next_heads();
+    if constexpr (IPV4) {
+        if (flags & kFlagFillL4) {
+            if (variant == 8 || variant == 9) {
+                csum_batch_kernel<U, true, false, kNT, false, true, true><<<grid, dim3(kBlock), 0, s>>>(
+                    b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
+            } else {
+                csum_batch_kernel<U, true, false, kNT, true, false, true><<<grid, dim3(kBlock), 0, s>>>(
+                    b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
+            }
+            return;
+        }
+    }
     switch (variant) {
         case 8:
             csum_batch_kernel<U, IPV4, false, kNT, false, true>
@@ -893,7 +1011,7 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
            const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n, uint32_t max_len,
            void* stream, uint32_t flags = 0) {
     if (n == 0) return SCCSUM_OK;
-    if (!d_bytes || !d_off || !d_len || !d_out) return SCCSUM_EINVAL;
+    if (!d_bytes || !d_off || !d_len || (!d_out && !(flags & kFlagFillL4))) return SCCSUM_EINVAL;
     if ((reinterpret_cast<uintptr_t>(d_bytes) & 15u) || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
         (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_seed) & 3u) ||
         (reinterpret_cast<uintptr_t>(d_out) & (IPV4 ? 3u : 1u))) {
@@ -901,6 +1019,7 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
     }
     int variant = g_variant.load(std::memory_order_relaxed);
     if (variant == 0) variant = (max_len != 0 && max_len <= 2048) ? 6 : 8;
+    if (variant == 1 && (flags & kFlagFillL4)) variant = 6;  // in-place write-back lives in the batch kernel
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
     // batch kernel: U = 2 for every size (long packets keep 4 groups in flight
@@ -996,6 +1115,31 @@ int sccsum_fragments(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_
     const unsigned grid = static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock);
     sccsum::frag_combine_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, static_cast<hipStream_t>(stream)>>>(
         d_frag_len, nfrag, d_pkt_first, raw, raw_st, d_seed, d_out, d_status, n);
+    return static_cast<int>(hipGetLastError());
+}
+
+int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
+                     uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len, uint32_t mode,
+                     void* stream) {
+    constexpr uint32_t kAll = SCCSUM_FILL_IP | SCCSUM_FILL_L4 | SCCSUM_FILL_L4_PSEUDO | SCCSUM_FILL_TSO;
+    if (mode == 0 || (mode & ~kAll) || ((mode & SCCSUM_FILL_L4) && (mode & SCCSUM_FILL_L4_PSEUDO)) ||
+        ((mode & SCCSUM_FILL_TSO) && !(mode & SCCSUM_FILL_L4_PSEUDO))) {
+        return SCCSUM_EINVAL;
+    }
+    if (n == 0) return SCCSUM_OK;
+    if (mode & SCCSUM_FILL_L4) {
+        const uint32_t flags = sccsum::kFlagFillL4 | ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u);
+        return sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len, stream,
+                                    flags);
+    }
+    if (!d_bytes || !d_off || !d_len || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
+        (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_out2) & 3u)) {
+        return SCCSUM_EINVAL;
+    }
+    const unsigned grid = static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock);
+    sccsum::fill_header_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<uint8_t*>(d_bytes), bytes_len, d_off, d_len, reinterpret_cast<uint32_t*>(d_out2), d_status, n,
+        mode);
     return static_cast<int>(hipGetLastError());
 }
 

@@ -23,6 +23,10 @@ ST_OK = 0x01
 ST_L4_OK = 0x02
 ST_MALFORMED = 0x04
 ST_RANGE = 0x08
+FILL_IP = 0x01
+FILL_L4 = 0x02
+FILL_L4_PSEUDO = 0x04
+FILL_TSO = 0x08
 
 
 class SccsumError(RuntimeError):
@@ -53,6 +57,7 @@ _PROTOS = {
     "sccsum_sync": (ctypes.c_int, [_vp]),
     "sccsum_fragments": (ctypes.c_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "sccsum_fragments_workspace": (_u64, [_u64]),
+    "sccsum_ipv4_fill": (ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u64, _u32, _u32, _vp]),
     "sccsum_set_kernel_variant": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_blocks_per_cu": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_group_units": (ctypes.c_int, [ctypes.c_int]),

@@ -73,3 +73,14 @@ def test_argument_validation_without_device():
         == native.SCCSUM_EINVAL
     assert lib.sccsum_fragments_workspace(0) >= 16
     assert lib.sccsum_fragments_workspace(1000) >= 3 * 1000
+    # in-place fill: mode checks come first, then n == 0 is a no-op
+    F = native
+    assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, 0, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, F.FILL_L4 | F.FILL_L4_PSEUDO, None) \
+        == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, F.FILL_IP | F.FILL_TSO, None) \
+        == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, 0x10, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, F.FILL_IP | F.FILL_L4, None) == 0
+    assert lib.sccsum_ipv4_fill(None, 64, None, None, None, None, 3, 0, F.FILL_IP, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_fill(None, 64, None, None, None, None, 3, 0, F.FILL_L4, None) == native.SCCSUM_EINVAL
