@@ -312,6 +312,9 @@ constexpr int kLongGroups = SCCSUM_LONG_GROUPS;  // groups in flight per step of
 #ifndef SCCSUM_BATCH_MIN_WAVES
 #define SCCSUM_BATCH_MIN_WAVES 1  // __launch_bounds__ waves per SIMD floor (8 = cap VGPRs at 64)
 #endif
+#ifndef SCCSUM_FILL_MIN_WAVES
+#define SCCSUM_FILL_MIN_WAVES SCCSUM_BATCH_MIN_WAVES
+#endif
 static_assert(kStashStride >= 16 * kStashUnits && kStashStride % 16 == 0, "stash row layout");
 
 // Exact folded sum (little-endian domain relative to a0) of [rs, re), one
@@ -346,7 +349,7 @@ __device__ uint32_t exact_range_sum(const uint8_t* a0, uint64_t rs, uint64_t re,
 //  D: packets the fast path cannot take (frames with options or a trimmed
 //     IP length, spans longer than 128 KiB) are redone exactly, one wave each.
 template <int U, bool IPV4, bool PIPE, int AUX, bool HYB, bool MULTI, bool FILL = false>
-__global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_kernel(
+__global__ __launch_bounds__(kBlock, FILL ? SCCSUM_FILL_MIN_WAVES : SCCSUM_BATCH_MIN_WAVES) void csum_batch_kernel(
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
     const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
@@ -616,8 +619,8 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
         if (head & 1u) S = swap16(S);
         uint32_t word = 0, st = 0;
         bool slow = huge && mine && !range_bad;
-        uint32_t ipc = 0, pseudo = 0, fo = 0;
-        bool has_field = false;
+        uint32_t ipc = 0, pseudo = 0;
+        uint32_t fpos = 0;  // fill: the L4 checksum field's byte offset from a0 (0 = no field to store)
         int srs = 0, sre = 0;
         if (IPV4) {
             // header dwords at byte `head` of the stash row
@@ -652,12 +655,12 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
                 // the L4 checksum field (UDP +6, udp.cc:184-195; TCP +16, tcp.hh:283-285) counts as
                 // zero: subtract its current value (ones' complement: add ~field).  The pseudo-header
                 // is never zero, so the fold lands in [1, 0xffff] exactly like the reference's.
-                fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
-                has_field = fo != 0u && l4_len >= fo + 2u && (st & SCCSUM_ST_MALFORMED) == 0u;
+                const uint32_t fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
+                const bool has_field = fo != 0u && l4_len >= fo + 2u && (st & SCCSUM_ST_MALFORMED) == 0u;
+                fpos = has_field ? static_cast<uint32_t>(srs) + fo : 0u;
                 uint32_t fv = 0;
-                if (has_field && !slow) {
-                    const uint32_t fb = head + 20u + fo;  // ihl == 5 here: inside head units 0..3
-                    fv = static_cast<uint32_t>(row[fb]) | (static_cast<uint32_t>(row[fb + 1]) << 8);
+                if (has_field && !slow) {  // ihl == 5 here: the field is inside head units 0..3
+                    fv = static_cast<uint32_t>(row[fpos]) | (static_cast<uint32_t>(row[fpos + 1]) << 8);
                 }
                 const uint32_t r = ~fold16(static_cast<uint64_t>(S) + pseudo + (~fv & 0xffffu)) & 0xffffu;
                 word = (fill_ip ? ipc : 0u) | (has_field ? r << 16 : 0u);
@@ -701,8 +704,8 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
             if (jhead & 1u) SJ = swap16(SJ);
             if (lane == j) {
                 if (IPV4 && fill) {
-                    if (has_field) {
-                        const uint8_t* fp = ja0 + rs + fo;
+                    if (fpos) {
+                        const uint8_t* fp = reinterpret_cast<const uint8_t*>(a0) + fpos;
                         const uint32_t fv = static_cast<uint32_t>(fp[0]) | (static_cast<uint32_t>(fp[1]) << 8);
                         const uint32_t r = ~fold16(static_cast<uint64_t>(SJ) + pseudo + (~fv & 0xffffu)) & 0xffffu;
                         word = (word & 0xffffu) | (r << 16);
@@ -720,16 +723,18 @@ __global__ __launch_bounds__(kBlock, SCCSUM_BATCH_MIN_WAVES) void csum_batch_ker
         }
 
         if (fill && mine && !range_bad && !short_frame) {
-            // in-place write-back: wire-ready frames (network-order bytes = the LE store of the sum)
-            uint8_t* wp = const_cast<uint8_t*>(ptr);
+            // in-place write-back: wire-ready frames (network-order bytes = the LE store of the sum).
+            // ~1 M scattered 2-byte stores per 1.5 GB batch cost ~75 us on top of the read stream
+            // whatever their form (byte, nontemporal, full 64-byte blocks, a separate pass): HBM
+            // read/write turnarounds, DESIGN.md §5.5.
+            uint8_t* wp = reinterpret_cast<uint8_t*>(a0);
             if (fill_ip) {
-                wp[10] = static_cast<uint8_t>(word);
-                wp[11] = static_cast<uint8_t>(word >> 8);
+                wp[head + 10] = static_cast<uint8_t>(word);
+                wp[head + 11] = static_cast<uint8_t>(word >> 8);
             }
-            if (has_field) {
-                const uint32_t fb = static_cast<uint32_t>(srs) - head + fo;
-                wp[fb] = static_cast<uint8_t>(word >> 16);
-                wp[fb + 1] = static_cast<uint8_t>(word >> 24);
+            if (fpos) {
+                wp[fpos] = static_cast<uint8_t>(word >> 16);
+                wp[fpos + 1] = static_cast<uint8_t>(word >> 24);
             }
         }
         if (mine) {

@@ -94,7 +94,8 @@ def load():
         raise RuntimeError(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
         )
-    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    # SCCSUM_LIB: diagnostic override (A/B builds of the same ABI); still a native library, never a fallback
+    lib = ctypes.CDLL(os.environ.get("SCCSUM_LIB", LIB_PATH), mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in _PROTOS.items():
         fn = getattr(lib, name)
         fn.restype = res
