@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the pre-timing parity check (A/B builds only)")
     ap.add_argument("--pmc", default=None, help="PMC summary JSON for roofline.traffic (default: newest in profiles/)")
+    ap.add_argument("--rotate", type=int, default=4,
+                    help="distinct batches (pairs for udp1500) launched in turn, so no launch replays cached lines")
     ap.add_argument("--config", default="udp1500", choices=["udp1500", "mixed", "tcp64k", "e2e", "fill"],
                     help="udp1500 = the metric's config (cfg 2, default); mixed = cfg 3; tcp64k = cfg 4 "
                          "(per-GPU shard); e2e = cfg 5 (pinned host mbufs, PCIe-inclusive); fill = cfg 2 tx "
@@ -161,16 +163,16 @@ def pmc_traffic(path: str | None, kernel_substr: str):
 def timed(step, steps, warmup, world, stream):
     """Warm up, then time `steps` calls bracketed by barrier + sync; returns
     (max-over-ranks wall seconds, mean seconds per launch from HIP events)."""
-    for _ in range(warmup):
-        step()
+    for k in range(warmup):
+        step(k)
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for e in evs:
+    for k, e in enumerate(evs):
         e[0].record(stream)
-        step()
+        step(k)
         e[1].record(stream)
     torch.cuda.synchronize()
     barrier(world)
@@ -202,7 +204,7 @@ def run_tcp64k(args, world, rank, dev):
     torch.cuda.synchronize()
     assert int((st != 1).sum()) == 0, "tcp64k verify failed"
     stream = torch.cuda.current_stream()
-    wall, launch_s = timed(lambda: batch.spans(b, seeds=seeds, out=out, status=st, stream=stream),
+    wall, launch_s = timed(lambda k: batch.spans(b, seeds=seeds, out=out, status=st, stream=stream),
                            args.steps, args.warmup, world, stream)
     alg = n * (seg + 12 + 4 + 2 + 1)
     if rank == 0:
@@ -222,11 +224,12 @@ def run_mixed(args, world, rank, dev):
 
     n = args.packets if args.packets != (1 << 20) else 3_400_000
     lens = synth.zipf_lengths(n, seed=SEED + rank)
-    b = devsynth.mixed_frames(lens, seed=SEED + 31 * rank, device=dev)
+    R = max(1, args.rotate)  # distinct batches launched in turn (no cached-line replay)
+    bs = [devsynth.mixed_frames(lens, seed=SEED + 31 * rank + 7 * r, device=dev) for r in range(R)]
     out = torch.empty(2 * n, dtype=torch.int16, device=dev)
     stream = torch.cuda.current_stream()
-    wall, launch_s = timed(lambda: batch.ipv4_frames(b, out2=out, stream=stream), args.steps, args.warmup, world,
-                           stream)
+    wall, launch_s = timed(lambda k: batch.ipv4_frames(bs[k % R], out2=out, stream=stream), args.steps,
+                           max(args.warmup, R), world, stream)
     total = int(lens.sum())
     alg = total + n * (12 + 4)
     if rank == 0:
@@ -234,6 +237,7 @@ def run_mixed(args, world, rank, dev):
              world * total * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": "cfg3: Zipf(s=1.2) IPv4/UDP frames 64..9000 B, packed back to back (odd offsets)",
               "packets_per_gpu": n, "bytes_per_gpu": total, "mean_len": round(total / n, 1),
+              "rotation": f"{R} distinct batches launched in turn",
               "parallelism": f"{world} independent shards"},
              {"bound": "hbm", "achieved": round(alg / launch_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
               "frac": round(alg / launch_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
@@ -246,21 +250,25 @@ def run_fill(args, world, rank, dev):
     step over the same 1 M x 1500 B batch (generate ignores the fields' old
     contents, so repeated steps are identical work)."""
     n = args.packets
-    b = devsynth.udp_frames(n, FRAME, seed=SEED + 7 * rank, device=dev)
+    R = max(1, args.rotate)  # distinct batches launched in turn (no cached-line replay)
+    bs = [devsynth.udp_frames(n, FRAME, seed=SEED + 7 * rank + 13 * r, device=dev) for r in range(R)]
     mode = native.FILL_IP | native.FILL_L4
-    batch.ipv4_fill(b, mode)
     st = torch.empty(n, dtype=torch.uint8, device=dev)
-    batch.ipv4_frames(b, status=st)
-    torch.cuda.synchronize()
-    assert args.no_check or int((st != 3).sum()) == 0, "filled frames do not verify"
+    for b in bs:
+        batch.ipv4_fill(b, mode)
+        batch.ipv4_frames(b, status=st)
+        torch.cuda.synchronize()
+        assert args.no_check or int((st != 3).sum()) == 0, "filled frames do not verify"
     stream = torch.cuda.current_stream()
-    wall, launch_s = timed(lambda: batch.ipv4_fill(b, mode, stream=stream), args.steps, args.warmup, world, stream)
+    wall, launch_s = timed(lambda k: batch.ipv4_fill(bs[k % R], mode, stream=stream), args.steps,
+                           max(args.warmup, R), world, stream)
     alg = n * (FRAME + META_BYTES + 4)  # read every byte + metadata, write the two 2-byte fields
     if rank == 0:
         line("GiB/s device-resident Internet checksum, 1500B-packet batches, in-place generate (cfg 2 tx)",
              world * n * FRAME * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": "cfg2 tx: 1500 B IPv4/UDP frames, IP + UDP checksums generated and stored in place",
-              "packets_per_gpu": n, "parallelism": f"{world} independent shards"},
+              "packets_per_gpu": n, "rotation": f"{R} distinct batches launched in turn",
+              "parallelism": f"{world} independent shards"},
              {"bound": "hbm", "achieved": round(alg / launch_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
               "frac": round(alg / launch_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
               "avg_launch_us": round(launch_s * 1e6, 2)})
@@ -322,43 +330,54 @@ def main():
         return
     n = args.packets
 
-    tx = devsynth.udp_frames(n, FRAME, seed=SEED + 7919 * rank, device=dev)
+    # R distinct tx/rx batch pairs launched in turn: 2R x 1.5 GB per rank, so no
+    # launch finds its batch's lines left in the 256 MB MALL by an earlier one
+    # (a replay of one resident batch would measure cache reuse, not streaming)
+    R = max(1, args.rotate)
+    txs, rxs, sts = [], [], []
     out_tx = torch.empty(2 * n, dtype=torch.int16, device=dev)
-    first = batch.ipv4_frames(tx, out2=out_tx)
-    rx = devsynth.store_checksums(tx, first)
+    out_rx = torch.empty(2 * n, dtype=torch.int16, device=dev)
     g = torch.Generator(device=dev)
     g.manual_seed(SEED + rank)
     bad = torch.randperm(n, device=dev, generator=g)[: n // 100]
-    devsynth.corrupt(rx, bad, byte=700)
-    out_rx = torch.empty(2 * n, dtype=torch.int16, device=dev)
-    st_rx = torch.empty(n, dtype=torch.uint8, device=dev)
+    for r in range(R):
+        tx = devsynth.udp_frames(n, FRAME, seed=SEED + 7919 * rank + 104723 * r, device=dev)
+        first = batch.ipv4_frames(tx, out2=out_tx)
+        rx = devsynth.store_checksums(tx, first)
+        devsynth.corrupt(rx, bad, byte=700)
+        txs.append(tx)
+        rxs.append(rx)
+        sts.append(torch.empty(n, dtype=torch.uint8, device=dev))
+    tx = txs[0]
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
 
-    def step(ev=None):
+    def step(k, ev=None):
+        r = k % R
         if ev is not None:
             ev[0].record(stream)
-        batch.ipv4_frames(tx, out2=out_tx, stream=stream)
+        batch.ipv4_frames(txs[r], out2=out_tx, stream=stream)
         if ev is not None:
             ev[1].record(stream)
-        batch.ipv4_frames(rx, out2=out_rx, status=st_rx, stream=stream)
+        batch.ipv4_frames(rxs[r], out2=out_rx, status=sts[r], stream=stream)
         if ev is not None:
             ev[2].record(stream)
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(max(args.warmup, R)):
+        step(k)
     torch.cuda.synchronize()
     # sanity: every uncorrupted rx frame verifies, every corrupted one fails
-    n_fail = int(((st_rx & 2) == 0).sum())
-    assert n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
+    for st_rx in sts:
+        n_fail = int(((st_rx & 2) == 0).sum())
+        assert n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        step(k, evs[k])
     torch.cuda.synchronize()
     barrier(world)
     wall = time.perf_counter() - t0
@@ -388,7 +407,7 @@ def main():
     torch.cuda.synchronize()
     ceiling = (tx.bytes_len & ~15) * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
 
-    traffic, traffic_src = pmc_traffic(args.pmc, "csum_batch_kernel")
+    traffic, traffic_src = pmc_traffic(args.pmc, "csum_flat_kernel")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -413,12 +432,13 @@ def main():
                             "step = generate (IP+UDP csum) + verify (1% corrupted) pass",
                 "packets_per_gpu": n,
                 "frame_bytes": FRAME,
+                "rotation": f"{R} distinct tx/rx batch pairs launched in turn ({2 * R * n * FRAME / 1e9:.1f} GB per GPU)",
                 "global_batch": n * world,
                 "parallelism": f"{world} independent shards, no collective",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "csum_batch_kernel<2,true,false,nt,hybrid> (sccsum_ipv4_frames)",
+                "kernel": "csum_flat_kernel<16,true,false,false,nt> (sccsum_ipv4_frames)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",

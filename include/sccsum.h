@@ -168,7 +168,17 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len,
  * kernel with the next packet in flight, 4 / 5 = 2 / 3 with default cache
  * policy instead of nontemporal loads, 6 / 7 = 2 / 3 with each packet's last
  * 128-byte line loaded with the default policy, 8 / 9 = 2 / 6 with short
- * packets sharing passes: 4 per pass on 16 lanes each or 2 on 32).  All variants produce
+ * packets sharing passes: 4 per pass on 16 lanes each or 2 on 32), 10-13 = flat
+ * kernel (each tile's byte extent streamed densely with a wave prefix scan
+ * over 16-byte unit sums; 2 or 4 units per lane per chunk, 11 / 13 with the
+ * next chunk in flight), 14 / 15 = 13 / 11 with default-policy loads,
+ * 16 / 17 = flat with 8 units per lane per chunk (17 pipelined), 18 = 16 units,
+ * 19 / 20 = 16 with 1 / 2 of the 8 unit rows loaded with the default cache
+ * policy, 21 = 13 with 1 of 4, 22 = 18 with 2 of 16, 23 = 17 with 1 of 8,
+ * 24 / 25 = 18 with 1 / 4 of 16, 26 = 17 with 2 of 8, 27 = 18 scanned in two
+ * LDS groups of 8 rows, 28 / 29 = 32 units per lane per chunk in LDS groups of
+ * 16 / 8 rows, 30 / 31 / 32 = 18 / 16 / 27 with the next tile's first chunk
+ * issued before the current tile's finishing step.  All variants produce
  * identical results; the knob exists for in-process A/B timing and for
  * cross-checking two independent kernels.  SCCSUM_EINVAL for an unknown one. */
 int sccsum_set_kernel_variant(int variant);
@@ -186,6 +196,15 @@ int sccsum_set_group_units(int units);
  * 1..64 (default 64).  Results are unaffected. */
 int sccsum_set_tile_packets(int packets);
 
+/* Diagnostic: target bytes per flat-kernel tile (variants 10-13; default
+ * 0 = only the packet cap).  Results are unaffected. */
+int sccsum_set_tile_bytes(int bytes);
+
+/* Diagnostic: the flat kernel's guided tail — the last tiles hold
+ * B / divisor packets and cover about per_slot such tiles per wave slot
+ * (default 1 = uniform tiles, 4).  Results are unaffected. */
+int sccsum_set_tail_tiles(int divisor, int per_slot);
+
 /* Diagnostic: batch-kernel tiles dequeued from per-XCD counters (1, the
  * default) or dealt round robin (0).  Results are unaffected. */
 int sccsum_set_dynamic_tiles(int on);
@@ -199,6 +218,10 @@ int sccsum_sync(void* stream);
  * the measured HBM read ceiling. */
 int sccsum_read_probe(const void* d_src, uint64_t bytes, uint64_t* d_sink, void* stream);
 int sccsum_read_probe_blocks(void);
+
+/* Diagnostic: how many of the read probe's 4 loads in flight use the default
+ * cache policy instead of nontemporal (0, 1, 2 or 4; default 0). */
+int sccsum_set_probe_policy(int default_loads);
 
 /* ---------------------------------------------------------------------------
  * Host pipeline: batches that live in HOST memory (DPDK mbuf pools, socket

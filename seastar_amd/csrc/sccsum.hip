@@ -698,7 +698,7 @@ __global__ __launch_bounds__(kBlock, FILL ? SCCSUM_FILL_MIN_WAVES : SCCSUM_BATCH
                 re = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(sre), j));
             } else {
                 rs = jhead;
-                re = static_cast<uint64_t>(jhead) + __builtin_amdgcn_readlane(L, j);
+                re = static_cast<uint64_t>(jhead) + static_cast<uint32_t>(__builtin_amdgcn_readlane(L, j));
             }
             uint32_t SJ = exact_range_sum(ja0, rs, re, lane);
             if (jhead & 1u) SJ = swap16(SJ);
@@ -747,6 +747,445 @@ __global__ __launch_bounds__(kBlock, FILL ? SCCSUM_FILL_MIN_WAVES : SCCSUM_BATCH
         }
         __builtin_amdgcn_wave_barrier();  // stash rows are rewritten by the next tile
         t = t_next;
+    }
+}
+
+// ---------------------------------------------------------------- flat kernel
+
+// Inclusive prefix sums over the 64 lanes: Hillis-Steele row scans by
+// row_shr 1/2/4/8 (zero fill at the row edge), then row_bcast 15/31 carry the
+// row totals into rows 1-3 (gfx9 DPP; six v_add_u32_dpp per value).
+// tools/dev/scan_check.hip checks the sequence lane by lane on the device.
+// U independent scans, step-interleaved so that no DPP op
+// reads the result of the instruction just before it (no hazard nops).
+template <int U>
+__device__ __forceinline__ void wave_scan_n(uint32_t (&x)[U]) {
+#define SCCSUM_SCAN_STEP(ctrl, rm, bm)                                                                          \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) x[u] +=                                                       \
+        static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x[u]), ctrl, rm, bm, true));
+    SCCSUM_SCAN_STEP(0x111, 0xF, 0xF)
+    SCCSUM_SCAN_STEP(0x112, 0xF, 0xF)
+    SCCSUM_SCAN_STEP(0x114, 0xF, 0xF)
+    SCCSUM_SCAN_STEP(0x118, 0xF, 0xF)
+    SCCSUM_SCAN_STEP(0x142, 0xA, 0xF)
+    SCCSUM_SCAN_STEP(0x143, 0xC, 0xF)
+#undef SCCSUM_SCAN_STEP
+}
+
+// Dword i of the 64 bytes held in four units.
+__device__ __forceinline__ uint32_t unit_dword(const u32x4 (&h)[4], int i) {
+    const u32x4& u = h[i >> 2];
+    return (i & 3) == 0 ? u.x : (i & 3) == 1 ? u.y : (i & 3) == 2 ? u.z : u.w;
+}
+
+// The dword at byte `head + 4 i` of the four units (head < 16): a 4-way
+// select on head / 4 and a byte funnel shift.
+__device__ __forceinline__ uint32_t header_dword(const u32x4 (&h)[4], uint32_t head, int i) {
+    const uint32_t q = head >> 2;
+    auto pick = [&](int j) {
+        const uint32_t a = unit_dword(h, j), b = unit_dword(h, j + 1), c = unit_dword(h, j + 2),
+                       d = unit_dword(h, j + 3);
+        return q == 0 ? a : q == 1 ? b : q == 2 ? c : d;
+    };
+    return __builtin_amdgcn_alignbyte(pick(i + 1), pick(i), head & 3u);
+}
+
+constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B) between packets
+
+// Flat kernel.  Same tiles, tile order and outputs as csum_batch_kernel, but
+// the bytes are streamed per RUN instead of per packet: a run is a maximal
+// sequence of tile packets whose 16-byte unit spans go forward with gaps of
+// at most kGapUnits (packed batches: the whole tile).  The wave reads the
+// run's unit extent densely — U units per lane per chunk, no empty lane
+// loads whatever the packet sizes — sums each unit (v_sad_u16), takes a
+// wave-wide inclusive prefix scan of the unit sums (DPP) and parks the chunk's
+// prefix values and units in LDS; every packet lane then picks up the prefix
+// just before its first unit and at its last unit, plus the units the
+// finishing step needs (the first 1/3/4 units, the last), when they pass.  A
+// packet's sum of units is the difference of its two prefix values (exact
+// mod 2^32; sums stay below 2^32 up to kExactMax bytes), after which the
+// finishing step is the batch kernel's (edge bytes, IPv4 header,
+// pseudo-header, exact redo of the packets the fast path cannot take).
+// Layouts that do not run forward (shuffled offsets) degrade to one run per
+// packet — the per-packet cost of the batch kernel.
+template <int U, bool IPV4, bool FILL, bool PIPE, int AUX = kNT, int DEFROWS = 0, int SUB = U, bool XT = false>
+__global__ __launch_bounds__(kBlock) void csum_flat_kernel(
+    const uint8_t* __restrict__ bytes, uint64_t bytes_len,
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
+    const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
+    uint8_t* __restrict__ status, uint64_t n, uint32_t B, uint32_t B2, uint64_t T1, uint32_t* __restrict__ heads,
+    uint32_t flags) {
+    static_assert(!FILL || IPV4, "in-place generate is a frames mode");
+    constexpr uint32_t C = kWave * U;     // units per chunk
+    constexpr uint32_t CS = kWave * SUB;  // units per LDS group
+    static_assert(U % SUB == 0, "chunk rows split into whole groups");
+    static_assert(!(XT && PIPE), "cross-tile prefetch is for the unpipelined chunk loop");
+    constexpr int kHead = FILL ? 4 : (IPV4 ? 3 : 1);
+    const bool raw = !IPV4 && (flags & kFlagRaw);
+    const bool fill_ip = FILL && (flags & kFlagFillIp);
+    __shared__ u32x4 ubuf_all[kWavesPerBlock][CS];
+    __shared__ uint32_t pbuf_all[kWavesPerBlock][CS];
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    u32x4* ubuf = ubuf_all[wv];
+    uint32_t* pbuf = pbuf_all[wv];
+    const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+    // guided tiles: T1 tiles of B packets, then tiles of B2 (< B) packets, so
+    // the dequeue's last draws are short and the launch ends evenly
+    const uint64_t big = T1 * B;
+    const uint64_t ntiles = T1 + (n - big + B2 - 1) / B2;
+    const bool has_seed = !IPV4 && seed != nullptr;
+    const uint32_t vo = 16u * lane;
+
+    // tile order: as csum_batch_kernel (static first tile, then dequeued)
+    const uint64_t wglob = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
+    const uint32_t grp = static_cast<uint32_t>(wglob % kGroups);
+    const uint64_t rest = ntiles > nwaves ? ntiles - nwaves : 0;
+    const uint32_t tiles_g = rest > grp ? static_cast<uint32_t>((rest - grp + kGroups - 1) / kGroups) : 0u;
+    const uint32_t waves_g = static_cast<uint32_t>(nwaves / kGroups);
+    auto next_tile = [&](uint64_t prev) -> uint64_t {
+        if (heads == nullptr) return prev + nwaves;
+        uint32_t d = 0;
+        if (lane == 0) {
+            uint32_t* h = heads + grp * kHeadStride;
+            d = __hip_atomic_fetch_add(h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (d == tiles_g + waves_g - 1) __hip_atomic_store(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        d = __builtin_amdgcn_readfirstlane(d);
+        return d < tiles_g ? nwaves + grp + static_cast<uint64_t>(kGroups) * d : ntiles;
+    };
+    auto tile_base = [&](uint64_t tt) { return tt < T1 ? tt * B : big + (tt - T1) * B2; };
+    // Two-deep tile pipeline: while tile t streams, the plan (offset, length,
+    // seed) of the next tile is already loading and the tile after it is being
+    // dequeued, so no tile starts on an exposed metadata or atomic round trip.
+    // Every wave still makes exactly one failing dequeue (the counter reset
+    // relies on it).
+    uint64_t t = wglob;
+    if (t >= ntiles && heads != nullptr) t = next_tile(t);
+    uint64_t t1 = t < ntiles ? next_tile(t) : ntiles;
+    auto plan_load = [&](uint64_t tt, uint64_t& o_, uint32_t& L_, uint32_t& sd_) {
+        const uint64_t b_ = tile_base(tt < ntiles ? tt : 0);
+        const uint32_t bb = tt < T1 ? B : B2;
+        const uint32_t c_ = tt < ntiles ? static_cast<uint32_t>(n - b_ < bb ? n - b_ : bb) : 0u;
+        const uint64_t q_ = b_ + (lane < c_ ? lane : 0);
+        o_ = off[q_];
+        L_ = lane < c_ ? len[q_] : 0u;
+        sd_ = has_seed ? seed[q_] : 0u;
+    };
+    // ---- A: a tile's per-lane packet plan and its runs: lane j starts a new
+    // run unless packet j-1 and j both take part and j's span starts at most
+    // kGapUnits past j-1's end and ends no earlier (so a run's extent is
+    // [fu of its first, lu of its last])
+    struct Tile {
+        uint64_t base, o, a0, fu, lu, starts, streamed;
+        uint32_t cnt, L, sd, head, nunits;
+        bool mine, range_bad, short_frame, huge, fast, part;
+    };
+    auto derive = [&](uint64_t tt, uint64_t o_, uint32_t L_, uint32_t sd_) {
+        Tile c;
+        c.base = tile_base(tt);
+        const uint32_t bt = tt < T1 ? B : B2;
+        const uint64_t left = n - c.base;
+        c.cnt = left < bt ? static_cast<uint32_t>(left) : bt;
+        c.mine = lane < c.cnt;
+        c.o = o_;
+        c.L = L_;
+        c.sd = sd_;
+        c.range_bad = c.o > bytes_len || c.L > bytes_len - c.o;
+        c.short_frame = IPV4 && c.L < 20;
+        c.huge = c.L > kExactMax;
+        const uint8_t* ptr = bytes + (c.range_bad ? 0 : c.o);
+        c.head = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ptr) & 15u);
+        c.a0 = reinterpret_cast<uint64_t>(ptr - c.head);
+        c.fast = c.mine && !c.range_bad && !c.short_frame && !c.huge;
+        c.nunits = (c.fast && c.L) ? (c.head + c.L + 15u) >> 4 : 0u;
+        c.part = c.nunits != 0;
+        c.fu = c.a0 >> 4;
+        c.lu = c.fu + c.nunits - 1;
+        const int pl = static_cast<int>(lane == 0 ? 0 : lane - 1);
+        const uint64_t pfu =
+            (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(c.fu >> 32), pl))) << 32) |
+            static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(c.fu)), pl));
+        const uint64_t plu =
+            (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(c.lu >> 32), pl))) << 32) |
+            static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(c.lu)), pl));
+        const bool ppart = __shfl(static_cast<int>(c.part), pl) != 0;
+        const bool joins = lane != 0 && c.part && ppart && c.fu >= pfu && c.lu >= plu && c.fu <= plu + kGapUnits;
+        c.starts = __ballot(c.mine && !joins) | (c.cnt < 64 ? (1ull << c.cnt) : 0ull);
+        c.streamed = c.starts & __ballot(c.part);  // runs that stream bytes start at a lane that takes part
+        return c;
+    };
+    // Run [k, k2) of tile c: its extent's first unit F and unit count.
+    struct Run {
+        uint32_t k, k2, ext;
+        uint64_t F;
+    };
+    auto run_of = [&](const Tile& c, uint32_t k) {
+        Run rn;
+        rn.k = k;
+        const uint64_t after = c.starts & ~((2ull << k) - 1ull);  // k < 64; bit cnt is the sentinel
+        rn.k2 = after ? static_cast<uint32_t>(__builtin_ctzll(after)) : c.cnt;
+        // (readlane returns int: widen through uint32_t, never sign-extend an address half)
+        const uint32_t Fhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(c.fu >> 32), k);
+        const uint32_t Flo = __builtin_amdgcn_readlane(static_cast<uint32_t>(c.fu), k);
+        rn.F = (static_cast<uint64_t>(Fhi) << 32) | Flo;
+        const uint32_t Llo = __builtin_amdgcn_readlane(static_cast<uint32_t>(c.lu), rn.k2 - 1);
+        rn.ext = Llo - static_cast<uint32_t>(rn.F) + 1u;  // units in the run's extent
+        return rn;
+    };
+    auto run_rsrc = [&](const Run& rn) { return rsrc(reinterpret_cast<const uint8_t*>(rn.F << 4), 16u * rn.ext); };
+    auto load = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t g, u32x4 (&v)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (u < DEFROWS) {
+                v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(16u * g + vo + 1024u * u), 0, 0);
+            } else {
+                v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(16u * g + vo + 1024u * u), 0, AUX);
+            }
+    };
+
+    uint64_t o_n = 0;
+    uint32_t L_n = 0, sd_n = 0;
+    plan_load(t, o_n, L_n, sd_n);
+    Tile cur{};
+    // XT: vpre holds chunk 0 of the current tile's first streamed run, issued
+    // before the previous tile's finishing step so no tile starts on an
+    // exposed memory round trip
+    u32x4 vpre[XT ? U : 1];
+    bool pre = false;
+    if constexpr (XT) {
+        if (t < ntiles) {
+            cur = derive(t, o_n, L_n, sd_n);
+            if (cur.streamed) {
+                const Run rn = run_of(cur, static_cast<uint32_t>(__builtin_ctzll(cur.streamed)));
+                load(run_rsrc(rn), 0, vpre);
+                pre = true;
+            }
+        }
+    }
+    while (t < ntiles) {
+        const uint64_t t2 = t1 < ntiles ? next_tile(t1) : ntiles;
+        if (!XT) cur = derive(t, o_n, L_n, sd_n);
+        if (t1 < ntiles) plan_load(t1, o_n, L_n, sd_n);
+        const uint64_t base = cur.base;
+        const uint32_t cnt = cur.cnt;
+        const bool mine = cur.mine;
+        const uint32_t L = cur.L, sd = cur.sd, head = cur.head, nunits = cur.nunits;
+        const uint64_t a0 = cur.a0;
+        const bool range_bad = cur.range_bad, short_frame = cur.short_frame, huge = cur.huge, fast = cur.fast;
+
+        // ---- B: stream each run's extent
+        u32x4 hs[4] = {u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}};
+        u32x4 hl = u32x4{0, 0, 0, 0};
+        uint32_t pst = 0, pend = 0;
+        uint64_t rem = cur.streamed;
+        while (rem != 0) {
+            const Run rn = run_of(cur, static_cast<uint32_t>(__builtin_ctzll(rem)));
+            rem &= rem - 1;
+            const uint32_t k = rn.k, k2 = rn.k2, ext = rn.ext;
+            const uint64_t F = rn.F;
+            const auto r = run_rsrc(rn);
+            const bool cap = lane >= k && lane < k2;
+            const int rf = cap ? static_cast<int>(static_cast<uint32_t>(cur.fu - F)) : -0x40000000;
+            const int rl = cap ? static_cast<int>(static_cast<uint32_t>(cur.lu - F)) : -0x40000000;
+            uint32_t carry = 0;
+            // one chunk = U rows of 64 units; scanned, parked in LDS and
+            // captured SUB-row group by SUB-row group (LDS holds one group)
+            auto chunk = [&](uint32_t g, const u32x4 (&v)[U]) {
+#pragma unroll
+                for (int s0 = 0; s0 < U; s0 += SUB) {
+                    uint32_t x[SUB];
+#pragma unroll
+                    for (int u = 0; u < SUB; ++u) x[u] = sad4(v[s0 + u], 0u);
+                    wave_scan_n<SUB>(x);
+#pragma unroll
+                    for (int u = 0; u < SUB; ++u) {
+                        pbuf[kWave * u + lane] = carry + x[u];
+                        ubuf[kWave * u + lane] = v[s0 + u];
+                        carry += __builtin_amdgcn_readlane(x[u], 63);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    const int gs = static_cast<int>(g) + kWave * s0;
+                    const int a = rf - gs;
+                    if (static_cast<uint32_t>(a) < CS) {
+                        const u32x4 w = ubuf[a];
+                        pst = pbuf[a] - sad4(w, 0u);  // prefix just before the first unit
+                        hs[0] = w;
+                    }
+#pragma unroll
+                    for (int j = 1; j < kHead; ++j) {
+                        if (static_cast<uint32_t>(a + j) < CS) hs[j] = ubuf[a + j];
+                    }
+                    const int b = rl - gs;
+                    if (static_cast<uint32_t>(b) < CS) {
+                        pend = pbuf[b];
+                        hl = ubuf[b];
+                    }
+                    __builtin_amdgcn_wave_barrier();  // this group's LDS reads precede the next group's writes
+                }
+            };
+            if (PIPE) {
+                u32x4 va[U], vb[U];
+                load(r, 0, va);
+                for (uint32_t g = 0; g < ext; g += 2 * C) {
+                    load(r, g + C, vb);
+                    chunk(g, va);
+                    load(r, g + 2 * C, va);
+                    chunk(g + C, vb);
+                }
+            } else {
+                uint32_t g = 0;
+                if constexpr (XT) {
+                    if (pre) {  // chunk 0 of the tile's first streamed run is already in flight
+                        chunk(0, vpre);
+                        g = C;
+                        pre = false;
+                    }
+                }
+                for (; g < ext; g += C) {
+                    u32x4 v[U];
+                    load(r, g, v);
+                    chunk(g, v);
+                }
+            }
+        }
+        if constexpr (XT) {  // next tile: plan, runs, first chunk in flight before this tile finishes
+            if (t1 < ntiles) {
+                cur = derive(t1, o_n, L_n, sd_n);
+                if (cur.streamed) {
+                    const Run rn = run_of(cur, static_cast<uint32_t>(__builtin_ctzll(cur.streamed)));
+                    load(run_rsrc(rn), 0, vpre);
+                    pre = true;
+                }
+            }
+        }
+        const uint32_t res = pend - pst;  // sum of the packet's units, mod 2^32
+
+        // ---- C: lane i finishes packet i (as csum_batch_kernel, stash in registers)
+        const int rs0 = static_cast<int>(head) + (IPV4 ? 20 : 0);
+        const int re0 = static_cast<int>(head + L);
+        const int lastu16 = 16 * (static_cast<int>(nunits) - 1);
+        uint32_t excl = unit_part(hs[0], 0, rs0);
+        if (IPV4) excl += unit_part(hs[1], 0, rs0 - 16) + unit_part(hs[2], 0, rs0 - 32);
+        excl += unit_part(hl, re0 - lastu16, 16);
+        const uint32_t kept = nunits ? res - excl : 0u;
+        uint32_t S = fold16(kept);
+        if (head & 1u) S = swap16(S);
+        uint32_t word = 0, st = 0;
+        bool slow = huge && mine && !range_bad;
+        uint32_t ipc = 0, pseudo = 0, fpos = 0;
+        int srs = 0, sre = 0;
+        if (IPV4) {
+            const uint32_t h0 = header_dword(hs, head, 0), h1 = header_dword(hs, head, 1);
+            const uint32_t h2 = header_dword(hs, head, 2), h3 = header_dword(hs, head, 3);
+            const uint32_t h4 = header_dword(hs, head, 4);
+            ipc = ~fold16(static_cast<uint64_t>(h0) + h1 + (FILL ? h2 & 0xffffu : h2) + h3 + h4) & 0xffffu;
+            const uint32_t ihl = h0 & 0xfu;
+            const uint32_t ip_len = swap16(h0 >> 16);
+            const uint32_t proto = (h2 >> 8) & 0xffu;
+            const uint32_t l4_off = 4u * ihl;
+            const uint32_t l4_end = ip_len < L ? ip_len : L;
+            uint32_t l4_len = 0;
+            if (L < ip_len) st |= SCCSUM_ST_MALFORMED;
+            if (l4_off > l4_end) {
+                st |= SCCSUM_ST_MALFORMED;
+            } else {
+                l4_len = l4_end - l4_off;
+            }
+            pseudo = fold16(static_cast<uint64_t>(h3 & 0xffffu) + (h3 >> 16) + (h4 & 0xffffu) + (h4 >> 16) +
+                            (proto << 8) + swap16(l4_len & 0xffffu));
+            slow = slow || (fast && (ihl != 5u || ip_len != L));
+            srs = static_cast<int>(head + l4_off);
+            sre = srs + static_cast<int>(l4_len);
+            if (FILL) {
+                const uint32_t fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
+                const bool has_field = fo != 0u && l4_len >= fo + 2u && (st & SCCSUM_ST_MALFORMED) == 0u;
+                fpos = has_field ? static_cast<uint32_t>(srs) + fo : 0u;
+                uint32_t fv = 0;
+                if (has_field && !slow) {  // ihl == 5: frame bytes 26-27 (UDP) / 36-37 (TCP)
+                    fv = fo == 6u ? header_dword(hs, head, 6) >> 16 : header_dword(hs, head, 9) & 0xffffu;
+                }
+                const uint32_t rr = ~fold16(static_cast<uint64_t>(S) + pseudo + (~fv & 0xffffu)) & 0xffffu;
+                word = (fill_ip ? ipc : 0u) | (has_field ? rr << 16 : 0u);
+                st |= (fill_ip ? SCCSUM_ST_OK : 0u) | (has_field ? SCCSUM_ST_L4_OK : 0u);
+            } else {
+                const uint32_t rr = ~fold16(static_cast<uint64_t>(S) + pseudo) & 0xffffu;
+                word = ipc | (rr << 16);
+                st |= (ipc == 0 ? SCCSUM_ST_OK : 0u) | (rr == 0 ? SCCSUM_ST_L4_OK : 0u);
+            }
+        } else {
+            const uint32_t rr = raw ? S : ~fold16(static_cast<uint64_t>(S) + swap16(fold16(sd))) & 0xffffu;
+            word = rr;
+            st = (!raw && rr == 0) ? SCCSUM_ST_OK : 0u;
+        }
+        if (range_bad) {
+            word = 0;
+            st = SCCSUM_ST_RANGE;
+        } else if (short_frame) {
+            word = 0;
+            st = SCCSUM_ST_MALFORMED;
+        }
+
+        // ---- D: exact redo of the packets the fast path could not take
+        uint64_t todo = __ballot(slow);
+        while (todo) {
+            const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            const uint32_t jlo = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0), j);
+            const uint32_t jhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0 >> 32), j);
+            const uint8_t* ja0 = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(jhi) << 32) | jlo);
+            const uint32_t jhead = __builtin_amdgcn_readlane(head, j);
+            uint64_t rs, re;
+            if (IPV4) {
+                rs = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(srs), j));
+                re = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(sre), j));
+            } else {
+                rs = jhead;
+                re = static_cast<uint64_t>(jhead) + static_cast<uint32_t>(__builtin_amdgcn_readlane(L, j));
+            }
+            uint32_t SJ = exact_range_sum(ja0, rs, re, lane);
+            if (jhead & 1u) SJ = swap16(SJ);
+            if (lane == j) {
+                if (IPV4 && FILL) {
+                    if (fpos) {
+                        const uint8_t* fp = reinterpret_cast<const uint8_t*>(a0) + fpos;
+                        const uint32_t fv = static_cast<uint32_t>(fp[0]) | (static_cast<uint32_t>(fp[1]) << 8);
+                        const uint32_t rr = ~fold16(static_cast<uint64_t>(SJ) + pseudo + (~fv & 0xffffu)) & 0xffffu;
+                        word = (word & 0xffffu) | (rr << 16);
+                    }
+                } else if (IPV4) {
+                    const uint32_t rr = ~fold16(static_cast<uint64_t>(SJ) + pseudo) & 0xffffu;
+                    word = ipc | (rr << 16);
+                    st = (st & ~SCCSUM_ST_L4_OK) | (rr == 0 ? SCCSUM_ST_L4_OK : 0u);
+                } else {
+                    const uint32_t rr = raw ? SJ : ~fold16(static_cast<uint64_t>(SJ) + swap16(fold16(sd))) & 0xffffu;
+                    word = rr;
+                    st = (!raw && rr == 0) ? SCCSUM_ST_OK : 0u;
+                }
+            }
+        }
+
+        if (FILL && mine && !range_bad && !short_frame) {
+            uint8_t* wp = reinterpret_cast<uint8_t*>(a0);
+            if (fill_ip) {
+                wp[head + 10] = static_cast<uint8_t>(word);
+                wp[head + 11] = static_cast<uint8_t>(word >> 8);
+            }
+            if (fpos) {
+                wp[fpos] = static_cast<uint8_t>(word >> 16);
+                wp[fpos + 1] = static_cast<uint8_t>(word >> 24);
+            }
+        }
+        if (mine) {
+            if (IPV4) {
+                if (out) reinterpret_cast<uint32_t*>(out)[base + lane] = word;
+            } else {
+                out[base + lane] = static_cast<uint16_t>(word);
+            }
+            if (status) status[base + lane] = static_cast<uint8_t>(st);
+        }
+        t = t1;
+        t1 = t2;
     }
 }
 
@@ -842,16 +1281,24 @@ __global__ __launch_bounds__(kBlock) void fill_header_kernel(uint8_t* __restrict
 }
 
 // Plain stream-read of the same load shape (16 B per lane, nontemporal).
+// DEF of the four loads in flight use the default cache policy, the rest nt
+// (diagnostic: sccsum_set_probe_policy).
+template <int DEF>
+__device__ __forceinline__ u32x4 probe_load(const u32x4* p, int k) {
+    return k < DEF ? *p : __builtin_nontemporal_load(p);
+}
+
+template <int DEF>
 __global__ __launch_bounds__(kBlock) void read_probe_kernel(const u32x4* __restrict__ src, uint64_t units,
                                                              uint64_t* __restrict__ sink) {
     uint64_t acc = 0;
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock;
     uint64_t i = static_cast<uint64_t>(xcd_block_id()) * kBlock + threadIdx.x;
     for (; i + 3 * stride < units; i += 4 * stride) {
-        const u32x4 a = __builtin_nontemporal_load(src + i);
-        const u32x4 b = __builtin_nontemporal_load(src + i + stride);
-        const u32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
-        const u32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
+        const u32x4 a = probe_load<DEF>(src + i, 0);
+        const u32x4 b = probe_load<DEF>(src + i + stride, 1);
+        const u32x4 c = probe_load<DEF>(src + i + 2 * stride, 2);
+        const u32x4 d = probe_load<DEF>(src + i + 3 * stride, 3);
         acc += static_cast<uint64_t>(a.x) + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
         acc += static_cast<uint64_t>(c.x) + c.y + c.z + c.w + d.x + d.y + d.z + d.w;
     }
@@ -944,6 +1391,72 @@ int units_class(uint32_t max_len) {
 // 8 / 9 = 2 / 6 with short packets sharing passes (4 x 16 or 2 x 32 lanes).
 std::atomic<int> g_variant{0};
 
+std::atomic<int> g_tile_bytes{0};
+std::atomic<int> g_probe_default{0};  // read probe: loads (of 4 in flight) with the default cache policy  // flat kernel: target bytes per tile (0 = packets cap only)
+
+// Flat-kernel launch: the grid is what the chip holds at once (the kernel's
+// occupancy, from its VGPR and LDS use, capped by the blocks-per-CU knob), so
+// every wave's static first tile starts at launch; tiles hold about
+// g_tile_bytes of packets (mean length from bytes_len / n), capped at 64.
+using FlatKernel = void (*)(const uint8_t*, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*, uint16_t*,
+                            uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t, uint32_t*, uint32_t);
+std::atomic<int> g_tail_div{1};    // flat kernel: tail tiles hold B / g_tail_div packets (1 = no guided tail)
+std::atomic<int> g_tail_tiles{4};  // ... and cover about this many tail tiles per wave slot
+
+int flat_occupancy(FlatKernel k) {
+    constexpr int kSlots = 16;
+    static std::atomic<FlatKernel> keys[kSlots];
+    static std::atomic<int> vals[kSlots];
+    for (int i = 0; i < kSlots; ++i) {
+        if (keys[i].load(std::memory_order_acquire) == k) return vals[i].load(std::memory_order_relaxed);
+    }
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k), kBlock, 0) != hipSuccess ||
+        nb <= 0) {
+        nb = 1;
+    }
+    for (int i = 0; i < kSlots; ++i) {
+        FlatKernel expect = nullptr;
+        if (keys[i].load(std::memory_order_relaxed) == nullptr) {
+            vals[i].store(nb, std::memory_order_relaxed);
+            if (keys[i].compare_exchange_strong(expect, k, std::memory_order_release)) break;
+        }
+    }
+    return nb;
+}
+
+void launch_flat(FlatKernel kern, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
+                 const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
+                 uint32_t flags) {
+    const int occ = flat_occupancy(kern);
+    const int knob = g_blocks_per_cu.load(std::memory_order_relaxed);
+    const uint64_t bpc = static_cast<uint64_t>(occ < knob ? occ : knob);
+    const uint64_t cap = static_cast<uint64_t>(cu_count()) * bpc;
+    const uint64_t slots = cap * kWavesPerBlock;
+    uint64_t bmax = static_cast<uint64_t>(g_tile_packets.load(std::memory_order_relaxed));
+    const uint64_t tb = static_cast<uint64_t>(g_tile_bytes.load(std::memory_order_relaxed));
+    if (tb) {
+        const uint64_t mean = bytes_len / n ? bytes_len / n : 1;
+        const uint64_t bb = tb / mean ? tb / mean : 1;
+        bmax = bb < bmax ? bb : bmax;
+    }
+    uint64_t B = (n + slots - 1) / slots;
+    B = B < 1 ? 1 : (B > bmax ? bmax : B);
+    // guided tail: the last ~g_tail_tiles small tiles per wave slot hold B / g_tail_div packets each
+    const int div = g_tail_div.load(std::memory_order_relaxed);
+    const uint64_t B2 = div > 1 && B / div ? B / div : B;
+    const uint64_t tail = B2 < B ? slots * B2 * static_cast<uint64_t>(g_tail_tiles.load(std::memory_order_relaxed)) : 0;
+    const uint64_t T1 = tail < n ? (n - tail) / B : 0;
+    const uint64_t tiles = T1 + (n - T1 * B + B2 - 1) / B2;
+    uint64_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    blocks = blocks < cap ? blocks : cap;
+    blocks = (blocks + 15) & ~uint64_t(15);  // multiple of 16: XCD mapping, waves divide into kGroups
+    uint32_t* heads = g_dynamic.load(std::memory_order_relaxed) ? next_heads() : nullptr;
+    kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
+        b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, static_cast<uint32_t>(B), static_cast<uint32_t>(B2), T1,
+        heads, flags);
+}
+
 template <int U, bool IPV4>
 void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
               const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
@@ -963,6 +1476,69 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     const uint32_t b32 = static_cast<uint32_t>(B);
     uint32_t* heads = nullptr;
     if (g_dynamic.load(std::memory_order_relaxed)) heads = next_heads();
+    if (variant >= 10) {  // flat kernel: 10 / 11 = U 2 (11 pipelined), 12 / 13 = U 4 (13 pipelined),
+                          // 14 / 15 = 13 / 11 with default-policy loads, 16 / 17 = U 8, 18 = U 16,
+                          // 19 / 20 = 16 with 1 / 2 of the 8 rows default-policy, 21 = 13 with 1 of 4,
+                          // 22 = 18 with 2 of 16, 23 = 17 with 1 of 8, 24 / 25 = 18 with 1 / 4 of 16,
+                          // 26 = 17 with 2 of 8, 27 = 18 scanned in 2 LDS groups of 8 rows,
+                          // 28 / 29 = 32 units per lane per chunk in groups of 16 / 8 rows,
+                          // 30 / 31 / 32 = 18 / 16 / 27 with the next tile's first chunk in flight
+        auto go = [&](auto kern) { launch_flat(kern, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags); };
+        if (IPV4 && (flags & kFlagFillL4)) {
+            switch (variant) {
+                case 10: go(csum_flat_kernel<2, IPV4, IPV4, false>); break;
+                case 11: go(csum_flat_kernel<2, IPV4, IPV4, true>); break;
+                case 12: go(csum_flat_kernel<4, IPV4, IPV4, false>); break;
+                case 14: go(csum_flat_kernel<4, IPV4, IPV4, true, 0>); break;
+                case 15: go(csum_flat_kernel<2, IPV4, IPV4, true, 0>); break;
+                case 16: go(csum_flat_kernel<8, IPV4, IPV4, false>); break;
+                case 17: go(csum_flat_kernel<8, IPV4, IPV4, true>); break;
+                case 18: go(csum_flat_kernel<16, IPV4, IPV4, false>); break;
+                case 19: go(csum_flat_kernel<8, IPV4, IPV4, false, kNT, 1>); break;
+                case 20: go(csum_flat_kernel<8, IPV4, IPV4, false, kNT, 2>); break;
+                case 21: go(csum_flat_kernel<4, IPV4, IPV4, true, kNT, 1>); break;
+                case 22: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 2>); break;
+                case 23: go(csum_flat_kernel<8, IPV4, IPV4, true, kNT, 1>); break;
+                case 24: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 1>); break;
+                case 25: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 4>); break;
+                case 26: go(csum_flat_kernel<8, IPV4, IPV4, true, kNT, 2>); break;
+                case 27: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 0, 8>); break;
+                case 28: go(csum_flat_kernel<32, IPV4, IPV4, false, kNT, 0, 16>); break;
+                case 29: go(csum_flat_kernel<32, IPV4, IPV4, false, kNT, 0, 8>); break;
+                case 30: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 0, 16, true>); break;
+                case 31: go(csum_flat_kernel<8, IPV4, IPV4, false, kNT, 0, 8, true>); break;
+                case 32: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 0, 8, true>); break;
+                default: go(csum_flat_kernel<4, IPV4, IPV4, true>); break;
+            }
+        } else {
+            switch (variant) {
+                case 10: go(csum_flat_kernel<2, IPV4, false, false>); break;
+                case 11: go(csum_flat_kernel<2, IPV4, false, true>); break;
+                case 12: go(csum_flat_kernel<4, IPV4, false, false>); break;
+                case 14: go(csum_flat_kernel<4, IPV4, false, true, 0>); break;
+                case 15: go(csum_flat_kernel<2, IPV4, false, true, 0>); break;
+                case 16: go(csum_flat_kernel<8, IPV4, false, false>); break;
+                case 17: go(csum_flat_kernel<8, IPV4, false, true>); break;
+                case 18: go(csum_flat_kernel<16, IPV4, false, false>); break;
+                case 19: go(csum_flat_kernel<8, IPV4, false, false, kNT, 1>); break;
+                case 20: go(csum_flat_kernel<8, IPV4, false, false, kNT, 2>); break;
+                case 21: go(csum_flat_kernel<4, IPV4, false, true, kNT, 1>); break;
+                case 22: go(csum_flat_kernel<16, IPV4, false, false, kNT, 2>); break;
+                case 23: go(csum_flat_kernel<8, IPV4, false, true, kNT, 1>); break;
+                case 24: go(csum_flat_kernel<16, IPV4, false, false, kNT, 1>); break;
+                case 25: go(csum_flat_kernel<16, IPV4, false, false, kNT, 4>); break;
+                case 26: go(csum_flat_kernel<8, IPV4, false, true, kNT, 2>); break;
+                case 27: go(csum_flat_kernel<16, IPV4, false, false, kNT, 0, 8>); break;
+                case 28: go(csum_flat_kernel<32, IPV4, false, false, kNT, 0, 16>); break;
+                case 29: go(csum_flat_kernel<32, IPV4, false, false, kNT, 0, 8>); break;
+                case 30: go(csum_flat_kernel<16, IPV4, false, false, kNT, 0, 16, true>); break;
+                case 31: go(csum_flat_kernel<8, IPV4, false, false, kNT, 0, 8, true>); break;
+                case 32: go(csum_flat_kernel<16, IPV4, false, false, kNT, 0, 8, true>); break;
+                default: go(csum_flat_kernel<4, IPV4, false, true>); break;
+            }
+        }
+        return;
+    }
     if constexpr (IPV4) {
         if (flags & kFlagFillL4) {
             if (variant == 8 || variant == 9) {
@@ -1023,7 +1599,11 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
         return SCCSUM_EINVAL;
     }
     int variant = g_variant.load(std::memory_order_relaxed);
-    if (variant == 0) variant = (max_len != 0 && max_len <= 2048) ? 6 : 8;
+    // default: the flat kernel, all loads nontemporal — 16 units per lane per
+    // chunk for big batches (>= 512 Ki packets and 256 MiB), else 8 units with
+    // the next chunk in flight: the 16-unit form runs 2 waves per SIMD, too
+    // few tiles per wave on smaller batches (DESIGN.md §5.1 has the A/B)
+    if (variant == 0) variant = (n >= (512u << 10) && bytes_len >= (256ull << 20)) ? 18 : 17;
     if (variant == 1 && (flags & kFlagFillL4)) variant = 6;  // in-place write-back lives in the batch kernel
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
@@ -1149,7 +1729,7 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
 }
 
 int sccsum_set_kernel_variant(int variant) {
-    if (variant < 0 || variant > 9) return SCCSUM_EINVAL;
+    if (variant < 0 || variant > 32) return SCCSUM_EINVAL;
     sccsum::g_variant.store(variant, std::memory_order_relaxed);
     return SCCSUM_OK;
 }
@@ -1172,6 +1752,19 @@ int sccsum_set_tile_packets(int packets) {
     return SCCSUM_OK;
 }
 
+int sccsum_set_tile_bytes(int bytes) {
+    if (bytes < 0) return SCCSUM_EINVAL;
+    sccsum::g_tile_bytes.store(bytes, std::memory_order_relaxed);
+    return SCCSUM_OK;
+}
+
+int sccsum_set_tail_tiles(int divisor, int per_slot) {
+    if (divisor < 1 || divisor > 64 || per_slot < 0 || per_slot > 64) return SCCSUM_EINVAL;
+    sccsum::g_tail_div.store(divisor, std::memory_order_relaxed);
+    sccsum::g_tail_tiles.store(per_slot, std::memory_order_relaxed);
+    return SCCSUM_OK;
+}
+
 int sccsum_set_dynamic_tiles(int on) {
     if (on != 0 && on != 1) return SCCSUM_EINVAL;
     sccsum::g_dynamic.store(on, std::memory_order_relaxed);
@@ -1185,9 +1778,21 @@ int sccsum_read_probe_blocks(void) { return sccsum::cu_count() * sccsum::kBlocks
 int sccsum_read_probe(const void* d_src, uint64_t bytes, uint64_t* d_sink, void* stream) {
     if (!d_src || !d_sink || (bytes & 15u) || (reinterpret_cast<uintptr_t>(d_src) & 15u)) return SCCSUM_EINVAL;
     const unsigned grid = static_cast<unsigned>(sccsum_read_probe_blocks()) & ~7u;
-    sccsum::read_probe_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, static_cast<hipStream_t>(stream)>>>(
-        static_cast<const sccsum::u32x4*>(d_src), bytes / 16, d_sink);
+    const auto* src = static_cast<const sccsum::u32x4*>(d_src);
+    const auto hs = static_cast<hipStream_t>(stream);
+    switch (sccsum::g_probe_default.load(std::memory_order_relaxed)) {
+        case 1: sccsum::read_probe_kernel<1><<<dim3(grid), dim3(sccsum::kBlock), 0, hs>>>(src, bytes / 16, d_sink); break;
+        case 2: sccsum::read_probe_kernel<2><<<dim3(grid), dim3(sccsum::kBlock), 0, hs>>>(src, bytes / 16, d_sink); break;
+        case 4: sccsum::read_probe_kernel<4><<<dim3(grid), dim3(sccsum::kBlock), 0, hs>>>(src, bytes / 16, d_sink); break;
+        default: sccsum::read_probe_kernel<0><<<dim3(grid), dim3(sccsum::kBlock), 0, hs>>>(src, bytes / 16, d_sink); break;
+    }
     return static_cast<int>(hipGetLastError());
+}
+
+int sccsum_set_probe_policy(int default_loads) {
+    if (default_loads != 0 && default_loads != 1 && default_loads != 2 && default_loads != 4) return SCCSUM_EINVAL;
+    sccsum::g_probe_default.store(default_loads, std::memory_order_relaxed);
+    return SCCSUM_OK;
 }
 
 }  // extern "C"

@@ -2,6 +2,11 @@
 on the bench workload and on mixed / long packets.  Prints one JSON line per
 (case, variant) with median and min launch time and GB/s (algorithmic bytes).
 
+--rotate R (default 4) keeps R distinct copies of each batch and launches on
+them in turn, so no launch finds the previous launch's lines in the 256 MB
+MALL (a back-to-back replay of ONE 1.5 GB batch lets default-policy lines
+survive between launches — a replay artefact, not streaming bandwidth).
+
 usage: python tools/ab_kernels.py [--rounds 10] [--variants 1,2]
 """
 from __future__ import annotations
@@ -46,7 +51,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn]]]]")
+    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn[:tile_bytes[:tail_div[:tail_per_slot]]]]]]]")
+    ap.add_argument("--rotate", type=int, default=4, help="distinct copies of each batch, launched in turn")
     ap.add_argument("--cases", default="udp1500_frames,udp1500_spans,zipf_spans,cfg3_zipf_frames,tcp64k_spans")
     args = ap.parse_args()
     variants = args.variants.split(",")
@@ -59,40 +65,55 @@ def main():
             continue
         outs = {}
         times = {v: [] for v in variants}
+        copies = [b] + [batch.PacketBatch(data=b.data.clone(), off=b.off.clone(), length=b.length.clone(),
+                                          bytes_len=b.bytes_len, max_len=b.max_len) for _ in range(args.rotate - 1)]
+        turn = [0]
 
-        def run(v):
-            parts = (v.split(":") + ["", "", "", ""])[:5]
+        def knobs(v):
+            parts = (v.split(":") + ["", "", "", "", "", "", ""])[:8]
             native.check(lib.sccsum_set_kernel_variant(int(parts[0])), "variant")
             native.check(lib.sccsum_set_blocks_per_cu(int(parts[1] or 8)), "blocks_per_cu")
             native.check(lib.sccsum_set_group_units(int(parts[2] or 0)), "group_units")
             native.check(lib.sccsum_set_tile_packets(int(parts[3] or 64)), "tile_packets")
             native.check(lib.sccsum_set_dynamic_tiles(int(parts[4] or 1)), "dynamic")
+            native.check(lib.sccsum_set_tile_bytes(int(parts[5] or 0)), "tile_bytes")
+            native.check(lib.sccsum_set_tail_tiles(int(parts[6] or 1), int(parts[7] or 4)), "tail")
+
+        def run(bb):
             if mode == "frames":
-                return batch.ipv4_frames(b)
-            return batch.spans(b)
+                return batch.ipv4_frames(bb)
+            return batch.spans(bb)
+
+        def run_next():
+            bb = copies[turn[0] % len(copies)]
+            turn[0] += 1
+            return run(bb)
 
         for v in variants:
-            outs[v] = run(v).clone()
+            knobs(v)
+            outs[v] = run(copies[0]).clone()
         torch.cuda.synchronize()
         ref = outs[variants[0]]
         for v in variants[1:]:
             assert torch.equal(outs[v], ref), f"{name}: variant {v} differs from {variants[0]}"
         for _ in range(args.rounds):
             for v in variants:
+                knobs(v)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                run(v)
+                run_next()
                 e0.record()
                 for _ in range(args.reps):
-                    run(v)
+                    run_next()
                 e1.record()
                 torch.cuda.synchronize()
                 times[v].append(e0.elapsed_time(e1) / args.reps)
         for v in variants:
             t = np.array(times[v])
-            print(json.dumps({"case": name, "variant": v, "median_us": round(float(np.median(t)) * 1e3, 1),
+            print(json.dumps({"case": name, "variant": v, "rotate": len(copies),
+                              "median_us": round(float(np.median(t)) * 1e3, 1),
                               "min_us": round(float(t.min()) * 1e3, 1),
                               "GBps_median": round(alg / (np.median(t) / 1e3) / 1e9, 1)}), flush=True)
-        del b
+        del b, copies
         torch.cuda.empty_cache()
     native.check(lib.sccsum_set_kernel_variant(0), "variant")
     native.check(lib.sccsum_set_blocks_per_cu(8), "blocks_per_cu")

@@ -22,6 +22,7 @@ import os
 from collections import defaultdict
 
 KERNELS = {
+    "csum_flat_kernel": "csum_flat_kernel",
     "csum_batch_kernel": "csum_batch_kernel",
     "csum_kernel<": "csum_kernel",
     "read_probe_kernel": "read_probe_kernel",
@@ -70,6 +71,7 @@ def main():
     ap.add_argument("--trace", default=None)
     ap.add_argument("--probe-bytes", type=float, required=True)
     ap.add_argument("--alg-bytes", type=float, default=None, help="algorithmic bytes per csum launch")
+    ap.add_argument("--alg-kernel", default="csum_flat_kernel", help="kernel the --alg-bytes figure belongs to")
     ap.add_argument("--label", default="")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
@@ -98,7 +100,7 @@ def main():
         if k in trace:
             entry["avg_us_kernel_trace"] = round(trace[k]["avg_us"], 2)
             entry["calls_kernel_trace"] = trace[k]["calls"]
-        if a.alg_bytes and k == "csum_batch_kernel" and entry["hbm_bytes_per_launch"]:
+        if a.alg_bytes and k == a.alg_kernel and entry["hbm_bytes_per_launch"]:
             entry["alg_bytes_per_launch"] = a.alg_bytes
             entry["traffic_over_alg"] = round(entry["hbm_bytes_per_launch"] / a.alg_bytes, 4)
         res["kernels"][k] = entry
