@@ -162,25 +162,19 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len,
                      uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len,
                      uint32_t mode, void* stream);
 
-/* Diagnostic: select the kernel family for later launches in this process
- * (0 = default (6 when max_len <= 2048, else 8), 1 = one-packet-per-wave
- * loop, 2 = batch kernel, 3 = batch
- * kernel with the next packet in flight, 4 / 5 = 2 / 3 with default cache
- * policy instead of nontemporal loads, 6 / 7 = 2 / 3 with each packet's last
- * 128-byte line loaded with the default policy, 8 / 9 = 2 / 6 with short
- * packets sharing passes: 4 per pass on 16 lanes each or 2 on 32), 10-13 = flat
- * kernel (each tile's byte extent streamed densely with a wave prefix scan
- * over 16-byte unit sums; 2 or 4 units per lane per chunk, 11 / 13 with the
- * next chunk in flight), 14 / 15 = 13 / 11 with default-policy loads,
- * 16 / 17 = flat with 8 units per lane per chunk (17 pipelined), 18 = 16 units,
- * 19 / 20 = 16 with 1 / 2 of the 8 unit rows loaded with the default cache
- * policy, 21 = 13 with 1 of 4, 22 = 18 with 2 of 16, 23 = 17 with 1 of 8,
- * 24 / 25 = 18 with 1 / 4 of 16, 26 = 17 with 2 of 8, 27 = 18 scanned in two
- * LDS groups of 8 rows, 28 / 29 = 32 units per lane per chunk in LDS groups of
- * 16 / 8 rows, 30 / 31 / 32 = 18 / 16 / 27 with the next tile's first chunk
- * issued before the current tile's finishing step.  All variants produce
- * identical results; the knob exists for in-process A/B timing and for
- * cross-checking two independent kernels.  SCCSUM_EINVAL for an unknown one. */
+/* Diagnostic: select the kernel family for later launches in this process.
+ * 0 = default: flat kernel, 16 (>= 512 Ki packets and >= 256 MiB) else 15.
+ * 1 = one packet per wave, per-lane byte masks (independent second
+ *     implementation, kept for cross-checking).
+ * 2-9 = batch kernel (round-1 default before the flat kernel): one packet per
+ *     pass; 3 = next packet in flight, 4 / 5 = 2 / 3 with default-policy
+ *     loads, 6 / 7 = 2 / 3 with each packet's last 128-byte line
+ *     default-policy, 8 / 9 = 2 / 6 with short packets sharing passes.
+ * 10-16 = flat kernel: each tile's byte extent streamed densely, unit sums
+ *     prefix-scanned across the wave; U = 2 (10, 11), 4 (12, 13), 8 (14, 15),
+ *     16 (16) units per lane per chunk, odd = next chunk in flight.
+ * All variants produce identical results; the knob exists for in-process A/B
+ * timing and cross-checking.  SCCSUM_EINVAL for an unknown one. */
 int sccsum_set_kernel_variant(int variant);
 
 /* Diagnostic: cap the launch grid at `blocks` 256-thread workgroups per
@@ -196,7 +190,7 @@ int sccsum_set_group_units(int units);
  * 1..64 (default 64).  Results are unaffected. */
 int sccsum_set_tile_packets(int packets);
 
-/* Diagnostic: target bytes per flat-kernel tile (variants 10-13; default
+/* Diagnostic: target bytes per flat-kernel tile (variants 10-16; default
  * 0 = only the packet cap).  Results are unaffected. */
 int sccsum_set_tile_bytes(int bytes);
 
@@ -219,9 +213,6 @@ int sccsum_sync(void* stream);
 int sccsum_read_probe(const void* d_src, uint64_t bytes, uint64_t* d_sink, void* stream);
 int sccsum_read_probe_blocks(void);
 
-/* Diagnostic: how many of the read probe's 4 loads in flight use the default
- * cache policy instead of nontemporal (0, 1, 2 or 4; default 0). */
-int sccsum_set_probe_policy(int default_loads);
 
 /* ---------------------------------------------------------------------------
  * Host pipeline: batches that live in HOST memory (DPDK mbuf pools, socket

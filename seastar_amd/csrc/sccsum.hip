@@ -808,7 +808,7 @@ constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B)
 // pseudo-header, exact redo of the packets the fast path cannot take).
 // Layouts that do not run forward (shuffled offsets) degrade to one run per
 // packet — the per-packet cost of the batch kernel.
-template <int U, bool IPV4, bool FILL, bool PIPE, int AUX = kNT, int DEFROWS = 0, int SUB = U, bool XT = false>
+template <int U, bool IPV4, bool FILL, bool PIPE>
 __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
@@ -816,15 +816,12 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
     uint8_t* __restrict__ status, uint64_t n, uint32_t B, uint32_t B2, uint64_t T1, uint32_t* __restrict__ heads,
     uint32_t flags) {
     static_assert(!FILL || IPV4, "in-place generate is a frames mode");
-    constexpr uint32_t C = kWave * U;     // units per chunk
-    constexpr uint32_t CS = kWave * SUB;  // units per LDS group
-    static_assert(U % SUB == 0, "chunk rows split into whole groups");
-    static_assert(!(XT && PIPE), "cross-tile prefetch is for the unpipelined chunk loop");
+    constexpr uint32_t C = kWave * U;  // units per chunk
     constexpr int kHead = FILL ? 4 : (IPV4 ? 3 : 1);
     const bool raw = !IPV4 && (flags & kFlagRaw);
     const bool fill_ip = FILL && (flags & kFlagFillIp);
-    __shared__ u32x4 ubuf_all[kWavesPerBlock][CS];
-    __shared__ uint32_t pbuf_all[kWavesPerBlock][CS];
+    __shared__ u32x4 ubuf_all[kWavesPerBlock][C];
+    __shared__ uint32_t pbuf_all[kWavesPerBlock][C];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     u32x4* ubuf = ubuf_all[wv];
@@ -937,35 +934,16 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
     auto load = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t g, u32x4 (&v)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (u < DEFROWS) {
-                v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(16u * g + vo + 1024u * u), 0, 0);
-            } else {
-                v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(16u * g + vo + 1024u * u), 0, AUX);
-            }
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(16u * g + vo + 1024u * u), 0, kNT);
     };
 
     uint64_t o_n = 0;
     uint32_t L_n = 0, sd_n = 0;
     plan_load(t, o_n, L_n, sd_n);
     Tile cur{};
-    // XT: vpre holds chunk 0 of the current tile's first streamed run, issued
-    // before the previous tile's finishing step so no tile starts on an
-    // exposed memory round trip
-    u32x4 vpre[XT ? U : 1];
-    bool pre = false;
-    if constexpr (XT) {
-        if (t < ntiles) {
-            cur = derive(t, o_n, L_n, sd_n);
-            if (cur.streamed) {
-                const Run rn = run_of(cur, static_cast<uint32_t>(__builtin_ctzll(cur.streamed)));
-                load(run_rsrc(rn), 0, vpre);
-                pre = true;
-            }
-        }
-    }
     while (t < ntiles) {
         const uint64_t t2 = t1 < ntiles ? next_tile(t1) : ntiles;
-        if (!XT) cur = derive(t, o_n, L_n, sd_n);
+        cur = derive(t, o_n, L_n, sd_n);
         if (t1 < ntiles) plan_load(t1, o_n, L_n, sd_n);
         const uint64_t base = cur.base;
         const uint32_t cnt = cur.cnt;
@@ -989,40 +967,36 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
             const int rf = cap ? static_cast<int>(static_cast<uint32_t>(cur.fu - F)) : -0x40000000;
             const int rl = cap ? static_cast<int>(static_cast<uint32_t>(cur.lu - F)) : -0x40000000;
             uint32_t carry = 0;
-            // one chunk = U rows of 64 units; scanned, parked in LDS and
-            // captured SUB-row group by SUB-row group (LDS holds one group)
+            // one chunk = U rows of 64 units: unit sums, scanned, parked in
+            // LDS with the units; packet lanes pick up what falls in it
             auto chunk = [&](uint32_t g, const u32x4 (&v)[U]) {
+                uint32_t x[U];
 #pragma unroll
-                for (int s0 = 0; s0 < U; s0 += SUB) {
-                    uint32_t x[SUB];
+                for (int u = 0; u < U; ++u) x[u] = sad4(v[u], 0u);
+                wave_scan_n<U>(x);
 #pragma unroll
-                    for (int u = 0; u < SUB; ++u) x[u] = sad4(v[s0 + u], 0u);
-                    wave_scan_n<SUB>(x);
-#pragma unroll
-                    for (int u = 0; u < SUB; ++u) {
-                        pbuf[kWave * u + lane] = carry + x[u];
-                        ubuf[kWave * u + lane] = v[s0 + u];
-                        carry += __builtin_amdgcn_readlane(x[u], 63);
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    const int gs = static_cast<int>(g) + kWave * s0;
-                    const int a = rf - gs;
-                    if (static_cast<uint32_t>(a) < CS) {
-                        const u32x4 w = ubuf[a];
-                        pst = pbuf[a] - sad4(w, 0u);  // prefix just before the first unit
-                        hs[0] = w;
-                    }
-#pragma unroll
-                    for (int j = 1; j < kHead; ++j) {
-                        if (static_cast<uint32_t>(a + j) < CS) hs[j] = ubuf[a + j];
-                    }
-                    const int b = rl - gs;
-                    if (static_cast<uint32_t>(b) < CS) {
-                        pend = pbuf[b];
-                        hl = ubuf[b];
-                    }
-                    __builtin_amdgcn_wave_barrier();  // this group's LDS reads precede the next group's writes
+                for (int u = 0; u < U; ++u) {
+                    pbuf[kWave * u + lane] = carry + x[u];
+                    ubuf[kWave * u + lane] = v[u];
+                    carry += __builtin_amdgcn_readlane(x[u], 63);
                 }
+                __builtin_amdgcn_wave_barrier();
+                const int a = rf - static_cast<int>(g);
+                if (static_cast<uint32_t>(a) < C) {
+                    const u32x4 w = ubuf[a];
+                    pst = pbuf[a] - sad4(w, 0u);  // prefix just before the first unit
+                    hs[0] = w;
+                }
+#pragma unroll
+                for (int j = 1; j < kHead; ++j) {
+                    if (static_cast<uint32_t>(a + j) < C) hs[j] = ubuf[a + j];
+                }
+                const int b = rl - static_cast<int>(g);
+                if (static_cast<uint32_t>(b) < C) {
+                    pend = pbuf[b];
+                    hl = ubuf[b];
+                }
+                __builtin_amdgcn_wave_barrier();  // this chunk's LDS reads precede the next chunk's writes
             };
             if (PIPE) {
                 u32x4 va[U], vb[U];
@@ -1034,28 +1008,10 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
                     chunk(g + C, vb);
                 }
             } else {
-                uint32_t g = 0;
-                if constexpr (XT) {
-                    if (pre) {  // chunk 0 of the tile's first streamed run is already in flight
-                        chunk(0, vpre);
-                        g = C;
-                        pre = false;
-                    }
-                }
-                for (; g < ext; g += C) {
+                for (uint32_t g = 0; g < ext; g += C) {
                     u32x4 v[U];
                     load(r, g, v);
                     chunk(g, v);
-                }
-            }
-        }
-        if constexpr (XT) {  // next tile: plan, runs, first chunk in flight before this tile finishes
-            if (t1 < ntiles) {
-                cur = derive(t1, o_n, L_n, sd_n);
-                if (cur.streamed) {
-                    const Run rn = run_of(cur, static_cast<uint32_t>(__builtin_ctzll(cur.streamed)));
-                    load(run_rsrc(rn), 0, vpre);
-                    pre = true;
                 }
             }
         }
@@ -1281,24 +1237,16 @@ __global__ __launch_bounds__(kBlock) void fill_header_kernel(uint8_t* __restrict
 }
 
 // Plain stream-read of the same load shape (16 B per lane, nontemporal).
-// DEF of the four loads in flight use the default cache policy, the rest nt
-// (diagnostic: sccsum_set_probe_policy).
-template <int DEF>
-__device__ __forceinline__ u32x4 probe_load(const u32x4* p, int k) {
-    return k < DEF ? *p : __builtin_nontemporal_load(p);
-}
-
-template <int DEF>
 __global__ __launch_bounds__(kBlock) void read_probe_kernel(const u32x4* __restrict__ src, uint64_t units,
                                                              uint64_t* __restrict__ sink) {
     uint64_t acc = 0;
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock;
     uint64_t i = static_cast<uint64_t>(xcd_block_id()) * kBlock + threadIdx.x;
     for (; i + 3 * stride < units; i += 4 * stride) {
-        const u32x4 a = probe_load<DEF>(src + i, 0);
-        const u32x4 b = probe_load<DEF>(src + i + stride, 1);
-        const u32x4 c = probe_load<DEF>(src + i + 2 * stride, 2);
-        const u32x4 d = probe_load<DEF>(src + i + 3 * stride, 3);
+        const u32x4 a = __builtin_nontemporal_load(src + i);
+        const u32x4 b = __builtin_nontemporal_load(src + i + stride);
+        const u32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
+        const u32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
         acc += static_cast<uint64_t>(a.x) + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
         acc += static_cast<uint64_t>(c.x) + c.y + c.z + c.w + d.x + d.y + d.z + d.w;
     }
@@ -1476,66 +1424,18 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     const uint32_t b32 = static_cast<uint32_t>(B);
     uint32_t* heads = nullptr;
     if (g_dynamic.load(std::memory_order_relaxed)) heads = next_heads();
-    if (variant >= 10) {  // flat kernel: 10 / 11 = U 2 (11 pipelined), 12 / 13 = U 4 (13 pipelined),
-                          // 14 / 15 = 13 / 11 with default-policy loads, 16 / 17 = U 8, 18 = U 16,
-                          // 19 / 20 = 16 with 1 / 2 of the 8 rows default-policy, 21 = 13 with 1 of 4,
-                          // 22 = 18 with 2 of 16, 23 = 17 with 1 of 8, 24 / 25 = 18 with 1 / 4 of 16,
-                          // 26 = 17 with 2 of 8, 27 = 18 scanned in 2 LDS groups of 8 rows,
-                          // 28 / 29 = 32 units per lane per chunk in groups of 16 / 8 rows,
-                          // 30 / 31 / 32 = 18 / 16 / 27 with the next tile's first chunk in flight
+    if (variant >= 10) {  // flat kernel: 10 / 11 = U 2, 12 / 13 = U 4, 14 / 15 = U 8 (odd: next chunk in flight), 16 = U 16
         auto go = [&](auto kern) { launch_flat(kern, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags); };
-        if (IPV4 && (flags & kFlagFillL4)) {
-            switch (variant) {
-                case 10: go(csum_flat_kernel<2, IPV4, IPV4, false>); break;
-                case 11: go(csum_flat_kernel<2, IPV4, IPV4, true>); break;
-                case 12: go(csum_flat_kernel<4, IPV4, IPV4, false>); break;
-                case 14: go(csum_flat_kernel<4, IPV4, IPV4, true, 0>); break;
-                case 15: go(csum_flat_kernel<2, IPV4, IPV4, true, 0>); break;
-                case 16: go(csum_flat_kernel<8, IPV4, IPV4, false>); break;
-                case 17: go(csum_flat_kernel<8, IPV4, IPV4, true>); break;
-                case 18: go(csum_flat_kernel<16, IPV4, IPV4, false>); break;
-                case 19: go(csum_flat_kernel<8, IPV4, IPV4, false, kNT, 1>); break;
-                case 20: go(csum_flat_kernel<8, IPV4, IPV4, false, kNT, 2>); break;
-                case 21: go(csum_flat_kernel<4, IPV4, IPV4, true, kNT, 1>); break;
-                case 22: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 2>); break;
-                case 23: go(csum_flat_kernel<8, IPV4, IPV4, true, kNT, 1>); break;
-                case 24: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 1>); break;
-                case 25: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 4>); break;
-                case 26: go(csum_flat_kernel<8, IPV4, IPV4, true, kNT, 2>); break;
-                case 27: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 0, 8>); break;
-                case 28: go(csum_flat_kernel<32, IPV4, IPV4, false, kNT, 0, 16>); break;
-                case 29: go(csum_flat_kernel<32, IPV4, IPV4, false, kNT, 0, 8>); break;
-                case 30: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 0, 16, true>); break;
-                case 31: go(csum_flat_kernel<8, IPV4, IPV4, false, kNT, 0, 8, true>); break;
-                case 32: go(csum_flat_kernel<16, IPV4, IPV4, false, kNT, 0, 8, true>); break;
-                default: go(csum_flat_kernel<4, IPV4, IPV4, true>); break;
-            }
-        } else {
-            switch (variant) {
-                case 10: go(csum_flat_kernel<2, IPV4, false, false>); break;
-                case 11: go(csum_flat_kernel<2, IPV4, false, true>); break;
-                case 12: go(csum_flat_kernel<4, IPV4, false, false>); break;
-                case 14: go(csum_flat_kernel<4, IPV4, false, true, 0>); break;
-                case 15: go(csum_flat_kernel<2, IPV4, false, true, 0>); break;
-                case 16: go(csum_flat_kernel<8, IPV4, false, false>); break;
-                case 17: go(csum_flat_kernel<8, IPV4, false, true>); break;
-                case 18: go(csum_flat_kernel<16, IPV4, false, false>); break;
-                case 19: go(csum_flat_kernel<8, IPV4, false, false, kNT, 1>); break;
-                case 20: go(csum_flat_kernel<8, IPV4, false, false, kNT, 2>); break;
-                case 21: go(csum_flat_kernel<4, IPV4, false, true, kNT, 1>); break;
-                case 22: go(csum_flat_kernel<16, IPV4, false, false, kNT, 2>); break;
-                case 23: go(csum_flat_kernel<8, IPV4, false, true, kNT, 1>); break;
-                case 24: go(csum_flat_kernel<16, IPV4, false, false, kNT, 1>); break;
-                case 25: go(csum_flat_kernel<16, IPV4, false, false, kNT, 4>); break;
-                case 26: go(csum_flat_kernel<8, IPV4, false, true, kNT, 2>); break;
-                case 27: go(csum_flat_kernel<16, IPV4, false, false, kNT, 0, 8>); break;
-                case 28: go(csum_flat_kernel<32, IPV4, false, false, kNT, 0, 16>); break;
-                case 29: go(csum_flat_kernel<32, IPV4, false, false, kNT, 0, 8>); break;
-                case 30: go(csum_flat_kernel<16, IPV4, false, false, kNT, 0, 16, true>); break;
-                case 31: go(csum_flat_kernel<8, IPV4, false, false, kNT, 0, 8, true>); break;
-                case 32: go(csum_flat_kernel<16, IPV4, false, false, kNT, 0, 8, true>); break;
-                default: go(csum_flat_kernel<4, IPV4, false, true>); break;
-            }
+        constexpr bool F = IPV4;  // frames may fill in place; spans never do
+        const bool fill = IPV4 && (flags & kFlagFillL4);
+        switch (variant) {
+            case 10: fill ? go(csum_flat_kernel<2, IPV4, F, false>) : go(csum_flat_kernel<2, IPV4, false, false>); break;
+            case 11: fill ? go(csum_flat_kernel<2, IPV4, F, true>) : go(csum_flat_kernel<2, IPV4, false, true>); break;
+            case 12: fill ? go(csum_flat_kernel<4, IPV4, F, false>) : go(csum_flat_kernel<4, IPV4, false, false>); break;
+            case 13: fill ? go(csum_flat_kernel<4, IPV4, F, true>) : go(csum_flat_kernel<4, IPV4, false, true>); break;
+            case 14: fill ? go(csum_flat_kernel<8, IPV4, F, false>) : go(csum_flat_kernel<8, IPV4, false, false>); break;
+            case 15: fill ? go(csum_flat_kernel<8, IPV4, F, true>) : go(csum_flat_kernel<8, IPV4, false, true>); break;
+            default: fill ? go(csum_flat_kernel<16, IPV4, F, false>) : go(csum_flat_kernel<16, IPV4, false, false>); break;
         }
         return;
     }
@@ -1603,7 +1503,7 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
     // chunk for big batches (>= 512 Ki packets and 256 MiB), else 8 units with
     // the next chunk in flight: the 16-unit form runs 2 waves per SIMD, too
     // few tiles per wave on smaller batches (DESIGN.md §5.1 has the A/B)
-    if (variant == 0) variant = (n >= (512u << 10) && bytes_len >= (256ull << 20)) ? 18 : 17;
+    if (variant == 0) variant = (n >= (512u << 10) && bytes_len >= (256ull << 20)) ? 16 : 15;
     if (variant == 1 && (flags & kFlagFillL4)) variant = 6;  // in-place write-back lives in the batch kernel
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
@@ -1729,7 +1629,7 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
 }
 
 int sccsum_set_kernel_variant(int variant) {
-    if (variant < 0 || variant > 32) return SCCSUM_EINVAL;
+    if (variant < 0 || variant > 16) return SCCSUM_EINVAL;
     sccsum::g_variant.store(variant, std::memory_order_relaxed);
     return SCCSUM_OK;
 }
@@ -1778,21 +1678,9 @@ int sccsum_read_probe_blocks(void) { return sccsum::cu_count() * sccsum::kBlocks
 int sccsum_read_probe(const void* d_src, uint64_t bytes, uint64_t* d_sink, void* stream) {
     if (!d_src || !d_sink || (bytes & 15u) || (reinterpret_cast<uintptr_t>(d_src) & 15u)) return SCCSUM_EINVAL;
     const unsigned grid = static_cast<unsigned>(sccsum_read_probe_blocks()) & ~7u;
-    const auto* src = static_cast<const sccsum::u32x4*>(d_src);
-    const auto hs = static_cast<hipStream_t>(stream);
-    switch (sccsum::g_probe_default.load(std::memory_order_relaxed)) {
-        case 1: sccsum::read_probe_kernel<1><<<dim3(grid), dim3(sccsum::kBlock), 0, hs>>>(src, bytes / 16, d_sink); break;
-        case 2: sccsum::read_probe_kernel<2><<<dim3(grid), dim3(sccsum::kBlock), 0, hs>>>(src, bytes / 16, d_sink); break;
-        case 4: sccsum::read_probe_kernel<4><<<dim3(grid), dim3(sccsum::kBlock), 0, hs>>>(src, bytes / 16, d_sink); break;
-        default: sccsum::read_probe_kernel<0><<<dim3(grid), dim3(sccsum::kBlock), 0, hs>>>(src, bytes / 16, d_sink); break;
-    }
+    sccsum::read_probe_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const sccsum::u32x4*>(d_src), bytes / 16, d_sink);
     return static_cast<int>(hipGetLastError());
-}
-
-int sccsum_set_probe_policy(int default_loads) {
-    if (default_loads != 0 && default_loads != 1 && default_loads != 2 && default_loads != 4) return SCCSUM_EINVAL;
-    sccsum::g_probe_default.store(default_loads, std::memory_order_relaxed);
-    return SCCSUM_OK;
 }
 
 }  // extern "C"

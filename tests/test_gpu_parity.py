@@ -20,13 +20,10 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(params=list(range(1, 33)),
+@pytest.fixture(params=list(range(1, 17)),
                 ids=["simple", "batch", "batch_pipe", "batch_dflt", "batch_pipe_dflt", "batch_hyb", "batch_pipe_hyb",
-                     "batch_multi", "batch_hyb_multi", "flat2", "flat2_pipe", "flat4", "flat4_pipe", "flat4_pipe_dflt",
-                     "flat2_pipe_dflt", "flat8", "flat8_pipe", "flat16", "flat8_mix1",
-                     "flat8_mix2", "flat4_pipe_mix1", "flat16_mix2", "flat8_pipe_mix1",
-                     "flat16_mix1", "flat16_mix4", "flat8_pipe_mix2", "flat16_sub8", "flat32_sub16",
-                     "flat32_sub8", "flat16_xt", "flat8_xt", "flat16_sub8_xt"], autouse=True)
+                     "batch_multi", "batch_hyb_multi", "flat2", "flat2_pipe", "flat4", "flat4_pipe", "flat8",
+                     "flat8_pipe", "flat16"], autouse=True)
 def kernel_variant(request, dev):
     """Every parity test runs against both kernel families."""
     lib = native.load()
@@ -268,7 +265,7 @@ def test_zipf_large_frames(dev):
 def test_host_pipeline_mbuf_pool(dev, gather, kernel_variant):
     """cfg 5 path: frames in an mbuf-shaped pinned pool, chunked through the
     GPU with async copies; small chunks force many stage recycles."""
-    if kernel_variant not in (1, 6, 10):
+    if kernel_variant not in (1, 6, 15):
         pytest.skip("pipeline exercised with two kernel families")
     from seastar_amd import pipeline
 
