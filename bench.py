@@ -278,7 +278,8 @@ def run_e2e(args, world, rank, dev):
     """cfg 5: frames in a pinned, DPDK-mbuf-shaped host pool (2304-B slots,
     data at +256); chunks H2D on a copy stream, kernel on a compute stream,
     results D2H, 3 chunks in flight.  A = slots copied as they lie; B =
-    packets gathered into pinned staging first (only packet bytes cross PCIe)."""
+    packets gathered into pinned staging first; C = one 2D DMA per chunk of
+    each slot's packet bytes (B and C: only packet bytes cross PCIe)."""
     from seastar_amd import pipeline
 
     n = args.packets
@@ -293,8 +294,9 @@ def run_e2e(args, world, rank, dev):
     del tx
     torch.cuda.empty_cache()
     res = {}
-    for name, gather, chunk_bytes in (("A_slots_as_is", False, 65536 * pipeline.MBUF_SLOT),
-                                      ("B_gathered", True, 65536 * FRAME)):
+    for name, gather, chunk_bytes in (("A_slots_as_is", native.GATHER_NONE, 65536 * pipeline.MBUF_SLOT),
+                                      ("B_gathered", native.GATHER_HOST, 65536 * FRAME),
+                                      ("C_strided_dma", native.GATHER_STRIDED, 65536 * ((FRAME + 15) & ~15))):
         pl = pipeline.HostPipeline(dev.index or 0, chunk_bytes=chunk_bytes, chunk_packets=65536, depth=3)
         got = pl.run(native.PIPE_IPV4, pool, off, length, gather=gather, max_len=FRAME)
         assert np.array_equal(got, want), f"e2e {name} mismatch vs device-resident results"
@@ -305,7 +307,7 @@ def run_e2e(args, world, rank, dev):
             times.append(time.perf_counter() - t0)
         pl.close()
         t = float(np.median(times))
-        pcie = n * (pipeline.MBUF_SLOT if not gather else FRAME) + n * (12 + 4)
+        pcie = n * (pipeline.MBUF_SLOT if gather == native.GATHER_NONE else FRAME) + n * (12 + 4)
         res[name] = {"GiBps_packet_bytes": round(n * FRAME / t / 2**30, 2), "ms_per_batch": round(t * 1e3, 2),
                      "pcie_GBps_h2d_plus_d2h": round(pcie / t / 1e9, 2)}
     if rank == 0:

@@ -135,6 +135,37 @@ int sccsum_fragments(const void* d_bytes, uint64_t bytes_len,
 uint64_t sccsum_fragments_workspace(uint64_t nfrag);
 
 /* sccsum_ipv4_fill modes */
+/* ---- RSS: the Toeplitz hash the rx path steers flows by --------------------
+ * include/seastar/net/toeplitz.hh:78-98 over the forward_hash the stack
+ * builds for a frame (net.hh:53-75):
+ *   SCCSUM_RSS_DISPATCH (net.cc:330-341 -> ip.cc:77-92): src + dst IP, then
+ *     for an atomic TCP / UDP datagram (MF clear, fragment offset 0) the 4
+ *     port bytes at frame offset 20 (sizeof(ip_hdr): options not skipped),
+ *     if the frame holds the TCP (20 B) / UDP (8 B) header there
+ *     (tcp.hh:852-862, udp.cc:153-161);
+ *   SCCSUM_RSS_REASSEMBLED (ip.cc:186-197): src + dst IP, then the ports at
+ *     4*ihl when the L4 part (up to min(ip total length, len)) holds the
+ *     TCP / UDP header.
+ * key: HOST pointer, key_len >= 4 bytes (the reference's defaults are 40 and
+ * 52 bytes, toeplitz.hh:52-71; only the first 16 can reach a 12-byte input).
+ * d_hash[i] = the 32-bit hash; 0 for a malformed frame (shorter than 20 B, or
+ * REASSEMBLED with 4*ihl past the datagram: status SCCSUM_ST_MALFORMED) or an
+ * out-of-range one (SCCSUM_ST_RANGE). */
+#define SCCSUM_RSS_DISPATCH    0
+#define SCCSUM_RSS_REASSEMBLED 1
+
+/* RSS hashes alone (one thread per frame, reads ~28 header bytes each). */
+int sccsum_ipv4_rss(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
+                    const uint8_t* key, uint32_t key_len, int mode, uint32_t* d_hash, uint8_t* d_status, uint64_t n,
+                    void* stream);
+
+/* sccsum_ipv4_frames plus the RSS hash of every frame in the same pass (the
+ * flat kernel computes it from the header bytes it already holds; no extra
+ * HBM traffic beyond the 4-byte hash). */
+int sccsum_ipv4_frames_rss(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
+                           uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len, const uint8_t* key,
+                           uint32_t key_len, int rss_mode, uint32_t* d_hash, void* stream);
+
 #define SCCSUM_FILL_IP        0x01u /* IPv4 header checksum, field at +10 (ip.cc:266-278) */
 #define SCCSUM_FILL_L4        0x02u /* full TCP/UDP checksum: pseudo-header + segment (udp.cc:190-192,
                                        tcp.hh:1691-1692 without tx offload) */
@@ -227,16 +258,24 @@ typedef struct sccsum_pipeline sccsum_pipeline;
 #define SCCSUM_PIPE_SPANS 0
 #define SCCSUM_PIPE_IPV4  1
 
+#define SCCSUM_GATHER_NONE    0 /* copy each chunk's covering byte range as it lies */
+#define SCCSUM_GATHER_HOST    1 /* pack packets into pinned staging on the host first */
+#define SCCSUM_GATHER_STRIDED 2 /* packets at one pitch (mbuf slots): one 2D DMA of each slot's packet bytes */
+
 /* Allocate device buffers and pinned staging for `depth` chunks on `device`. */
 int sccsum_pipeline_create(int device, uint64_t chunk_bytes, uint32_t chunk_packets, int depth,
                            sccsum_pipeline** out);
 
 /* Checksum n packets at host_bytes[host_off[i] .. +host_len[i]) (all HOST
- * pointers; host_bytes should be pinned — sccsum_host_alloc — when gather is
- * 0).  gather = 0: each chunk's covering byte range is copied as it lies
+ * pointers; host_bytes should be pinned — sccsum_host_alloc — unless gather
+ * is 1).  gather = 0: each chunk's covering byte range is copied as it lies
  * (e.g. whole mbuf slots, headers and headroom included); gather = 1: the
  * packets are first packed into pinned staging on the host (only packet bytes
- * cross PCIe).  mode = SCCSUM_PIPE_SPANS (host_seed optional, host_out[n]) or
+ * cross PCIe); gather = 2: where a chunk's packets sit at one pitch P (the
+ * slots of an mbuf pool, dpdk.cc:139-156) and none is longer than P, one 2D
+ * DMA (hipMemcpy2DAsync) copies the first W bytes of each slot, W = the
+ * chunk's longest packet — only packet bytes cross PCIe, with no host copy;
+ * other chunks are copied as they lie.  mode = SCCSUM_PIPE_SPANS (host_seed optional, host_out[n]) or
  * SCCSUM_PIPE_IPV4 (host_out[2n]); host_status optional.  Returns when all
  * results are in host_out.  host_len is the size of the host_bytes area. */
 int sccsum_pipeline_run(sccsum_pipeline* p, int mode, int gather, const void* host_bytes, uint64_t host_len,

@@ -53,6 +53,9 @@ def lib():
             "oracle_batch_ipv4": (None, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int]),
             "oracle_batch_fragments": (None, [_P, _P, _P, _P, _P, _P, ctypes.c_uint64]),
             "oracle_batch_ipv4_fill": (None, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_uint32]),
+            "oracle_toeplitz": (ctypes.c_uint32, [_P, ctypes.c_size_t, _P, ctypes.c_size_t]),
+            "oracle_batch_ipv4_rss": (None, [_P, _P, _P, ctypes.c_uint64, _P, ctypes.c_size_t, ctypes.c_int, _P,
+                                             _P]),
         }
         for name, (res, args) in protos.items():
             fn = getattr(L, name)
@@ -141,3 +144,26 @@ def batch_ipv4_fill(buf, off, length, mode):
     st = np.empty(n, dtype=np.uint8)
     lib().oracle_batch_ipv4_fill(_addr(buf), _addr(off), _addr(length), _addr(out2), _addr(st), n, mode)
     return buf, out2.reshape(n, 2), st
+
+
+# Mellanox driver key the reference ships as its default (toeplitz.hh:52-58)
+RSS_KEY_40 = bytes.fromhex("d181c62cf7f4db5b1983a2fc943e1adbd9389e6bd1039c2ca74499ad593d56d9f3253c062adc1ffc")
+
+
+def toeplitz(key: bytes, data: bytes) -> int:
+    kb = np.frombuffer(bytes(key), np.uint8)
+    db = np.frombuffer(bytes(data), np.uint8) if data else np.zeros(1, np.uint8)
+    return int(lib().oracle_toeplitz(_addr(kb), kb.size, _addr(db), len(data)))
+
+
+def batch_ipv4_rss(buf, off, length, key: bytes = RSS_KEY_40, mode: int = 0):
+    """(hash u32 [n], status u8 [n]) per frame, as oracle_ipv4_rss."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    kb = np.frombuffer(bytes(key), np.uint8)
+    h = np.empty(off.size, dtype=np.uint32)
+    st = np.empty(off.size, dtype=np.uint8)
+    lib().oracle_batch_ipv4_rss(_addr(buf), _addr(off), _addr(length), off.size, _addr(kb), kb.size, mode,
+                                _addr(h), _addr(st))
+    return h, st

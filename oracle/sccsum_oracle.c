@@ -319,3 +319,63 @@ void oracle_batch_ipv4_fill(uint8_t* bytes, const uint64_t* off, const uint32_t*
         if (status) status[i] = st;
     }
 }
+
+/* ---- RSS (Toeplitz) -------------------------------------------------------- */
+
+/* include/seastar/net/toeplitz.hh:78-98, bit for bit. */
+uint32_t oracle_toeplitz(const uint8_t* key, size_t key_len, const uint8_t* data, size_t len) {
+    uint32_t hash = 0;
+    uint32_t v = ((uint32_t)key[0] << 24) + ((uint32_t)key[1] << 16) + ((uint32_t)key[2] << 8) + key[3];
+    for (size_t i = 0; i < len; i++) {
+        for (unsigned b = 0; b < 8; b++) {
+            if (data[i] & (1u << (7 - b))) hash ^= v;
+            v <<= 1;
+            if ((i + 4) < key_len && (key[i + 4] & (1u << (7 - b)))) v |= 1;
+        }
+    }
+    return hash;
+}
+
+uint32_t oracle_ipv4_rss(const uint8_t* p, size_t len, const uint8_t* key, size_t key_len, int mode,
+                         uint8_t* status) {
+    uint8_t data[12];
+    size_t n = 0;
+    *status = 0;
+    if (len < 20) {
+        *status = 4;
+        return 0;
+    }
+    memcpy(data, p + 12, 8); /* ip.cc:81-82: src_ip, dst_ip as stored (network order) */
+    n = 8;
+    const uint8_t proto = p[9];
+    const uint32_t need = proto == 6 ? 20 : (proto == 17 ? 8 : 0); /* tcp_hdr::len / sizeof(udp_hdr) */
+    if (mode == 0) {
+        const uint32_t frag = ((uint32_t)p[6] << 8) | p[7];
+        const int mf = (frag & 0x2000) != 0, offset = (frag & 0x1fff) != 0; /* ip.hh:390-391 */
+        if (need && !mf && !offset && len >= 20 + need) {                 /* ip.cc:87-89 */
+            memcpy(data + 8, p + 20, 4);
+            n = 12;
+        }
+    } else {
+        const uint32_t ihl = p[0] & 0xf, ip_len = ((uint32_t)p[2] << 8) | p[3];
+        const uint32_t l4_off = 4 * ihl, l4_end = ip_len < len ? ip_len : (uint32_t)len;
+        if (l4_off > l4_end) {
+            *status = 4;
+            return 0;
+        }
+        if (need && l4_end - l4_off >= need) {
+            memcpy(data + 8, p + l4_off, 4);
+            n = 12;
+        }
+    }
+    return oracle_toeplitz(key, key_len, data, n);
+}
+
+void oracle_batch_ipv4_rss(const uint8_t* bytes, const uint64_t* off, const uint32_t* len, uint64_t n,
+                           const uint8_t* key, size_t key_len, int mode, uint32_t* hash, uint8_t* status) {
+    for (uint64_t i = 0; i < n; ++i) {
+        uint8_t st = 0;
+        hash[i] = oracle_ipv4_rss(bytes + off[i], len[i], key, key_len, mode, &st);
+        if (status) status[i] = st;
+    }
+}

@@ -96,6 +96,26 @@ void oracle_batch_ipv4_fill(uint8_t* bytes, const uint64_t* off, const uint32_t*
 /* Fold a checksummer csum to a seed value (end-around carry, zero stays zero). */
 uint32_t oracle_fold_seed(const oracle_checksummer* c);
 
+/* toeplitz_hash(key, data), include/seastar/net/toeplitz.hh:78-98: for each
+ * data bit, MSB first, XOR in the 32-bit key window that starts at that bit;
+ * key bits shift into the window while i + 4 < key_len. */
+uint32_t oracle_toeplitz(const uint8_t* key, size_t key_len, const uint8_t* data, size_t len);
+
+/* RSS hash of one IPv4 frame (no Ethernet header) as the native stack builds
+ * its forward_hash (net.hh:53-75: bytes in wire order):
+ *   mode 0 (dispatch, net.cc:330-341 -> ip.cc:77-92): src + dst IP, then for
+ *     an atomic datagram (MF clear, offset 0) of TCP (tcp.hh:852-862, needs
+ *     20 B) or UDP (udp.cc:153-161, needs 8 B) the 4 port bytes at frame
+ *     offset 20 (sizeof(ip_hdr), IP options not skipped);
+ *   mode 1 (reassembled datagram, ip.cc:186-197): src + dst IP, then for TCP /
+ *     UDP the 4 port bytes at 4*ihl when the L4 part (up to min(ip_len, len))
+ *     holds 20 / 8 bytes.
+ * status: 0 ok, 4 malformed (shorter than 20 B, or 4*ihl past the end: hash 0). */
+uint32_t oracle_ipv4_rss(const uint8_t* frame, size_t len, const uint8_t* key, size_t key_len, int mode,
+                         uint8_t* status);
+void oracle_batch_ipv4_rss(const uint8_t* bytes, const uint64_t* off, const uint32_t* len, uint64_t n,
+                           const uint8_t* key, size_t key_len, int mode, uint32_t* hash, uint8_t* status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,6 +8,7 @@ libsccsum.so.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 import numpy as np
@@ -113,6 +114,48 @@ def ipv4_fill(batch: PacketBatch, mode: int = native.FILL_IP | native.FILL_L4, o
     )
     native.check(code, "sccsum_ipv4_fill")
     return None if out2 is None else out2[: 2 * n].view(n, 2)
+
+
+# The reference's default RSS key (Mellanox driver key, toeplitz.hh:52-58).
+RSS_KEY_40 = bytes.fromhex("d181c62cf7f4db5b1983a2fc943e1adbd9389e6bd1039c2ca74499ad593d56d9f3253c062adc1ffc")
+
+
+def _key(key: bytes):
+    kb = bytes(key)
+    return (ctypes.c_uint8 * len(kb)).from_buffer_copy(kb), len(kb)
+
+
+def ipv4_rss(batch: PacketBatch, key: bytes = RSS_KEY_40, mode: int = native.RSS_DISPATCH,
+             hash_out: torch.Tensor | None = None, status: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """sccsum_ipv4_rss: the Toeplitz RSS hash of every frame (int32 tensor [n])."""
+    lib = native.load()
+    n = batch.n
+    if hash_out is None:
+        hash_out = torch.empty(max(n, 1), dtype=torch.int32, device=batch.device)
+    kb, kl = _key(key)
+    code = lib.sccsum_ipv4_rss(ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off),
+                               ctypes_ptr(batch.length), ctypes.addressof(kb), kl, mode, ctypes_ptr(hash_out),
+                               _ptr(status), n, _stream(stream))
+    native.check(code, "sccsum_ipv4_rss")
+    return hash_out[:n]
+
+
+def ipv4_frames_rss(batch: PacketBatch, key: bytes = RSS_KEY_40, mode: int = native.RSS_DISPATCH,
+                    out2: torch.Tensor | None = None, status: torch.Tensor | None = None,
+                    hash_out: torch.Tensor | None = None, stream=None):
+    """sccsum_ipv4_frames_rss: ([n, 2] int16 checksums, [n] int32 RSS hashes) in one pass."""
+    lib = native.load()
+    n = batch.n
+    if out2 is None:
+        out2 = torch.empty(max(2 * n, 2), dtype=torch.int16, device=batch.device)
+    if hash_out is None:
+        hash_out = torch.empty(max(n, 1), dtype=torch.int32, device=batch.device)
+    kb, kl = _key(key)
+    code = lib.sccsum_ipv4_frames_rss(
+        ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length), ctypes_ptr(out2),
+        _ptr(status), n, batch.max_len, ctypes.addressof(kb), kl, mode, ctypes_ptr(hash_out), _stream(stream))
+    native.check(code, "sccsum_ipv4_frames_rss")
+    return (out2[: 2 * n].view(n, 2) if n else out2[:0].view(0, 2)), hash_out[:n]
 
 
 def fragments(data: torch.Tensor, bytes_len: int, frag_off: torch.Tensor, frag_len: torch.Tensor,

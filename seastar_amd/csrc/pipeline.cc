@@ -6,7 +6,8 @@
 // dpdk.cc:139-156: 128 B rte_mbuf + 128 B headroom + 2048 B data room per
 // slot; virtio rx buffers).  A pipeline cuts a host batch into chunks; chunk
 // c uses stage c % depth:
-//   copy stream:    [gather into pinned staging (host memcpy) |] H2D bytes + offsets/lengths/seeds
+//   copy stream:    [gather into pinned staging (host memcpy) |] H2D bytes (as they lie, or one 2D
+//                   DMA of each slot's packet bytes) + offsets/lengths/seeds
 //   compute stream: wait(copied[c]) -> sccsum kernel -> D2H results -> record(done[c])
 // so the H2D of chunk c+1 overlaps the kernel of chunk c and the D2H of c-1.
 // Results land in pinned staging and are copied to the caller's arrays when
@@ -150,7 +151,7 @@ int run_chunks(sccsum_pipeline* p, int mode, int gather, const void* host_bytes,
                const uint64_t* host_off, const uint32_t* host_lens, const uint32_t* host_seed, uint64_t n,
                uint32_t max_len, uint16_t* host_out, uint8_t* host_status) {
     if (!p || (mode != SCCSUM_PIPE_SPANS && mode != SCCSUM_PIPE_IPV4) || !host_off || !host_lens || !host_out ||
-        (n && !host_bytes)) {
+        (n && !host_bytes) || gather < 0 || gather > SCCSUM_GATHER_STRIDED) {
         return SCCSUM_EINVAL;
     }
     SCCSUM_TRY(hipSetDevice(p->device));
@@ -164,13 +165,27 @@ int run_chunks(sccsum_pipeline* p, int mode, int gather, const void* host_bytes,
         if (rcf != SCCSUM_OK) return rcf;
         // take packets while they fit the chunk (by count and by bytes)
         uint64_t j = i, lo = UINT64_MAX, hi = 0, packed = 0;
+        // strided (gather == 2): packets at one pitch P (an mbuf pool's slots);
+        // each row's first W bytes (the longest packet so far) cross PCIe as
+        // one 2D DMA into rows of Wd = round16(W) bytes on the device
+        bool rows = gather == SCCSUM_GATHER_STRIDED && n - i >= 2;
+        const uint64_t P = rows ? host_off[i + 1] - host_off[i] : 0;
+        rows = rows && host_off[i + 1] > host_off[i];
+        uint64_t W = 0;
         for (; j < n && j - i < p->chunk_packets; ++j) {
             const uint64_t o = host_off[j], L = host_lens[j];
             if (o > host_len || L > host_len - o) return SCCSUM_EINVAL;  // outside the caller's buffer
-            if (gather) {
+            if (rows) {
+                const bool on_pitch = j == i || o == host_off[j - 1] + P;
+                const uint64_t nW = std::max(W, L);
+                if (j > i && (!on_pitch || L > P || (j - i + 1) * ((nW + 15) & ~uint64_t(15)) > p->chunk_bytes)) break;
+                if (j == i && L > P) rows = false;  // not slot-shaped after all: copy as it lies
+                W = nW;
+            }
+            if (gather == 1) {
                 if (j > i && packed + L > p->chunk_bytes) break;
                 packed += L;
-            } else {
+            } else if (!rows) {
                 const uint64_t nlo = std::min(lo, o), nhi = std::max(hi, o + L);
                 if (j > i && nhi - nlo > p->chunk_bytes) break;
                 lo = nlo;
@@ -178,9 +193,21 @@ int run_chunks(sccsum_pipeline* p, int mode, int gather, const void* host_bytes,
             }
         }
         const uint64_t npk = j - i;
-        if (gather ? packed > p->chunk_bytes : hi - lo > p->chunk_bytes) return SCCSUM_EINVAL;  // one oversized packet
+        if (rows && npk < 2) rows = false;
+        if (!rows && gather == SCCSUM_GATHER_STRIDED) {  // irregular chunk: recompute its covering range
+            lo = UINT64_MAX;
+            hi = 0;
+            for (uint64_t k = i; k < j; ++k) {
+                lo = std::min(lo, host_off[k]);
+                hi = std::max(hi, host_off[k] + host_lens[k]);
+            }
+        }
+        const uint64_t Wd = (W + 15) & ~uint64_t(15);
+        if (gather == 1 ? packed > p->chunk_bytes : (rows ? npk * Wd > p->chunk_bytes : hi - lo > p->chunk_bytes)) {
+            return SCCSUM_EINVAL;  // one oversized packet
+        }
         uint64_t nbytes;
-        if (gather) {
+        if (gather == 1) {
             uint64_t pos = 0;
             for (uint64_t k = 0; k < npk; ++k) {
                 std::memcpy(s.h_bytes + pos, src + host_off[i + k], host_lens[i + k]);
@@ -188,13 +215,21 @@ int run_chunks(sccsum_pipeline* p, int mode, int gather, const void* host_bytes,
                 pos += host_lens[i + k];
             }
             nbytes = pos;
+        } else if (rows) {
+            for (uint64_t k = 0; k < npk; ++k) s.h_off[k] = k * Wd;
+            nbytes = npk * Wd;
         } else {
             for (uint64_t k = 0; k < npk; ++k) s.h_off[k] = host_off[i + k] - lo;
             nbytes = hi - lo;
         }
         std::memcpy(s.h_len, host_lens + i, npk * 4);
         if (host_seed) std::memcpy(s.h_seed, host_seed + i, npk * 4);
-        SCCSUM_TRY(hipMemcpyAsync(s.d_bytes, gather ? s.h_bytes : src + lo, nbytes, hipMemcpyHostToDevice, p->copy));
+        if (rows) {
+            SCCSUM_TRY(hipMemcpy2DAsync(s.d_bytes, Wd, src + host_off[i], P, W, npk, hipMemcpyHostToDevice, p->copy));
+        } else {
+            SCCSUM_TRY(hipMemcpyAsync(s.d_bytes, gather == 1 ? s.h_bytes : src + lo, nbytes, hipMemcpyHostToDevice,
+                                      p->copy));
+        }
         SCCSUM_TRY(hipMemcpyAsync(s.d_off, s.h_off, npk * 8, hipMemcpyHostToDevice, p->copy));
         SCCSUM_TRY(hipMemcpyAsync(s.d_len, s.h_len, npk * 4, hipMemcpyHostToDevice, p->copy));
         if (host_seed) SCCSUM_TRY(hipMemcpyAsync(s.d_seed, s.h_seed, npk * 4, hipMemcpyHostToDevice, p->copy));

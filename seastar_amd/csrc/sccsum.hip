@@ -750,6 +750,107 @@ __global__ __launch_bounds__(kBlock, FILL ? SCCSUM_FILL_MIN_WAVES : SCCSUM_BATCH
     }
 }
 
+// ---------------------------------------------------------------- RSS (Toeplitz)
+
+// toeplitz_hash (include/seastar/net/toeplitz.hh:78-98) XORs, for every set
+// data bit j (MSB first), the 32-bit key window that starts at key bit j; key
+// bits past key_len read as 0.  The host precomputes the 96 windows a 12-byte
+// IPv4 forward_hash can touch, so a lane's hash is 96 select-XORs, and a
+// datagram without ports hashes its 8 IP bytes by zeroing the port word.
+struct RssParams {
+    uint32_t* hash;  // per-frame output (nullptr: no RSS)
+    uint32_t mode;   // SCCSUM_RSS_DISPATCH / SCCSUM_RSS_REASSEMBLED
+    uint32_t w[96];  // key window at data bit j
+};
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ uint32_t toeplitz96(const RssParams& P, uint32_t d0, uint32_t d1, uint32_t d2) {
+    uint32_t h = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        h ^= (d0 & (0x80000000u >> j)) ? P.w[j] : 0u;
+        h ^= (d1 & (0x80000000u >> j)) ? P.w[32 + j] : 0u;
+        h ^= (d2 & (0x80000000u >> j)) ? P.w[64 + j] : 0u;
+    }
+    return h;
+}
+
+// The forward_hash of one IPv4 frame (net.hh:53-75, bytes in wire order):
+// h0..h4 = the header's dwords as loaded (little-endian), ports20 = the dword
+// at frame byte 20, ports_l4 = the dword at 4*ihl (REASSEMBLED only).
+//  DISPATCH (net.cc:330-341 -> ip.cc:77-92): src, dst; then for an atomic
+//    datagram (MF clear, offset 0, ip.cc:87) of TCP (tcp.hh:852-862, 20 B
+//    header) or UDP (udp.cc:153-161, 8 B) the port bytes at +20
+//    (sizeof(ip_hdr): options are not skipped), if the frame holds them.
+//  REASSEMBLED (ip.cc:186-197): src, dst; then the ports at 4*ihl when the
+//    L4 part, up to min(ip_len, len), holds the TCP / UDP header.
+// Returns false (hash 0) for a malformed frame: shorter than 20 B, or (mode 1)
+// 4*ihl past the end of the datagram.
+__device__ __forceinline__ bool rss_ipv4(const RssParams& P, uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
+                                         uint32_t h4, uint32_t ports20, uint32_t ports_l4, uint32_t L,
+                                         uint32_t& hash) {
+    const uint32_t proto = (h2 >> 8) & 0xffu;
+    const uint32_t need = proto == 6u ? 20u : (proto == 17u ? 8u : 0u);
+    uint32_t ports = 0;
+    if (P.mode == SCCSUM_RSS_DISPATCH) {
+        const uint32_t frag = swap16(h1 >> 16);  // flags + fragment offset (ip.hh:390-391)
+        if (need && (frag & 0x3fffu) == 0u && L >= 20u + need) ports = ports20;
+    } else {
+        const uint32_t l4_off = 4u * (h0 & 0xfu);
+        const uint32_t ip_len = swap16(h0 >> 16);
+        const uint32_t l4_end = ip_len < L ? ip_len : L;
+        if (l4_off > l4_end) {
+            hash = 0;
+            return false;
+        }
+        if (need && l4_end - l4_off >= need) ports = ports_l4;
+    }
+    hash = toeplitz96(P, bswap32(h3), bswap32(h4), bswap32(ports));
+    return true;
+}
+
+// Standalone RSS over a frame batch: one thread per frame, header dwords
+// loaded aligned and re-aligned with v_alignbyte (frames at any offset; the
+// buffer is readable to round16(bytes_len)).
+__global__ __launch_bounds__(kBlock) void rss_kernel(const uint8_t* __restrict__ bytes, uint64_t bytes_len,
+                                                     const uint64_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ len, uint8_t* __restrict__ status,
+                                                     uint64_t n, const RssParams P) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t o = off[i];
+    const uint32_t L = len[i];
+    uint32_t hash = 0, st = 0;
+    if (o > bytes_len || L > bytes_len - o) {
+        st = SCCSUM_ST_RANGE;
+    } else if (L < 20u) {
+        st = SCCSUM_ST_MALFORMED;
+    } else {
+        const uint8_t* p = bytes + o;
+        const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p) & 3u);
+        const uint64_t padded = (bytes_len + 15u) & ~uint64_t(15);  // readable extent of the buffer
+        auto dword_at = [&](uint64_t byte_off) -> uint32_t {          // aligned dword at bytes + byte_off
+            return byte_off + 4u <= padded ? *reinterpret_cast<const uint32_t*>(bytes + byte_off) : 0u;
+        };
+        uint32_t d[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) d[k] = dword_at(o - sh + 4u * k);  // bytes [-sh, 28 - sh) of the frame
+        const uint32_t h0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh), h1 = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+        const uint32_t h2 = __builtin_amdgcn_alignbyte(d[3], d[2], sh), h3 = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+        const uint32_t h4 = __builtin_amdgcn_alignbyte(d[5], d[4], sh), h5 = __builtin_amdgcn_alignbyte(d[6], d[5], sh);
+        uint32_t pl = h5;
+        const uint32_t l4_off = 4u * (h0 & 0xfu);
+        if (P.mode != SCCSUM_RSS_DISPATCH && l4_off != 20u && l4_off + 4u <= L) {
+            const uint64_t q = o + l4_off - sh;
+            pl = __builtin_amdgcn_alignbyte(dword_at(q + 4u), dword_at(q), sh);
+        }
+        if (!rss_ipv4(P, h0, h1, h2, h3, h4, h5, pl, L, hash)) st = SCCSUM_ST_MALFORMED;
+    }
+    P.hash[i] = hash;
+    if (status) status[i] = static_cast<uint8_t>(st);
+}
+
 // ---------------------------------------------------------------- flat kernel
 
 // Inclusive prefix sums over the 64 lanes: Hillis-Steele row scans by
@@ -814,7 +915,7 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
     const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
     uint8_t* __restrict__ status, uint64_t n, uint32_t B, uint32_t B2, uint64_t T1, uint32_t* __restrict__ heads,
-    uint32_t flags) {
+    uint32_t flags, const RssParams rss) {
     static_assert(!FILL || IPV4, "in-place generate is a frames mode");
     constexpr uint32_t C = kWave * U;  // units per chunk
     constexpr int kHead = FILL ? 4 : (IPV4 ? 3 : 1);
@@ -946,7 +1047,6 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
         cur = derive(t, o_n, L_n, sd_n);
         if (t1 < ntiles) plan_load(t1, o_n, L_n, sd_n);
         const uint64_t base = cur.base;
-        const uint32_t cnt = cur.cnt;
         const bool mine = cur.mine;
         const uint32_t L = cur.L, sd = cur.sd, head = cur.head, nunits = cur.nunits;
         const uint64_t a0 = cur.a0;
@@ -1053,6 +1153,18 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
             slow = slow || (fast && (ihl != 5u || ip_len != L));
             srs = static_cast<int>(head + l4_off);
             sre = srs + static_cast<int>(l4_len);
+            if (rss.hash != nullptr) {  // fused RSS: the 4-tuple is already in registers
+                const uint32_t h5 = header_dword(hs, head, 5);
+                uint32_t pl = h5;
+                if (rss.mode != SCCSUM_RSS_DISPATCH && ihl != 5u && l4_off + 4u <= L && mine && !range_bad) {
+                    const uint8_t* q = reinterpret_cast<const uint8_t*>(a0) + head + l4_off;  // options: rare
+                    pl = static_cast<uint32_t>(q[0]) | (static_cast<uint32_t>(q[1]) << 8) |
+                         (static_cast<uint32_t>(q[2]) << 16) | (static_cast<uint32_t>(q[3]) << 24);
+                }
+                uint32_t hv = 0;
+                rss_ipv4(rss, h0, h1, h2, h3, h4, h5, pl, L, hv);
+                if (mine) rss.hash[base + lane] = (range_bad || short_frame) ? 0u : hv;
+            }
             if (FILL) {
                 const uint32_t fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
                 const bool has_field = fo != 0u && l4_len >= fo + 2u && (st & SCCSUM_ST_MALFORMED) == 0u;
@@ -1339,15 +1451,14 @@ int units_class(uint32_t max_len) {
 // 8 / 9 = 2 / 6 with short packets sharing passes (4 x 16 or 2 x 32 lanes).
 std::atomic<int> g_variant{0};
 
-std::atomic<int> g_tile_bytes{0};
-std::atomic<int> g_probe_default{0};  // read probe: loads (of 4 in flight) with the default cache policy  // flat kernel: target bytes per tile (0 = packets cap only)
+std::atomic<int> g_tile_bytes{0};  // flat kernel: target bytes per tile (0 = packets cap only)
 
 // Flat-kernel launch: the grid is what the chip holds at once (the kernel's
 // occupancy, from its VGPR and LDS use, capped by the blocks-per-CU knob), so
 // every wave's static first tile starts at launch; tiles hold about
 // g_tile_bytes of packets (mean length from bytes_len / n), capped at 64.
 using FlatKernel = void (*)(const uint8_t*, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*, uint16_t*,
-                            uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t, uint32_t*, uint32_t);
+                            uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t, uint32_t*, uint32_t, const RssParams);
 std::atomic<int> g_tail_div{1};    // flat kernel: tail tiles hold B / g_tail_div packets (1 = no guided tail)
 std::atomic<int> g_tail_tiles{4};  // ... and cover about this many tail tiles per wave slot
 
@@ -1375,7 +1486,7 @@ int flat_occupancy(FlatKernel k) {
 
 void launch_flat(FlatKernel kern, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
                  const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
-                 uint32_t flags) {
+                 uint32_t flags, const RssParams& rss) {
     const int occ = flat_occupancy(kern);
     const int knob = g_blocks_per_cu.load(std::memory_order_relaxed);
     const uint64_t bpc = static_cast<uint64_t>(occ < knob ? occ : knob);
@@ -1402,13 +1513,13 @@ void launch_flat(FlatKernel kern, hipStream_t s, const uint8_t* b, uint64_t byte
     uint32_t* heads = g_dynamic.load(std::memory_order_relaxed) ? next_heads() : nullptr;
     kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
         b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, static_cast<uint32_t>(B), static_cast<uint32_t>(B2), T1,
-        heads, flags);
+        heads, flags, rss);
 }
 
 template <int U, bool IPV4>
 void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
               const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
-              uint32_t flags) {
+              uint32_t flags, const RssParams& rss) {
     if (variant == 1) {
         csum_kernel<U, IPV4>
             <<<dim3(grid_for(n)), dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
@@ -1425,7 +1536,9 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     uint32_t* heads = nullptr;
     if (g_dynamic.load(std::memory_order_relaxed)) heads = next_heads();
     if (variant >= 10) {  // flat kernel: 10 / 11 = U 2, 12 / 13 = U 4, 14 / 15 = U 8 (odd: next chunk in flight), 16 = U 16
-        auto go = [&](auto kern) { launch_flat(kern, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags); };
+        auto go = [&](auto kern) {
+            launch_flat(kern, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
+        };
         constexpr bool F = IPV4;  // frames may fill in place; spans never do
         const bool fill = IPV4 && (flags & kFlagFillL4);
         switch (variant) {
@@ -1487,10 +1600,28 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     }
 }
 
+// Host-side Toeplitz windows: w[j] = the 32 key bits starting at bit j (MSB
+// first), bits past key_len zero — what toeplitz.hh:84-94 holds in `v` when it
+// reaches data bit j.
+RssParams make_rss(const uint8_t* key, uint32_t key_len, uint32_t mode, uint32_t* d_hash) {
+    RssParams P{};
+    P.hash = d_hash;
+    P.mode = mode;
+    auto bit = [&](uint32_t k) -> uint32_t { return k < 8u * key_len ? (key[k >> 3] >> (7u - (k & 7u))) & 1u : 0u; };
+    for (uint32_t j = 0; j < 96; ++j) {
+        uint32_t w = 0;
+        for (uint32_t t = 0; t < 32; ++t) w |= bit(j + t) << (31u - t);
+        P.w[j] = w;
+    }
+    return P;
+}
+
+const RssParams kNoRss{};
+
 template <bool IPV4>
 int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
            const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n, uint32_t max_len,
-           void* stream, uint32_t flags = 0) {
+           void* stream, uint32_t flags = 0, const RssParams& rss = kNoRss) {
     if (n == 0) return SCCSUM_OK;
     if (!d_bytes || !d_off || !d_len || (!d_out && !(flags & kFlagFillL4))) return SCCSUM_EINVAL;
     if ((reinterpret_cast<uintptr_t>(d_bytes) & 15u) || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
@@ -1513,17 +1644,21 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
     const int uc = variant == 1 ? units_class(max_len) : (forced ? forced : 2);
     switch (uc) {
         case 1:
-            launch_u<1, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+            launch_u<1, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
             break;
         case 2:
-            launch_u<2, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+            launch_u<2, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
             break;
         case 4:
-            launch_u<4, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+            launch_u<4, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
             break;
         default:
-            launch_u<8, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+            launch_u<8, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
             break;
+    }
+    if (IPV4 && rss.hash != nullptr && variant < 10) {  // RSS is fused only in the flat kernel
+        rss_kernel<<<dim3(static_cast<unsigned>((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s>>>(
+            b, bytes_len, d_off, d_len, nullptr, n, rss);
     }
     return static_cast<int>(hipGetLastError());
 }
@@ -1577,6 +1712,37 @@ int sccsum_spans(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off,
 int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
                        uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len, void* stream) {
     return sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len, stream);
+}
+
+static int rss_args_ok(const uint8_t* key, uint32_t key_len, int mode, const uint32_t* d_hash) {
+    return key && key_len >= 4 && (mode == SCCSUM_RSS_DISPATCH || mode == SCCSUM_RSS_REASSEMBLED) && d_hash &&
+           !(reinterpret_cast<uintptr_t>(d_hash) & 3u);
+}
+
+int sccsum_ipv4_rss(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
+                    const uint8_t* key, uint32_t key_len, int mode, uint32_t* d_hash, uint8_t* d_status, uint64_t n,
+                    void* stream) {
+    if (n == 0) return SCCSUM_OK;
+    if (!rss_args_ok(key, key_len, mode, d_hash) || !d_bytes || !d_off || !d_len ||
+        (reinterpret_cast<uintptr_t>(d_bytes) & 15u) || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
+        (reinterpret_cast<uintptr_t>(d_len) & 3u)) {
+        return SCCSUM_EINVAL;
+    }
+    const sccsum::RssParams P = sccsum::make_rss(key, key_len, static_cast<uint32_t>(mode), d_hash);
+    sccsum::rss_kernel<<<dim3(static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock)), dim3(sccsum::kBlock),
+                         0, static_cast<hipStream_t>(stream)>>>(static_cast<const uint8_t*>(d_bytes), bytes_len, d_off,
+                                                                d_len, d_status, n, P);
+    return static_cast<int>(hipGetLastError());
+}
+
+int sccsum_ipv4_frames_rss(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
+                           uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len, const uint8_t* key,
+                           uint32_t key_len, int rss_mode, uint32_t* d_hash, void* stream) {
+    if (n == 0) return SCCSUM_OK;
+    if (!rss_args_ok(key, key_len, rss_mode, d_hash)) return SCCSUM_EINVAL;
+    const sccsum::RssParams P = sccsum::make_rss(key, key_len, static_cast<uint32_t>(rss_mode), d_hash);
+    return sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len, stream, 0u,
+                                P);
 }
 
 uint64_t sccsum_fragments_workspace(uint64_t nfrag) { return ((2 * nfrag + 15) & ~uint64_t(15)) + nfrag + 16; }

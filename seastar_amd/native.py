@@ -58,6 +58,9 @@ _PROTOS = {
     "sccsum_fragments": (ctypes.c_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "sccsum_fragments_workspace": (_u64, [_u64]),
     "sccsum_ipv4_fill": (ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u64, _u32, _u32, _vp]),
+    "sccsum_ipv4_rss": (ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _u32, ctypes.c_int, _vp, _vp, _u64, _vp]),
+    "sccsum_ipv4_frames_rss": (ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u64, _u32, _vp, _u32, ctypes.c_int,
+                                               _vp, _vp]),
     "sccsum_set_kernel_variant": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_blocks_per_cu": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_group_units": (ctypes.c_int, [ctypes.c_int]),
@@ -76,6 +79,11 @@ _PROTOS = {
 }
 PIPE_SPANS = 0
 PIPE_IPV4 = 1
+GATHER_NONE = 0
+GATHER_HOST = 1
+GATHER_STRIDED = 2
+RSS_DISPATCH = 0
+RSS_REASSEMBLED = 1
 
 
 def header_symbols() -> list[str]:

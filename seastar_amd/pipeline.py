@@ -50,7 +50,9 @@ class HostPipeline:
         self._h = h
 
     def run(self, mode: int, buf: np.ndarray, off: np.ndarray, length: np.ndarray, seeds: np.ndarray | None = None,
-            status: bool = False, gather: bool = False, max_len: int = 0):
+            status: bool = False, gather: int = 0, max_len: int = 0):
+        """gather: 0 = copy chunks as they lie, 1 = pack on the host first,
+        2 = one 2D DMA of each slot's packet bytes (native.GATHER_*)."""
         off = np.ascontiguousarray(off, dtype=np.uint64)
         length = np.ascontiguousarray(length, dtype=np.uint32)
         n = off.size

@@ -153,3 +153,36 @@ def store_ipv4_checksums(buf: np.ndarray, off: np.ndarray, out2: np.ndarray) -> 
         proto = int(buf[o + 9])
         pos = o + 20 + (16 if proto == PROTO_TCP else 6)
         buf[pos:pos + 2] = np.frombuffer(np.uint16(out2[i, 1]).tobytes(), np.uint8)
+
+
+def rss_frames(n: int, seed: int = 0x55):
+    """A varied IPv4 batch for RSS hashing (forward_hash edge cases): UDP, TCP,
+    ICMP and other protocols; fragments (MF set / nonzero offset); IP options
+    (ihl 5-8); Ethernet-style padding (len > ip total length) and truncation;
+    frames of 0-19 bytes and just below / at the TCP and UDP header bounds;
+    packed back to back at odd offsets.  Returns (buf, off, length)."""
+    rng = _rng(seed)
+    lens = rng.choice([8, 19, 20, 27, 28, 39, 40, 44, 60, 64, 100, 576, 1500], size=n).astype(np.uint32)
+    off, total = pack(lens, seed=seed + 1, max_gap=3)
+    buf = rng.integers(0, 256, size=int(total) + 64, dtype=np.uint8)
+    protos = rng.choice([PROTO_UDP, PROTO_TCP, 1, 47], size=n, p=[0.4, 0.4, 0.1, 0.1])
+    for i in range(n):
+        o, L = int(off[i]), int(lens[i])
+        if L < 20:
+            continue
+        f = buf[o:o + L]
+        ihl = int(rng.choice([5, 5, 5, 6, 8]))
+        f[0] = 0x40 | ihl
+        ip_len = L if rng.random() < 0.7 else int(rng.integers(20, L + 40))
+        f[2], f[3] = (ip_len >> 8) & 0xFF, ip_len & 0xFF
+        frag = 0
+        r = rng.random()
+        if r < 0.15:
+            frag = 0x2000  # MF
+        elif r < 0.25:
+            frag = int(rng.integers(1, 0x2000))  # nonzero offset
+        elif r < 0.3:
+            frag = 0x4000  # DF only: still atomic
+        f[6], f[7] = (frag >> 8) & 0xFF, frag & 0xFF
+        f[9] = int(protos[i])
+    return buf, off, lens

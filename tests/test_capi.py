@@ -84,3 +84,11 @@ def test_argument_validation_without_device():
     assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, F.FILL_IP | F.FILL_L4, None) == 0
     assert lib.sccsum_ipv4_fill(None, 64, None, None, None, None, 3, 0, F.FILL_IP, None) == native.SCCSUM_EINVAL
     assert lib.sccsum_ipv4_fill(None, 64, None, None, None, None, 3, 0, F.FILL_L4, None) == native.SCCSUM_EINVAL
+
+
+def test_rss_argument_validation_without_device():
+    lib = native.load()
+    assert lib.sccsum_ipv4_rss(None, 0, None, None, None, 0, 0, None, None, 0, None) == 0  # n = 0: nothing to do
+    assert lib.sccsum_ipv4_rss(None, 0, None, None, None, 0, 0, None, None, 1, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_frames_rss(None, 0, None, None, None, None, 1, 0, None, 40, 0, None, None) \
+        == native.SCCSUM_EINVAL

@@ -5,6 +5,7 @@ Small cases compare every output with the oracle; the full-size cases
 generate -> store -> verify round trips, exact failure sets after corruption,
 and oracle comparison on a random sample.
 """
+import ctypes
 import json
 import os
 
@@ -261,7 +262,7 @@ def test_zipf_large_frames(dev):
     assert np.array_equal(got, want) and np.array_equal(st, want_st)
 
 
-@pytest.mark.parametrize("gather", [False, True])
+@pytest.mark.parametrize("gather", [0, 1, 2], ids=["as_is", "host_gather", "strided_dma"])
 def test_host_pipeline_mbuf_pool(dev, gather, kernel_variant):
     """cfg 5 path: frames in an mbuf-shaped pinned pool, chunked through the
     GPU with async copies; small chunks force many stage recycles."""
@@ -281,6 +282,31 @@ def test_host_pipeline_mbuf_pool(dev, gather, kernel_variant):
     got2 = pl.run(native.PIPE_SPANS, pool, poff, plen, seeds=seeds, gather=gather)
     assert np.array_equal(got2, oracle.batch_spans(pool, poff, plen, seeds))
     pl.close()
+
+
+def test_host_pipeline_strided_irregular(dev):
+    """gather = 2 on layouts that are only partly slot-shaped: a pitch break
+    mid-batch, a packet longer than the pitch, a single-packet tail chunk and
+    chunk_bytes that cut rows — every chunk either rows or as-is, all exact."""
+    from seastar_amd import pipeline
+
+    rng = np.random.default_rng(40)
+    n = 700
+    lens = rng.integers(20, 600, size=n).astype(np.uint32)
+    lens[350] = 900  # longer than the 640-B pitch: that chunk falls back
+    off = np.arange(n, dtype=np.uint64) * 640 + 64
+    off[500:] += 3  # pitch break (and odd slot starts from here on)
+    total = int(off[-1]) + 1024
+    pool = pipeline.pinned_empty(total)
+    pool[:] = rng.integers(0, 256, size=total, dtype=np.uint8)
+    seeds = rng.integers(0, 65536, n).astype(np.uint32)
+    want = oracle.batch_spans(pool, off, lens, seeds)
+    for chunk_bytes, chunk_packets in ((1 << 20, 256), (40 * 1024, 256), (1 << 20, 699)):
+        pl = pipeline.HostPipeline(0, chunk_bytes=chunk_bytes, chunk_packets=chunk_packets, depth=2)
+        got, st = pl.run(native.PIPE_SPANS, pool, off, lens, seeds=seeds, status=True,
+                         gather=native.GATHER_STRIDED)
+        pl.close()
+        assert np.array_equal(got, want), (chunk_bytes, chunk_packets)
 
 
 def _frag_batch(rng, n, sizes_fn, scatter=True):
@@ -443,3 +469,48 @@ def test_ipv4_fill_full_scale_udp1500(dev):
     st = torch.empty(b.n, dtype=torch.uint8, device=dev)
     batch.ipv4_frames(b, status=st)
     assert int((st == 3).sum()) == b.n
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["dispatch", "reassembled"])
+def test_rss_standalone_and_fused(dev, mode, kernel_variant):
+    """Toeplitz RSS (toeplitz.hh:78-98 over the stack's forward_hash) per frame:
+    sccsum_ipv4_rss and the fused sccsum_ipv4_frames_rss vs the oracle, on
+    fragments, options, ICMP/other protocols, padded / truncated / short frames
+    at odd offsets; the fused pass leaves the checksums and status unchanged."""
+    if kernel_variant not in (1, 6, 10, 15, 16):
+        pytest.skip("RSS exercised with the simple, batch and flat families")
+    rss = json.load(open(os.path.join(GOLDEN, "rss.json")))
+    buf, off, lens = synth.rss_frames(5000, seed=21)
+    # the last frame ends exactly at a 16-aligned buffer end (the padded-read guard)
+    end = (int(off[-1] + lens[-1]) + 15) & ~15
+    lens[-1] = end - int(off[-1])
+    buf = buf[:end]
+    b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+    ref2, ref_st = _frames(dev, buf, off, lens)
+    for key in (batch.RSS_KEY_40, bytes.fromhex(rss["cases"][0]["key"]), bytes(range(7, 15))):
+        want, want_st = oracle.batch_ipv4_rss(buf, off, lens, key=key, mode=mode)
+        st = torch.empty(b.n, dtype=torch.uint8, device=dev)
+        got = batch.ipv4_rss(b, key=key, mode=mode, status=st)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint32), want)
+        assert np.array_equal(st.cpu().numpy() & 4, want_st & 4)
+        fst = torch.empty(b.n, dtype=torch.uint8, device=dev)
+        out2, h = batch.ipv4_frames_rss(b, key=key, mode=mode, status=fst)
+        torch.cuda.synchronize()
+        assert np.array_equal(h.cpu().numpy().view(np.uint32), want)
+        assert np.array_equal(batch.as_u16(out2), ref2) and np.array_equal(fst.cpu().numpy(), ref_st)
+
+
+def test_rss_errors(dev):
+    lib = native.load()
+    k = (ctypes.c_uint8 * 3)(1, 2, 3)
+    b = batch.PacketBatch.from_host(np.zeros(64, np.uint8), np.zeros(1, np.uint64), np.full(1, 40, np.uint32),
+                                    device=dev)
+    h = torch.empty(1, dtype=torch.int32, device=dev)
+    args = (batch.ctypes_ptr(b.data), b.bytes_len, batch.ctypes_ptr(b.off), batch.ctypes_ptr(b.length))
+    assert lib.sccsum_ipv4_rss(*args, ctypes.addressof(k), 3, 0, batch.ctypes_ptr(h), None, 1, None) == native.SCCSUM_EINVAL
+    k5 = (ctypes.c_uint8 * 5)(1, 2, 3, 4, 5)
+    assert lib.sccsum_ipv4_rss(*args, ctypes.addressof(k5), 5, 2, batch.ctypes_ptr(h), None, 1, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_rss(*args, ctypes.addressof(k5), 5, 0, None, None, 1, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_rss(*args, ctypes.addressof(k5), 5, 0, batch.ctypes_ptr(h), None, 1, None) == native.SCCSUM_OK
+    torch.cuda.synchronize()

@@ -175,3 +175,58 @@ def test_batch_drivers_match_single_calls(nthreads):
     assert np.all(st & 0x4 == 0)
     spans = oracle.batch_spans(buf, off, lens, nthreads=nthreads)
     assert spans[5] == closed_form(buf[int(off[5]):int(off[5]) + 1500].tobytes())
+
+
+# ---- RSS (Toeplitz) --------------------------------------------------------
+
+RSS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "rss.json")))
+
+
+def test_toeplitz_matches_reference_build():
+    """oracle_toeplitz vs the reference's own toeplitz_hash (rss.json, built
+    from include/seastar/net/toeplitz.hh; MS RSS suite rows included)."""
+    for c in RSS["cases"]:
+        data = bytes.fromhex(c["data"]) if c["data"] != "-" else b""
+        assert oracle.toeplitz(bytes.fromhex(c["key"]), data) == c["hash"], c
+
+
+def _fwd_hash(frame: bytes, mode: int) -> bytes | None:
+    """forward_hash bytes, restated from the reference code in Python:
+    ip.cc:77-92 + udp.cc:153-161 + tcp.hh:852-862 (mode 0), ip.cc:186-197 (mode 1)."""
+    if len(frame) < 20:
+        return None
+    data = frame[12:20]
+    proto = frame[9]
+    need = {6: 20, 17: 8}.get(proto, 0)
+    if mode == 0:
+        frag = (frame[6] << 8) | frame[7]
+        if need and not (frag & 0x2000) and not (frag & 0x1FFF) and len(frame) >= 20 + need:
+            data += frame[20:24]
+    else:
+        l4_off = 4 * (frame[0] & 0xF)
+        ip_len = (frame[2] << 8) | frame[3]
+        l4_end = min(ip_len, len(frame))
+        if l4_off > l4_end:
+            return None
+        if need and l4_end - l4_off >= need:
+            data += frame[l4_off:l4_off + 4]
+    return data
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_rss_forward_hash_construction(mode):
+    from seastar_amd import synth
+
+    buf, off, lens = synth.rss_frames(3000, seed=9)
+    for key in (oracle.RSS_KEY_40, bytes.fromhex(RSS["cases"][0]["key"]), bytes(range(1, 9))):
+        h, st = oracle.batch_ipv4_rss(buf, off, lens, key=key, mode=mode)
+        for i in range(off.size):
+            fr = bytes(buf[int(off[i]):int(off[i]) + int(lens[i])])
+            d = _fwd_hash(fr, mode)
+            if d is None:
+                assert st[i] == 4 and h[i] == 0
+            else:
+                assert st[i] == 0 and h[i] == oracle.toeplitz(key, d), (i, len(fr))
+    # the batch really exercises the branches
+    kinds = {len(_fwd_hash(bytes(buf[int(o):int(o) + int(L)]), mode) or b"") for o, L in zip(off, lens)}
+    assert {0, 8, 12} <= kinds
