@@ -56,7 +56,11 @@ def parse():
     return ap.parse_args()
 
 
-BACKEND = os.environ.get("SCCSUM_DIST_BACKEND", "nccl")  # gloo: rehearse N ranks on fewer GPUs
+# The path exchanges no data between GPUs (independent shards):
+# the process group only carries the timing barrier and one max-over-ranks
+# reduction, so it runs on gloo (host TCP) and RCCL is never initialised.
+# SCCSUM_DIST_BACKEND=nccl puts that control traffic on RCCL instead.
+BACKEND = os.environ.get("SCCSUM_DIST_BACKEND", "gloo")
 
 
 def dist_setup():
@@ -160,24 +164,29 @@ def pmc_traffic(path: str | None, kernel_substr: str):
     return None, None
 
 
-def timed(step, steps, warmup, world, stream):
+def timed(step, steps, warmup, world, stream, launches_per_step=1):
     """Warm up, then time `steps` calls bracketed by barrier + sync; returns
-    (max-over-ranks wall seconds, mean seconds per launch from HIP events)."""
+    (max-over-ranks wall seconds, mean seconds per launch).  The launch mean
+    comes from ONE pair of HIP events around the timed launches on their
+    stream: an event between every two launches leaves the GPU idle ~5 us at
+    each (a timestamp packet), which the old per-launch events added to the
+    wall time (profiles/r01_kernel_stats_bench.csv gap analysis)."""
     for k in range(warmup):
         step(k)
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k, e in enumerate(evs):
-        e[0].record(stream)
+    e0.record(stream)
+    for k in range(steps):
         step(k)
-        e[1].record(stream)
+    e1.record(stream)
     torch.cuda.synchronize()
+    t1 = time.perf_counter()  # this rank's end, before the closing barrier's own latency
     barrier(world)
-    wall = max_over_ranks(time.perf_counter() - t0, world)
-    return wall, float(np.mean([a.elapsed_time(b) for a, b in evs])) / 1e3
+    wall = max_over_ranks(t1 - t0, world)
+    return wall, e0.elapsed_time(e1) / 1e3 / (steps * launches_per_step)
 
 
 def line(metric, value, unit, args, world, wall, dtype, config, roofline=None, cpu=None, extra=None):
@@ -355,16 +364,10 @@ def main():
 
     stream = torch.cuda.current_stream()
 
-    def step(k, ev=None):
+    def step(k):
         r = k % R
-        if ev is not None:
-            ev[0].record(stream)
         batch.ipv4_frames(txs[r], out2=out_tx, stream=stream)
-        if ev is not None:
-            ev[1].record(stream)
         batch.ipv4_frames(rxs[r], out2=out_rx, status=sts[r], stream=stream)
-        if ev is not None:
-            ev[2].record(stream)
 
     for k in range(max(args.warmup, R)):
         step(k)
@@ -374,22 +377,21 @@ def main():
         n_fail = int(((st_rx & 2) == 0).sum())
         assert n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    # timed region: barrier + sync on both sides, one HIP event pair around the
+    # launches on their stream (see timed())
+    e_start, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    e_start.record(stream)
     for k in range(args.steps):
-        step(k, evs[k])
+        step(k)
+    e_end.record(stream)
     torch.cuda.synchronize()
+    wall = time.perf_counter() - t0  # this rank's end, before the closing barrier's own latency
     barrier(world)
-    wall = time.perf_counter() - t0
     wall_max = max_over_ranks(wall, world)
-
-    launch_ms = []
-    for e in evs:
-        launch_ms.append(e[0].elapsed_time(e[1]))
-        launch_ms.append(e[1].elapsed_time(e[2]))
-    avg_launch_s = float(np.mean(launch_ms)) / 1e3
+    avg_launch_s = e_start.elapsed_time(e_end) / 1e3 / (2 * args.steps)
 
     bytes_per_step = 2 * n * FRAME  # per rank
     value = world * bytes_per_step * args.steps / wall_max / 2**30

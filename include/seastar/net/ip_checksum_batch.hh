@@ -12,6 +12,9 @@
 //       udp.cc:184-195, tcp.hh:1656-1694, tcp.hh:1004-1016
 //   ip.cc:121-127 (IPv4 verify) + tcp.hh:876-883 (TCP verify) ipv4_frames(batch, ...)
 //   ip.cc:271-277 (IPv4 generate) + udp/tcp generate          ipv4_frames(batch, ...) on zeroed fields
+//   the same, stored into the frames (wire-ready tx)          ipv4_fill(batch, SCCSUM_FILL_IP | SCCSUM_FILL_L4, ...)
+//   checksummer::sum(const packet&)  ip_checksum.cc:64-68     (C-ABI sccsum_fragments)
+//   toeplitz_hash(rss_key(), forward_hash)  net.cc:330-341    ipv4_rss(batch, key, ...) / ipv4_frames_rss(...)
 //
 // Results are network-order uint16 values, exactly what checksummer::get()
 // returns; a verify passes when the value is 0.  Errors throw
@@ -24,6 +27,10 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+
+#if __cplusplus >= 202002L
+#include <span>
+#endif
 
 namespace seastar {
 
@@ -81,6 +88,41 @@ public:
         check(sccsum_ipv4_frames(b.bytes, b.bytes_len, b.off, b.len, d_out2, d_status, b.n, b.max_len, stream),
               "sccsum_ipv4_frames");
     }
+
+    // Generate IPv4 header and/or TCP/UDP checksums and store them into the
+    // frames (mode: SCCSUM_FILL_*; d_out2 / d_status may be null).
+    void ipv4_fill(const device_packet_batch& b, uint32_t mode, uint16_t* d_out2, uint8_t* d_status,
+                   void* stream) const {
+        check(sccsum_ipv4_fill(const_cast<void*>(b.bytes), b.bytes_len, b.off, b.len, d_out2, d_status, b.n,
+                               b.max_len, mode, stream),
+              "sccsum_ipv4_fill");
+    }
+
+    // RSS: d_hash[i] = toeplitz_hash(key, forward_hash of frame i) (toeplitz.hh:78-98, net.cc:330-341);
+    // mode SCCSUM_RSS_DISPATCH or SCCSUM_RSS_REASSEMBLED.  key is host memory
+    // (the reference's rss_key_type: 40 or 52 bytes, at least 4).
+    void ipv4_rss(const device_packet_batch& b, const uint8_t* key, size_t key_len, int mode, uint32_t* d_hash,
+                  uint8_t* d_status, void* stream) const {
+        check(sccsum_ipv4_rss(b.bytes, b.bytes_len, b.off, b.len, key, static_cast<uint32_t>(key_len), mode, d_hash,
+                              d_status, b.n, stream),
+              "sccsum_ipv4_rss");
+    }
+
+    // ipv4_frames and ipv4_rss in one pass over the bytes.
+    void ipv4_frames_rss(const device_packet_batch& b, const uint8_t* key, size_t key_len, int mode,
+                         uint16_t* d_out2, uint8_t* d_status, uint32_t* d_hash, void* stream) const {
+        check(sccsum_ipv4_frames_rss(b.bytes, b.bytes_len, b.off, b.len, d_out2, d_status, b.n, b.max_len, key,
+                                     static_cast<uint32_t>(key_len), mode, d_hash, stream),
+              "sccsum_ipv4_frames_rss");
+    }
+
+#if __cplusplus >= 202002L
+    // The same with the reference's key type (rss_key_type = std::span<const uint8_t>, toeplitz.hh:49).
+    void ipv4_rss(const device_packet_batch& b, std::span<const uint8_t> key, int mode, uint32_t* d_hash,
+                  uint8_t* d_status, void* stream) const {
+        ipv4_rss(b, key.data(), key.size(), mode, d_hash, d_status, stream);
+    }
+#endif
 
     void sync(void* stream) const { check(sccsum_sync(stream), "sccsum_sync"); }
 };

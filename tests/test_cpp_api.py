@@ -38,6 +38,23 @@ def test_batch_header_compiles(tmp_path):
     assert os.path.exists(exe)
 
 
+def test_batch_header_compiles_cxx20_rss_span(tmp_path):
+    """The rss_key_type (std::span) overload, as the reference's callers hold the key."""
+    src = tmp_path / "r.cc"
+    src.write_text('#include <seastar/net/ip_checksum_batch.hh>\n'
+                   'static const uint8_t key[40] = {0xd1, 0x81};\n'
+                   'void f(const seastar::net::batch_checksummer& e, const seastar::net::device_packet_batch& b,\n'
+                   '       uint32_t* h) { e.ipv4_rss(b, std::span<const uint8_t>(key), SCCSUM_RSS_DISPATCH, h, nullptr,\n'
+                   '                                nullptr); }\n'
+                   'int main() { return 0; }\n')
+    exe = str(tmp_path / "r")
+    cmd = ["g++", "-std=c++20", "-O2", "-Wall", "-Wextra", "-I", os.path.join(REPO, "include"), str(src), "-o", exe,
+           "-L", os.path.join(REPO, "seastar_amd", "lib"), "-lsccsum",
+           "-Wl,-rpath," + os.path.join(REPO, "seastar_amd", "lib")]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
 @pytest.mark.gpu
 def test_batch_cpp_program_on_gpu(tmp_path):
     """Native host program: hipMalloc'd batch -> batch_checksummer ->

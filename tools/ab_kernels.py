@@ -25,11 +25,21 @@ import torch  # noqa: E402
 from seastar_amd import batch, devsynth, native, synth  # noqa: E402
 
 
+CASES: set[str] = set()
+
+
 def cases(dev):
     n = 1 << 20
     tx = devsynth.udp_frames(n, 1500, seed=1, device=dev)
     yield "udp1500_frames", tx, "frames", n * (1500 + 12 + 4)
     yield "udp1500_spans", tx, "spans", n * (1500 + 12 + 2)
+    yield "udp1500_frames_rss", tx, "frames_rss", n * (1500 + 12 + 4 + 4)
+    if "udp1500x2_frames" in CASES:  # one launch over 2 M frames: launch ramp/tail = 2 T(1 M) - T(2 M)
+        del tx
+        torch.cuda.empty_cache()
+        tx2 = devsynth.udp_frames(2 * n, 1500, seed=2, device=dev)
+        yield "udp1500x2_frames", tx2, "frames", 2 * n * (1500 + 12 + 4)
+        del tx2
     lens = synth.zipf_lengths(200_000, seed=3)
     off, total = synth.pack(lens, seed=4, max_gap=3)
     buf = np.random.default_rng(5).integers(0, 256, size=total, dtype=np.uint8)
@@ -53,8 +63,10 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn[:tile_bytes[:tail_div[:tail_per_slot]]]]]]]")
     ap.add_argument("--rotate", type=int, default=4, help="distinct copies of each batch, launched in turn")
-    ap.add_argument("--cases", default="udp1500_frames,udp1500_spans,zipf_spans,cfg3_zipf_frames,tcp64k_spans")
+    ap.add_argument("--cases", default="udp1500_frames,udp1500_spans,udp1500_frames_rss,zipf_spans,cfg3_zipf_frames,"
+                                       "tcp64k_spans")
     args = ap.parse_args()
+    CASES.update(args.cases.split(","))
     variants = args.variants.split(",")
     lib = native.load()
     native.check(lib.sccsum_init(0), "init")
@@ -82,6 +94,8 @@ def main():
         def run(bb):
             if mode == "frames":
                 return batch.ipv4_frames(bb)
+            if mode == "frames_rss":
+                return batch.ipv4_frames_rss(bb)[1]
             return batch.spans(bb)
 
         def run_next():
