@@ -63,6 +63,7 @@ extern "C" {
 #define SCCSUM_OK 0
 #define SCCSUM_EINVAL (-1)   /* bad argument (null pointer, misalignment) */
 #define SCCSUM_ENODEV (-2)   /* no HIP device / device index out of range */
+#define SCCSUM_EBUSY  (-3)   /* burst queue: every batch slot is in flight; poll and retry */
 
 /* per-packet status bits (d_status) */
 #define SCCSUM_ST_OK        0x01u /* spans: result == 0; frames: IPv4 header verifies */
@@ -283,6 +284,58 @@ int sccsum_pipeline_run(sccsum_pipeline* p, int mode, int gather, const void* ho
                         uint64_t n, uint32_t max_len, uint16_t* host_out, uint8_t* host_status);
 
 int sccsum_pipeline_destroy(sccsum_pipeline* p);
+
+/* ---- Burst queue: the batching hook at the qp boundary ----------------------
+ * The native stack checksums packet by packet on the shard's reactor thread;
+ * qp::poll_tx refills up to 128 packets per poll (src/net/net.cc:81-105) and
+ * DPDK rx hands over bursts of 32 (src/net/dpdk.cc:2190-2204).  A burst queue
+ * accumulates such packets from HOST memory into GPU batches and completes
+ * them asynchronously.  It is shaped like a reactor::poller (net.cc:109):
+ * every call is non-blocking except sccsum_burst_drain, and sccsum_burst_poll
+ * reports whether it did work.  One queue per shard / thread; not thread-safe.
+ *
+ * mode: SCCSUM_PIPE_SPANS (each packet's sum seeded with its seed, results
+ * [count]) or SCCSUM_PIPE_IPV4 (frames: IPv4 header + L4 checksums, results
+ * [2*count]).  A batch launches when it holds batch_packets packets or no room
+ * for the next one, or on the first poll after max_delay_ns.  depth = batch
+ * slots (staging + device buffers each). */
+typedef struct sccsum_burst sccsum_burst;
+
+/* Completion, called from sccsum_burst_poll / _drain on the caller's thread:
+ * the packets with tickets first_ticket .. first_ticket + count - 1, in submit
+ * order; results / status point into the queue's pinned memory, valid until
+ * the callback returns. */
+typedef void (*sccsum_burst_done_fn)(void* user, uint64_t first_ticket, uint32_t count, const uint16_t* results,
+                                     const uint8_t* status);
+
+int sccsum_burst_create(int device, int mode, uint64_t batch_bytes, uint32_t batch_packets, uint64_t max_delay_ns,
+                        int depth, sccsum_burst_done_fn fn, void* user, sccsum_burst** out);
+
+/* One piece of a packet, in the layout of seastar::net::fragment {char* base;
+ * size_t size;} (include/seastar/net/packet.hh:43-46): a packet's
+ * fragment_array() / nr_frags() (packet.hh:245-247) pass as they are. */
+typedef struct sccsum_fragment {
+    const void* base;
+    size_t size;
+} sccsum_fragment;
+
+/* Stage one packet given as its fragments (checksummer::sum(const packet&)
+ * over the fragments in order, ip_checksum.cc:64-68): they are copied into
+ * pinned staging now, so the caller may reuse them on return.  *ticket (may be
+ * NULL) identifies the packet in the completion.  seed: SCCSUM_PIPE_SPANS only.
+ * SCCSUM_EBUSY: every slot is in flight (poll, then retry); SCCSUM_EINVAL: a
+ * packet longer than a batch. */
+int sccsum_burst_submit(sccsum_burst* b, const sccsum_fragment* frags, uint32_t nfrag, uint32_t seed,
+                        uint64_t* ticket);
+
+/* Reactor poller: launch the open batch if full or aged; deliver every
+ * finished batch.  *did_work (may be NULL) = 1 when it launched or delivered. */
+int sccsum_burst_poll(sccsum_burst* b, int* did_work);
+
+/* Launch what is staged, wait for every batch in flight, deliver them all. */
+int sccsum_burst_drain(sccsum_burst* b);
+
+int sccsum_burst_destroy(sccsum_burst* b);
 
 /* Pinned (page-locked) host memory for packet pools. */
 int sccsum_host_alloc(void** p, uint64_t bytes);

@@ -15,6 +15,8 @@
 //   the same, stored into the frames (wire-ready tx)          ipv4_fill(batch, SCCSUM_FILL_IP | SCCSUM_FILL_L4, ...)
 //   checksummer::sum(const packet&)  ip_checksum.cc:64-68     (C-ABI sccsum_fragments)
 //   toeplitz_hash(rss_key(), forward_hash)  net.cc:330-341    ipv4_rss(batch, key, ...) / ipv4_frames_rss(...)
+//   per packet as qp::poll_tx / DPDK rx hand them over         burst_queue (host packets, async completion)
+//       net.cc:81-105, dpdk.cc:2190-2204
 //
 // Results are network-order uint16 values, exactly what checksummer::get()
 // returns; a verify passes when the value is 0.  Errors throw
@@ -27,6 +29,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <utility>
 
 #if __cplusplus >= 202002L
 #include <span>
@@ -125,6 +128,56 @@ public:
 #endif
 
     void sync(void* stream) const { check(sccsum_sync(stream), "sccsum_sync"); }
+};
+
+// Burst queue (<sccsum.h> sccsum_burst_*): packets from HOST memory, handed
+// over one at a time as qp::poll_tx and the DPDK rx loop do, batched for the
+// GPU and completed through `done(first_ticket, count, results, status)` on
+// the polling thread, in submit order.  poll() has pollfn::poll's contract
+// (core/internal/poll.hh:26-29: true = did work), so it registers as a poller
+// the way qp registers poll_tx (net.cc:109):
+//   burst_queue q(gpu, SCCSUM_PIPE_IPV4, 16 << 20, 8192, 50'000, 4, on_done);
+//   auto p = reactor::poller::simple([&] { return q.poll(); });
+//   q.submit(reinterpret_cast<const sccsum_fragment*>(pkt.fragment_array()), pkt.nr_frags());
+// The queue hands `this` to the C-ABI, so it neither copies nor moves.
+template <typename Done>
+class burst_queue {
+    sccsum_burst* _q = nullptr;
+    Done _done;
+
+    static void complete(void* self, uint64_t first, uint32_t count, const uint16_t* results, const uint8_t* status) {
+        static_cast<burst_queue*>(self)->_done(first, count, results, status);
+    }
+    static void check(int rc, const char* what) {
+        if (rc != SCCSUM_OK) {
+            throw std::runtime_error(std::string(what) + ": " + sccsum_strerror(rc));
+        }
+    }
+
+public:
+    burst_queue(int device, int mode, uint64_t batch_bytes, uint32_t batch_packets, uint64_t max_delay_ns, int depth,
+                Done done)
+        : _done(std::move(done)) {
+        check(sccsum_burst_create(device, mode, batch_bytes, batch_packets, max_delay_ns, depth, &complete, this, &_q),
+              "sccsum_burst_create");
+    }
+    burst_queue(const burst_queue&) = delete;
+    burst_queue& operator=(const burst_queue&) = delete;
+    ~burst_queue() { sccsum_burst_destroy(_q); }
+
+    // false: every batch slot is in flight (poll, then submit again)
+    bool submit(const sccsum_fragment* frags, uint32_t nfrag, uint32_t seed = 0, uint64_t* ticket = nullptr) {
+        const int rc = sccsum_burst_submit(_q, frags, nfrag, seed, ticket);
+        if (rc == SCCSUM_EBUSY) return false;
+        check(rc, "sccsum_burst_submit");
+        return true;
+    }
+    bool poll() {
+        int did = 0;
+        check(sccsum_burst_poll(_q, &did), "sccsum_burst_poll");
+        return did != 0;
+    }
+    void drain() { check(sccsum_burst_drain(_q), "sccsum_burst_drain"); }
 };
 
 }  // namespace net

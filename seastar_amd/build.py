@@ -10,6 +10,7 @@ SOURCES = [
     os.path.join(PKG_DIR, "csrc", "sccsum.hip"),
     os.path.join(PKG_DIR, "csrc", "checksummer.cc"),
     os.path.join(PKG_DIR, "csrc", "pipeline.cc"),
+    os.path.join(PKG_DIR, "csrc", "burst.cc"),
 ]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 

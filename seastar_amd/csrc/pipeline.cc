@@ -178,7 +178,12 @@ int run_chunks(sccsum_pipeline* p, int mode, int gather, const void* host_bytes,
             if (rows) {
                 const bool on_pitch = j == i || o == host_off[j - 1] + P;
                 const uint64_t nW = std::max(W, L);
-                if (j > i && (!on_pitch || L > P || (j - i + 1) * ((nW + 15) & ~uint64_t(15)) > p->chunk_bytes)) break;
+                // every row is read W bytes wide: earlier rows stay inside their slot (W <= P),
+                // the last row must stay inside the caller's buffer
+                if (j > i && (!on_pitch || L > P || o + nW > host_len ||
+                              (j - i + 1) * ((nW + 15) & ~uint64_t(15)) > p->chunk_bytes)) {
+                    break;
+                }
                 if (j == i && L > P) rows = false;  // not slot-shaped after all: copy as it lies
                 W = nW;
             }

@@ -595,6 +595,13 @@ __global__ __launch_bounds__(kBlock, FILL ? SCCSUM_FILL_MIN_WAVES : SCCSUM_BATCH
                 if (m1) body(k + 1, PB);
             }
         }
+        if (IPV4 && huge && mine && !range_bad) {  // not streamed (phase D redoes its sum): head units from the frame
+            constexpr uint32_t kHeadH = FILL ? kStashHead : 3u;
+            uint8_t* hrow = stash + lane * kStashStride;
+            const auto* hu = reinterpret_cast<const u32x4*>(a0);
+#pragma unroll
+            for (uint32_t j = 0; j < kHeadH; ++j) *reinterpret_cast<u32x4*>(hrow + 16u * j) = hu[j];
+        }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): stash writes visible to this wave's reads
         __builtin_amdgcn_wave_barrier();
 
@@ -1116,6 +1123,11 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
             }
         }
         const uint32_t res = pend - pst;  // sum of the packet's units, mod 2^32
+        if (IPV4 && huge && mine && !range_bad) {  // not streamed (phase D redoes its sum): head units from the frame
+            const auto* hu = reinterpret_cast<const u32x4*>(a0);
+#pragma unroll
+            for (int j = 0; j < kHead; ++j) hs[j] = hu[j];
+        }
 
         // ---- C: lane i finishes packet i (as csum_batch_kernel, stash in registers)
         const int rs0 = static_cast<int>(head) + (IPV4 ? 20 : 0);
@@ -1440,10 +1452,8 @@ int units_class(uint32_t max_len) {
     return 8;
 }
 
-// Kernel variant: 0 = default (batch kernel: 6 when max_len <= 2 KiB, else 8;
-// measured: the hybrid policy pays for packed MTU-size frames, shared passes
-// for short packets + all-nontemporal for mixed and long ones; cross-packet
-// prefetch (3, 5, 7) only adds issue work),
+// Kernel variant: 0 = default (the flat kernel: 16 for batches of >= 512 Ki
+// packets and >= 256 MiB, else 15), 10-16 = the flat kernel's forms (launch_u),
 // 1 = simple one-packet-per-wave loop (independent second implementation),
 // 2 = batch kernel, 3 = batch kernel with the next packet in flight (both
 // with nontemporal loads), 4 / 5 = 2 / 3 with default-policy loads,
@@ -1525,16 +1535,6 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
             <<<dim3(grid_for(n)), dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
         return;
     }
-    // batch kernel: tiles of B <= 64 packets, enough tiles to fill every wave slot
-    const uint64_t slots = static_cast<uint64_t>(cu_count()) * g_blocks_per_cu.load() * kWavesPerBlock;
-    const uint64_t bmax = static_cast<uint64_t>(g_tile_packets.load(std::memory_order_relaxed));
-    uint64_t B = (n + slots - 1) / slots;
-    B = B < 1 ? 1 : (B > bmax ? bmax : B);
-    // grid: multiple of 16 workgroups so the wave count divides into kGroups
-    const dim3 grid((grid_for((n + B - 1) / B) + 15u) & ~15u);
-    const uint32_t b32 = static_cast<uint32_t>(B);
-    uint32_t* heads = nullptr;
-    if (g_dynamic.load(std::memory_order_relaxed)) heads = next_heads();
     if (variant >= 10) {  // flat kernel: 10 / 11 = U 2, 12 / 13 = U 4, 14 / 15 = U 8 (odd: next chunk in flight), 16 = U 16
         auto go = [&](auto kern) {
             launch_flat(kern, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
@@ -1552,6 +1552,16 @@ void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
         }
         return;
     }
+    // batch kernel: tiles of B <= 64 packets, enough tiles to fill every wave slot
+    const uint64_t slots = static_cast<uint64_t>(cu_count()) * g_blocks_per_cu.load() * kWavesPerBlock;
+    const uint64_t bmax = static_cast<uint64_t>(g_tile_packets.load(std::memory_order_relaxed));
+    uint64_t B = (n + slots - 1) / slots;
+    B = B < 1 ? 1 : (B > bmax ? bmax : B);
+    // grid: multiple of 16 workgroups so the wave count divides into kGroups
+    const dim3 grid((grid_for((n + B - 1) / B) + 15u) & ~15u);
+    const uint32_t b32 = static_cast<uint32_t>(B);
+    uint32_t* heads = nullptr;
+    if (g_dynamic.load(std::memory_order_relaxed)) heads = next_heads();
     if constexpr (IPV4) {
         if (flags & kFlagFillL4) {
             if (variant == 8 || variant == 9) {
@@ -1674,6 +1684,7 @@ const char* sccsum_strerror(int err) {
     if (err == SCCSUM_OK) return "success";
     if (err == SCCSUM_EINVAL) return "invalid argument";
     if (err == SCCSUM_ENODEV) return "no such HIP device";
+    if (err == SCCSUM_EBUSY) return "every batch slot is in flight";
     if (err > 0) return hipGetErrorString(static_cast<hipError_t>(err));
     return "unknown sccsum error";
 }

@@ -19,6 +19,7 @@ HEADER_PATH = os.path.join(REPO_DIR, "include", "sccsum.h")
 SCCSUM_OK = 0
 SCCSUM_EINVAL = -1
 SCCSUM_ENODEV = -2
+SCCSUM_EBUSY = -3
 ST_OK = 0x01
 ST_L4_OK = 0x02
 ST_MALFORMED = 0x04
@@ -74,6 +75,12 @@ _PROTOS = {
     "sccsum_pipeline_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, _u64, _vp, _vp, _vp, _u64, _u32,
                                            _vp, _vp]),
     "sccsum_pipeline_destroy": (ctypes.c_int, [_vp]),
+    "sccsum_burst_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _u64, _u32, _u64, ctypes.c_int, _vp, _vp,
+                                           ctypes.POINTER(_vp)]),
+    "sccsum_burst_submit": (ctypes.c_int, [_vp, _vp, _u32, _u32, ctypes.POINTER(_u64)]),
+    "sccsum_burst_poll": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
+    "sccsum_burst_drain": (ctypes.c_int, [_vp]),
+    "sccsum_burst_destroy": (ctypes.c_int, [_vp]),
     "sccsum_host_alloc": (ctypes.c_int, [ctypes.POINTER(_vp), _u64]),
     "sccsum_host_free": (ctypes.c_int, [_vp]),
 }
@@ -84,6 +91,11 @@ GATHER_HOST = 1
 GATHER_STRIDED = 2
 RSS_DISPATCH = 0
 RSS_REASSEMBLED = 1
+
+
+class Fragment(ctypes.Structure):
+    """sccsum_fragment: the layout of seastar::net::fragment (packet.hh:43-46)."""
+    _fields_ = [("base", ctypes.c_void_p), ("size", ctypes.c_size_t)]
 
 
 def header_symbols() -> list[str]:

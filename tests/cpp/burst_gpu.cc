@@ -1,0 +1,120 @@
+// Native host program over the burst queue (seastar::net::burst_queue over
+// <sccsum.h> sccsum_burst_*): IPv4/UDP frames sit in mbuf-shaped host slots
+// (2304 B, data at +256, dpdk.cc:139-156) and are handed over one at a time,
+// as the DPDK rx loop delivers them (bursts of 32, dpdk.cc:2190-2204, after
+// which the reactor polls); every 7th frame arrives as two fragments split at
+// an odd offset (the `odd` carry of checksummer::sum(const packet&),
+// ip_checksum.cc:64-68).  Every result is checked against the per-packet API;
+// the hook's throughput is printed.  Usage: burst_gpu [frames] [depth]
+#include <seastar/net/ip_checksum.hh>
+#include <seastar/net/ip_checksum_batch.hh>
+
+#include <arpa/inet.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+using namespace seastar::net;
+
+int main(int argc, char** argv) {
+    const uint64_t n = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 50000;
+    const int depth = argc > 2 ? std::atoi(argv[2]) : 4;
+    constexpr uint32_t kSlot = 2304, kData = 256;
+    const uint32_t pool_n = static_cast<uint32_t>(n < 65536 ? n : 65536);  // slots, reused round robin
+    std::mt19937 rng(11);
+    std::vector<uint8_t> pool(size_t(pool_n) * kSlot);
+    std::vector<uint32_t> len(pool_n);
+    std::vector<uint16_t> want(2 * size_t(pool_n));
+    for (uint32_t i = 0; i < pool_n; ++i) {
+        const uint32_t L = 28 + rng() % 1473;  // 20 B IPv4 + 8 B UDP + payload, up to 1500
+        uint8_t* f = pool.data() + size_t(i) * kSlot + kData;
+        for (uint32_t k = 0; k < L; ++k) f[k] = uint8_t(rng());
+        const uint32_t src = rng(), dst = rng();
+        f[0] = 0x45;
+        f[1] = 0;
+        uint16_t be = htons(uint16_t(L));
+        std::memcpy(f + 2, &be, 2);
+        std::memset(f + 4, 0, 4);
+        f[8] = 64;
+        f[9] = 17;
+        f[10] = f[11] = 0;
+        const uint32_t s = htonl(src), d = htonl(dst);
+        std::memcpy(f + 12, &s, 4);
+        std::memcpy(f + 16, &d, 4);
+        be = htons(uint16_t(L - 20));
+        std::memcpy(f + 24, &be, 2);
+        f[26] = f[27] = 0;
+        len[i] = L;
+        checksummer ipc;
+        ipc.sum(reinterpret_cast<const char*>(f), 20);
+        checksummer l4;
+        l4.sum_many(src, dst, uint8_t(0), uint8_t(17), uint16_t(L - 20));
+        l4.sum(reinterpret_cast<const char*>(f + 20), L - 20);
+        want[2 * i] = ipc.get();
+        want[2 * i + 1] = l4.get();
+    }
+
+    std::vector<uint16_t> got(2 * n, 0xdead);
+    uint64_t batches = 0, delivered = 0;
+    auto done = [&](uint64_t first, uint32_t count, const uint16_t* r, const uint8_t*) {
+        std::memcpy(got.data() + 2 * first, r, 4 * size_t(count));
+        ++batches;
+        delivered += count;
+    };
+    int bad = 0;
+    uint64_t busy = 0, bytes = 0;
+    double secs = 0;
+    try {
+        burst_queue<decltype(done)> q(0, SCCSUM_PIPE_IPV4, 16u << 20, 16384, 100000, depth, done);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint32_t k = static_cast<uint32_t>(i % pool_n);
+            const uint8_t* f = pool.data() + size_t(k) * kSlot + kData;
+            sccsum_fragment fr[2] = {{f, len[k]}, {nullptr, 0}};
+            uint32_t nf = 1;
+            if (i % 7 == 3 && len[k] > 333) {  // a chained mbuf with an odd-length first segment
+                fr[0].size = 333;
+                fr[1] = {f + 333, len[k] - 333u};
+                nf = 2;
+            }
+            uint64_t t = 0;
+            while (!q.submit(fr, nf, 0, &t)) {
+                ++busy;
+                q.poll();
+            }
+            if (t != i && bad++ < 5) std::printf("ticket %llu for packet %llu\n", (unsigned long long)t, (unsigned long long)i);
+            bytes += len[k];
+            if ((i & 31) == 31) q.poll();  // a burst of 32 handed over: the reactor runs its pollers
+        }
+        q.drain();
+        secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    } catch (const std::exception& e) {
+        std::printf("FAILED: %s\n", e.what());
+        return 2;
+    }
+    if (delivered != n) {
+        std::printf("delivered %llu of %llu\n", (unsigned long long)delivered, (unsigned long long)n);
+        ++bad;
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t k = static_cast<uint32_t>(i % pool_n);
+        if ((got[2 * i] != want[2 * k] || got[2 * i + 1] != want[2 * k + 1]) && bad++ < 10) {
+            std::printf("frame %llu: gpu %04x/%04x cpu %04x/%04x\n", (unsigned long long)i, got[2 * i], got[2 * i + 1],
+                        want[2 * k], want[2 * k + 1]);
+        }
+    }
+    std::printf("burst_gpu: %llu frames, %.1f MB, %llu batches, depth %d, %.3f s: %.2f Mpkt/s, %.2f GiB/s of packet "
+                "bytes, %llu busy polls\n",
+                (unsigned long long)n, bytes / 1e6, (unsigned long long)batches, depth, secs, n / secs / 1e6,
+                bytes / secs / (1u << 30), (unsigned long long)busy);
+    if (bad) {
+        std::printf("FAILED: %d mismatches\n", bad);
+        return 1;
+    }
+    std::printf("burst_gpu: OK\n");
+    return 0;
+}

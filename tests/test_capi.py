@@ -92,3 +92,27 @@ def test_rss_argument_validation_without_device():
     assert lib.sccsum_ipv4_rss(None, 0, None, None, None, 0, 0, None, None, 1, None) == native.SCCSUM_EINVAL
     assert lib.sccsum_ipv4_frames_rss(None, 0, None, None, None, None, 1, 0, None, 40, 0, None, None) \
         == native.SCCSUM_EINVAL
+
+
+def test_burst_argument_validation_without_device():
+    import ctypes
+
+    from seastar_amd import burst
+
+    lib = native.load()
+    out = ctypes.c_void_p()
+    fn = burst.DONE_FN(lambda *a: None)
+    cb = ctypes.cast(fn, ctypes.c_void_p)
+    for args in ((0, 7, 1 << 20, 64, 0, 2),     # mode
+                 (0, 0, 1 << 20, 64, 0, 0),     # depth 0
+                 (0, 0, 1 << 20, 64, 0, 65),    # depth > 64
+                 (0, 0, 1 << 20, 0, 0, 2),      # no packets per batch
+                 (0, 1, 32, 64, 0, 2)):         # batch under 64 bytes
+        assert lib.sccsum_burst_create(*args, cb, None, ctypes.byref(out)) == native.SCCSUM_EINVAL
+    assert lib.sccsum_burst_create(0, 0, 1 << 20, 64, 0, 2, None, None, ctypes.byref(out)) == native.SCCSUM_EINVAL
+    assert lib.sccsum_burst_submit(None, None, 0, 0, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_burst_poll(None, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_burst_drain(None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_burst_destroy(None) == native.SCCSUM_OK
+    assert lib.sccsum_strerror(native.SCCSUM_EBUSY) == b"every batch slot is in flight"
+    assert ctypes.sizeof(native.Fragment) == 16  # char* base; size_t size (packet.hh:43-46)

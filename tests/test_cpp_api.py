@@ -69,3 +69,44 @@ def test_batch_cpp_program_on_gpu(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK" in r.stdout
+
+
+def test_burst_queue_header_compiles(tmp_path):
+    """seastar::net::burst_queue over sccsum_burst_*, fed a packet's fragment
+    array in the reference's own layout (packet.hh:43-46)."""
+    src = tmp_path / "q.cc"
+    src.write_text(
+        '#include <seastar/net/ip_checksum_batch.hh>\n'
+        'struct fragment { char* base; size_t size; };  // seastar::net::fragment, packet.hh:43-46\n'
+        'static_assert(sizeof(fragment) == sizeof(sccsum_fragment) && alignof(fragment) == alignof(sccsum_fragment));\n'
+        'int main() {\n'
+        '    auto done = [](uint64_t, uint32_t, const uint16_t*, const uint8_t*) {};\n'
+        '    try {\n'
+        '        seastar::net::burst_queue<decltype(done)> q(0, SCCSUM_PIPE_IPV4, 1 << 20, 256, 20000, 2, done);\n'
+        '        char b[64] = {};\n'
+        '        fragment f[1] = {{b, 64}};\n'
+        '        (void)q.submit(reinterpret_cast<const sccsum_fragment*>(f), 1);\n'
+        '        q.poll();\n'
+        '        q.drain();\n'
+        '    } catch (const std::exception&) {\n'
+        '    }\n'
+        '    return 0;\n'
+        '}\n')
+    _build(tmp_path, "q", [str(src)], ["-L", os.path.join(REPO, "seastar_amd", "lib"), "-lsccsum",
+                                       "-Wl,-rpath," + os.path.join(REPO, "seastar_amd", "lib")])
+
+
+@pytest.mark.gpu
+def test_burst_cpp_program_on_gpu(tmp_path):
+    """Native host program: frames handed to burst_queue one at a time from
+    mbuf-shaped host slots (some as two fragments), compared frame by frame
+    with the per-packet C++ API."""
+    exe = _build(tmp_path, "burst_gpu",
+                 [os.path.join(REPO, "tests", "cpp", "burst_gpu.cc"),
+                  os.path.join(REPO, "seastar_amd", "csrc", "checksummer.cc")],
+                 ["-L", os.path.join(REPO, "seastar_amd", "lib"), "-lsccsum",
+                  "-Wl,-rpath," + os.path.join(REPO, "seastar_amd", "lib")])
+    r = subprocess.run([exe, "200000", "3"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout
+    print(r.stdout)

@@ -1,0 +1,81 @@
+"""Burst queue (sccsum_burst_*, the batching hook at the qp boundary, SURVEY.md
+§8(f)3) against the oracle: packets handed over one at a time as fragment
+lists, batched for the GPU, completed in submit order."""
+import numpy as np
+import pytest
+
+import oracle
+from seastar_amd import native, synth
+from seastar_amd.burst import BurstQueue
+
+pytestmark = pytest.mark.gpu
+
+
+def _split(rng, pkt):
+    """1-4 fragments at random cut points (odd lengths and empty fragments included)."""
+    cuts = sorted(int(c) for c in rng.integers(0, pkt.size + 1, size=int(rng.integers(0, 4))))
+    edges = [0, *cuts, pkt.size]
+    return [pkt[a:b] for a, b in zip(edges[:-1], edges[1:])]
+
+
+def _feed(q, rng, buf, off, lens, seeds=None, poll_every=7):
+    """Submit every packet (polling while the queue pushes back), poll every
+    few packets as the reactor would, drain at the end."""
+    tickets = []
+    for i in range(lens.size):
+        pkt = buf[int(off[i]):int(off[i]) + int(lens[i])]
+        frags = _split(rng, pkt)
+        while (t := q.submit(frags, 0 if seeds is None else int(seeds[i]))) is None:
+            q.poll()
+        tickets.append(t)
+        if i % poll_every == 0:
+            q.poll()
+    q.drain()
+    return tickets
+
+
+def test_burst_spans_fragments_seeds(dev):
+    rng = np.random.default_rng(51)
+    lens = np.concatenate([rng.integers(0, 2100, 3000), [0, 1, 9000, 65535, 70000]]).astype(np.uint32)
+    off, total = synth.pack(lens, seed=52, max_gap=3)
+    buf = rng.integers(0, 256, size=max(int(total), 1), dtype=np.uint8)
+    seeds = rng.integers(0, 65536, lens.size).astype(np.uint32)
+    q = BurstQueue(native.PIPE_SPANS, batch_bytes=256 << 10, batch_packets=200, max_delay_ns=0, depth=3)
+    tickets = _feed(q, rng, buf, off, lens, seeds)
+    assert tickets == list(range(lens.size))
+    got = np.array([int(q.results[t]) for t in tickets], np.uint16)
+    assert np.array_equal(got, oracle.batch_spans(buf, off, lens, seeds))
+    assert q.batches >= lens.size // 200
+    q.close()
+
+
+def test_burst_frames_and_backpressure(dev):
+    buf, off, lens, _ = synth.mixed_udp_frames(1500, seed=53, max_gap=3)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
+    rng = np.random.default_rng(54)
+    q = BurstQueue(native.PIPE_IPV4, batch_bytes=1 << 20, batch_packets=128, max_delay_ns=10**12, depth=2)
+    tickets = _feed(q, rng, buf, off, lens, poll_every=32)
+    assert tickets == list(range(lens.size))
+    got = np.stack([q.results[t] for t in tickets])
+    st = np.array([q.status[t] for t in tickets], np.uint8)
+    assert np.array_equal(got, want) and np.array_equal(st, want_st)
+    q.close()
+
+    # depth 1, one packet per batch: the second submit finds the only slot in flight
+    seen = []
+    q1 = BurstQueue(native.PIPE_IPV4, batch_bytes=64 << 10, batch_packets=1, max_delay_ns=10**12, depth=1,
+                    on_done=lambda first, r, s: seen.append((first, r, s)))
+    f0 = buf[int(off[0]):int(off[0]) + int(lens[0])]
+    f1 = buf[int(off[1]):int(off[1]) + int(lens[1])]
+    assert q1.submit([f0]) == 0
+    assert q1.submit([f1]) is None  # it launched the full slot; nothing is free until that one is delivered
+    q1.drain()
+    assert q1.submit([f1]) == 1
+    assert q1.poll() in (True, False)
+    q1.drain()
+    assert [s[0] for s in seen] == [0, 1]
+    assert np.array_equal(np.stack([s[1][0] for s in seen]), want[:2])
+    assert [int(s[2][0]) for s in seen] == [int(x) for x in want_st[:2]]
+    with pytest.raises(native.SccsumError):
+        q1.submit([np.zeros((64 << 10) + 1, np.uint8)])  # longer than a batch
+    q1.close()

@@ -514,3 +514,55 @@ def test_rss_errors(dev):
     assert lib.sccsum_ipv4_rss(*args, ctypes.addressof(k5), 5, 0, None, None, 1, None) == native.SCCSUM_EINVAL
     assert lib.sccsum_ipv4_rss(*args, ctypes.addressof(k5), 5, 0, batch.ctypes_ptr(h), None, 1, None) == native.SCCSUM_OK
     torch.cuda.synchronize()
+
+
+def test_packets_over_128k(dev, kernel_variant):
+    """Packets over 128 KiB leave the fast path for the exact redo (phase D);
+    their IPv4 header, pseudo-header and RSS inputs still come from the frame's
+    own head units.  Mixed with short frames in one tile; verify, spans, fused
+    RSS and in-place generate."""
+    lens = np.array([140_000, 1500, 131_073, 131_072, 64, 200_001, 1500, 300_000, 9000, 131_200], np.uint32)
+    buf, off, lens, _ = synth.mixed_udp_frames(lens.size, seed=91, max_gap=3, lengths=lens)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
+    got, st = _frames(dev, buf, off, lens)
+    assert np.array_equal(got, want) and np.array_equal(st, want_st)
+    assert np.array_equal(_spans(dev, buf, off, lens), oracle.batch_spans(buf, off, lens))
+    b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+    want_h, _ = oracle.batch_ipv4_rss(buf, off, lens)
+    out2, h = batch.ipv4_frames_rss(b)
+    torch.cuda.synchronize()
+    assert np.array_equal(h.cpu().numpy().view(np.uint32), want_h)
+    assert np.array_equal(batch.as_u16(out2), want)
+    m = native.FILL_IP | native.FILL_L4
+    out2 = torch.empty(2 * b.n, dtype=torch.int16, device=dev)
+    stf = torch.empty(b.n, dtype=torch.uint8, device=dev)
+    batch.ipv4_fill(b, m, out2=out2, status=stf)
+    torch.cuda.synchronize()
+    want_buf, want_out2, want_stf = oracle.batch_ipv4_fill(buf, off, lens, m)
+    assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want_out2)
+    assert np.array_equal(stf.cpu().numpy(), want_stf)
+    assert np.array_equal(b.data.cpu().numpy()[: buf.size], want_buf)
+
+
+def test_host_pipeline_strided_short_last_row(dev, kernel_variant):
+    """gather = 2 where the caller's buffer ends right after a short last
+    packet: the 2D copy reads every row W bytes wide, so that row goes in a
+    chunk of its own and nothing is read past the buffer."""
+    if kernel_variant not in (1, 15):
+        pytest.skip("pipeline chunking is kernel independent")
+    from seastar_amd import pipeline
+
+    rng = np.random.default_rng(41)
+    n = 300
+    lens = rng.integers(200, 600, size=n).astype(np.uint32)
+    lens[-1] = 20
+    off = np.arange(n, dtype=np.uint64) * 640 + 64
+    end = int(off[-1]) + 20
+    pool = pipeline.pinned_empty(end + 4096)
+    pool[:] = rng.integers(0, 256, size=pool.size, dtype=np.uint8)
+    seeds = rng.integers(0, 65536, n).astype(np.uint32)
+    want = oracle.batch_spans(pool[:end], off, lens, seeds)
+    pl = pipeline.HostPipeline(0, chunk_bytes=1 << 20, chunk_packets=128, depth=2)
+    got = pl.run(native.PIPE_SPANS, pool[:end], off, lens, seeds=seeds, gather=native.GATHER_STRIDED)
+    pl.close()
+    assert np.array_equal(got, want)
