@@ -328,6 +328,16 @@ typedef struct sccsum_fragment {
 int sccsum_burst_submit(sccsum_burst* b, const sccsum_fragment* frags, uint32_t nfrag, uint32_t seed,
                         uint64_t* ticket);
 
+/* Zero-copy submit: as sccsum_burst_submit, but the fragments lie in memory
+ * the device can read at the same address (see sccsum_gather: pinned or
+ * hipHostRegister'd host memory, or device memory) and must stay untouched
+ * until the packet's completion.  Only a descriptor is recorded; the batch's
+ * launch gathers the bytes on the device (over PCIe for host memory), so no
+ * host thread copies packet bytes.  Both submits may be mixed in one queue.
+ * SCCSUM_EINVAL also when a packet has more than 4 * batch_packets fragments. */
+int sccsum_burst_submit_mapped(sccsum_burst* b, const sccsum_fragment* frags, uint32_t nfrag, uint32_t seed,
+                               uint64_t* ticket);
+
 /* Reactor poller: launch the open batch if full or aged; deliver every
  * finished batch.  *did_work (may be NULL) = 1 when it launched or delivered. */
 int sccsum_burst_poll(sccsum_burst* b, int* did_work);
@@ -336,6 +346,21 @@ int sccsum_burst_poll(sccsum_burst* b, int* did_work);
 int sccsum_burst_drain(sccsum_burst* b);
 
 int sccsum_burst_destroy(sccsum_burst* b);
+
+/* Gather: copy n fragments into one device buffer, d_dst[dst_off ..
+ * +len) = src[0 .. len), for every descriptor (one kernel).  src may be device
+ * memory or pinned host memory the device can read at the same address
+ * (sccsum_host_alloc / hipHostMalloc; hipHostRegister'd memory such as a DPDK
+ * mempool, registered once) — then the bytes cross PCIe without a host thread
+ * touching them.  Any alignment; destinations must not overlap.  d_desc is a
+ * DEVICE array (8-byte aligned). */
+typedef struct sccsum_gather_desc {
+    const void* src;
+    uint32_t dst_off;
+    uint32_t len;
+} sccsum_gather_desc;
+
+int sccsum_gather(const sccsum_gather_desc* d_desc, uint64_t n, void* d_dst, void* stream);
 
 /* Pinned (page-locked) host memory for packet pools. */
 int sccsum_host_alloc(void** p, uint64_t bytes);

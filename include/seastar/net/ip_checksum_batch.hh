@@ -172,6 +172,14 @@ public:
         check(rc, "sccsum_burst_submit");
         return true;
     }
+    // zero-copy: fragments in device-readable pinned / registered host memory,
+    // untouched until their completion (sccsum_burst_submit_mapped)
+    bool submit_mapped(const sccsum_fragment* frags, uint32_t nfrag, uint32_t seed = 0, uint64_t* ticket = nullptr) {
+        const int rc = sccsum_burst_submit_mapped(_q, frags, nfrag, seed, ticket);
+        if (rc == SCCSUM_EBUSY) return false;
+        check(rc, "sccsum_burst_submit_mapped");
+        return true;
+    }
     bool poll() {
         int did = 0;
         check(sccsum_burst_poll(_q, &did), "sccsum_burst_poll");

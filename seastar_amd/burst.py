@@ -53,19 +53,23 @@ class BurstQueue:
             self.results[first + k] = r[k]
             self.status[first + k] = int(s[k])
 
-    def submit(self, fragments, seed: int = 0) -> int | None:
+    def submit(self, fragments, seed: int = 0, mapped: bool = False) -> int | None:
         """Stage one packet given as a list of uint8 arrays / bytes (its
         fragments, in order); returns its ticket, or None when every slot is
-        in flight (poll, then retry)."""
+        in flight (poll, then retry).  mapped=True: zero-copy
+        (sccsum_burst_submit_mapped) — the arrays must be views of pinned
+        memory (pipeline.pinned_empty) and stay untouched until completion."""
         bufs = [np.ascontiguousarray(np.frombuffer(f, np.uint8) if isinstance(f, (bytes, bytearray)) else f,
                                      dtype=np.uint8) for f in fragments]
+        if mapped and not all(isinstance(f, np.ndarray) and f.flags.c_contiguous for f in fragments):
+            raise ValueError("mapped fragments must be contiguous views of pinned memory")
         frags = (native.Fragment * max(len(bufs), 1))()
         for j, b in enumerate(bufs):
             frags[j].base = b.ctypes.data if b.size else None
             frags[j].size = b.size
         ticket = ctypes.c_uint64()
-        code = self._lib.sccsum_burst_submit(self._h, ctypes.cast(frags, ctypes.c_void_p), len(bufs), seed,
-                                             ctypes.byref(ticket))
+        fn = self._lib.sccsum_burst_submit_mapped if mapped else self._lib.sccsum_burst_submit
+        code = fn(self._h, ctypes.cast(frags, ctypes.c_void_p), len(bufs), seed, ctypes.byref(ticket))
         if code == native.SCCSUM_EBUSY:
             return None
         native.check(code, "sccsum_burst_submit")

@@ -15,10 +15,17 @@
 //            loads); landing contiguously keeps checksummer::sum(const
 //            packet&)'s odd carry (ip_checksum.cc:64-68) with no device work.
 //            SCCSUM_EBUSY when every slot is in flight (poll, then retry)
+//   submit_mapped: zero-copy — the fragments lie in memory the device reads
+//            (pinned / registered host memory, e.g. a DPDK mempool): only a
+//            {src, dst, len} descriptor is recorded; at launch a gather kernel
+//            (sccsum_gather) pulls the bytes over PCIe into the batch, so no
+//            host thread touches packet bytes
 //   poll:    launch the open slot when full (bytes / packets) or older than
-//            max_delay_ns — on the slot's own stream: H2D of the staged bytes
-//            + metadata, the kernel, D2H of the results, an event, so one
-//            batch's copies overlap the previous batch's kernel; then deliver
+//            max_delay_ns — on the slot's own stream: ONE H2D of the staged
+//            bytes with the metadata packed behind them, the kernel, ONE D2H
+//            of results + status, an event (4 stream operations: launch cost
+//            is per batch, not per array), so one batch's copies overlap the
+//            previous batch's kernel; then deliver
 //            every finished slot, oldest first, through the completion
 //            callback (results in submit order, tickets consecutive)
 //   drain:   launch what is staged, wait for everything, deliver
@@ -37,21 +44,21 @@ struct sccsum_burst {
     struct Slot {
         state st = state::free;
         hipStream_t stream = nullptr;
-        uint8_t* h_bytes = nullptr;  // pinned staging: packets back to back
-        uint64_t* h_off = nullptr;
+        // pinned staging: packets back to back, then (at launch) the metadata
+        // arrays packed right behind them, so one H2D carries the whole batch
+        uint8_t* h_stage = nullptr;
+        uint64_t* h_off = nullptr;  // metadata as submitted
         uint32_t* h_len = nullptr;
         uint32_t* h_seed = nullptr;
-        uint16_t* h_out = nullptr;
-        uint8_t* h_status = nullptr;
-        uint8_t* d_bytes = nullptr;
-        uint64_t* d_off = nullptr;
-        uint32_t* d_len = nullptr;
-        uint32_t* d_seed = nullptr;
-        uint16_t* d_out = nullptr;
-        uint8_t* d_status = nullptr;
+        sccsum_gather_desc* h_desc = nullptr;  // zero-copy fragments (submit_mapped)
+        uint8_t* h_res = nullptr;  // results then status, one D2H
+        uint8_t* d_stage = nullptr;
+        uint8_t* d_res = nullptr;
         hipEvent_t done = nullptr;
         uint64_t used = 0;  // staged bytes
         uint32_t npk = 0;
+        uint32_t ndesc = 0;   // mapped fragments the device gathers
+        bool copied = false;  // some packet was memcpy'd into h_stage
         uint32_t max_len = 0;
         uint64_t first_ticket = 0;
         std::chrono::steady_clock::time_point opened{};
@@ -82,40 +89,62 @@ int hip_rc(hipError_t e) { return e == hipSuccess ? SCCSUM_OK : static_cast<int>
     } while (0)
 
 void free_slot(sccsum_burst::Slot& s) {
-    (void)hipHostFree(s.h_bytes);
+    (void)hipHostFree(s.h_stage);
     (void)hipHostFree(s.h_off);
     (void)hipHostFree(s.h_len);
     (void)hipHostFree(s.h_seed);
-    (void)hipHostFree(s.h_out);
-    (void)hipHostFree(s.h_status);
-    (void)hipFree(s.d_bytes);
-    (void)hipFree(s.d_off);
-    (void)hipFree(s.d_len);
-    (void)hipFree(s.d_seed);
-    (void)hipFree(s.d_out);
-    (void)hipFree(s.d_status);
+    (void)hipHostFree(s.h_desc);
+    (void)hipHostFree(s.h_res);
+    (void)hipFree(s.d_stage);
+    (void)hipFree(s.d_res);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
 }
 
 int width(const sccsum_burst* b) { return b->mode == SCCSUM_PIPE_IPV4 ? 2 : 1; }
 
+// gather descriptors per slot (a packet of more fragments launches its slot early)
+uint64_t desc_cap(const sccsum_burst* b) { return 4ull * b->batch_packets; }
+
+// staging bytes per slot: the data room plus room for the packed metadata
+// and gather descriptors
+uint64_t stage_bytes(const sccsum_burst* b) {
+    return b->batch_bytes + 16ull * b->batch_packets + sizeof(sccsum_gather_desc) * desc_cap(b) + 32;
+}
+
+// One H2D (packets + metadata packed behind them), the kernel, one D2H
+// (results + status), an event: 4 stream operations per batch.
 int launch_slot(sccsum_burst* b, sccsum_burst::Slot& s) {
+    SCCSUM_TRY(hipSetDevice(b->device));
     const hipStream_t st = s.stream;
     const uint64_t n = s.npk;
-    SCCSUM_TRY(hipMemcpyAsync(s.d_bytes, s.h_bytes, (s.used + 15) & ~uint64_t(15), hipMemcpyHostToDevice, st));
-    SCCSUM_TRY(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice, st));
-    SCCSUM_TRY(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice, st));
-    int rk;
-    if (b->mode == SCCSUM_PIPE_IPV4) {
-        rk = sccsum_ipv4_frames(s.d_bytes, s.used, s.d_off, s.d_len, s.d_out, s.d_status, n, s.max_len, st);
-    } else {
-        SCCSUM_TRY(hipMemcpyAsync(s.d_seed, s.h_seed, n * 4, hipMemcpyHostToDevice, st));
-        rk = sccsum_spans(s.d_bytes, s.used, s.d_off, s.d_len, s.d_seed, s.d_out, s.d_status, n, s.max_len, st);
+    const uint64_t a_off = (s.used + 15) & ~uint64_t(15), a_len = a_off + 8 * n, a_seed = a_len + 4 * n;
+    const bool spans = b->mode != SCCSUM_PIPE_IPV4;
+    const uint64_t a_desc = ((spans ? a_seed + 4 * n : a_seed) + 7) & ~uint64_t(7);
+    const uint64_t total = a_desc + sizeof(sccsum_gather_desc) * s.ndesc;
+    std::memcpy(s.h_stage + a_off, s.h_off, 8 * n);
+    std::memcpy(s.h_stage + a_len, s.h_len, 4 * n);
+    if (spans) std::memcpy(s.h_stage + a_seed, s.h_seed, 4 * n);
+    if (s.ndesc) std::memcpy(s.h_stage + a_desc, s.h_desc, sizeof(sccsum_gather_desc) * s.ndesc);
+    // only mapped packets: the packet bytes come over PCIe through the gather,
+    // the H2D carries the metadata alone
+    const uint64_t from = s.copied ? 0 : a_off;
+    SCCSUM_TRY(hipMemcpyAsync(s.d_stage + from, s.h_stage + from, total - from, hipMemcpyHostToDevice, st));
+    if (s.ndesc) {
+        const int rg = sccsum_gather(reinterpret_cast<const sccsum_gather_desc*>(s.d_stage + a_desc), s.ndesc,
+                                     s.d_stage, st);
+        if (rg != SCCSUM_OK) return rg;
     }
+    const auto* d_off = reinterpret_cast<const uint64_t*>(s.d_stage + a_off);
+    const auto* d_len = reinterpret_cast<const uint32_t*>(s.d_stage + a_len);
+    auto* d_out = reinterpret_cast<uint16_t*>(s.d_res);
+    uint8_t* d_status = s.d_res + 2 * width(b) * n;
+    const int rk = spans ? sccsum_spans(s.d_stage, s.used, d_off, d_len,
+                                        reinterpret_cast<const uint32_t*>(s.d_stage + a_seed), d_out, d_status, n,
+                                        s.max_len, st)
+                         : sccsum_ipv4_frames(s.d_stage, s.used, d_off, d_len, d_out, d_status, n, s.max_len, st);
     if (rk != SCCSUM_OK) return rk;
-    SCCSUM_TRY(hipMemcpyAsync(s.h_out, s.d_out, n * width(b) * 2, hipMemcpyDeviceToHost, st));
-    SCCSUM_TRY(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, st));
+    SCCSUM_TRY(hipMemcpyAsync(s.h_res, s.d_res, (2 * width(b) + 1) * n, hipMemcpyDeviceToHost, st));
     SCCSUM_TRY(hipEventRecord(s.done, st));
     s.st = sccsum_burst::state::inflight;
     ++b->inflight;
@@ -136,10 +165,13 @@ int deliver(sccsum_burst* b, bool wait, bool* did) {
             if (q == hipErrorNotReady) break;
             SCCSUM_TRY(q);
         }
-        b->fn(b->user, s.first_ticket, s.npk, s.h_out, s.h_status);
+        b->fn(b->user, s.first_ticket, s.npk, reinterpret_cast<const uint16_t*>(s.h_res),
+              s.h_res + 2 * width(b) * s.npk);
         s.st = sccsum_burst::state::free;
         s.used = 0;
         s.npk = 0;
+        s.ndesc = 0;
+        s.copied = false;
         s.max_len = 0;
         --b->inflight;
         b->next_deliver = (b->next_deliver + 1) % b->slots.size();
@@ -175,19 +207,21 @@ int sccsum_burst_create(int device, int mode, uint64_t batch_bytes, uint32_t bat
     int rc = SCCSUM_OK;
     for (auto& s : b->slots) {
         rc = hip_rc(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-        if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_bytes, b->batch_bytes, hipHostMallocDefault));
+        if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_stage, stage_bytes(b), hipHostMallocDefault));
         if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_off, np * 8, hipHostMallocDefault));
         if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_len, np * 4, hipHostMallocDefault));
         if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_seed, np * 4, hipHostMallocDefault));
-        if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_out, np * w * 2, hipHostMallocDefault));
-        if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_status, np, hipHostMallocDefault));
-        if (rc == SCCSUM_OK) rc = hip_rc(hipMalloc(&s.d_bytes, b->batch_bytes));
-        if (rc == SCCSUM_OK) rc = hip_rc(hipMalloc(&s.d_off, np * 8));
-        if (rc == SCCSUM_OK) rc = hip_rc(hipMalloc(&s.d_len, np * 4));
-        if (rc == SCCSUM_OK) rc = hip_rc(hipMalloc(&s.d_seed, np * 4));
-        if (rc == SCCSUM_OK) rc = hip_rc(hipMalloc(&s.d_out, np * w * 2));
-        if (rc == SCCSUM_OK) rc = hip_rc(hipMalloc(&s.d_status, np));
+        if (rc == SCCSUM_OK) {
+            rc = hip_rc(hipHostMalloc(&s.h_desc, desc_cap(b) * sizeof(sccsum_gather_desc), hipHostMallocDefault));
+        }
+        if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_res, np * (2 * w + 1), hipHostMallocDefault));
+        if (rc == SCCSUM_OK) rc = hip_rc(hipMalloc(&s.d_stage, stage_bytes(b)));
+        if (rc == SCCSUM_OK) rc = hip_rc(hipMalloc(&s.d_res, np * (2 * w + 1)));
         if (rc == SCCSUM_OK) rc = hip_rc(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        // first use of a stream creates its hardware queue (milliseconds):
+        // pay that here, not on the first batches
+        if (rc == SCCSUM_OK) rc = hip_rc(hipMemsetAsync(s.d_res, 0, 1, s.stream));
+        if (rc == SCCSUM_OK) rc = hip_rc(hipStreamSynchronize(s.stream));
         if (rc != SCCSUM_OK) break;
     }
     if (rc != SCCSUM_OK) {
@@ -198,16 +232,20 @@ int sccsum_burst_create(int device, int mode, uint64_t batch_bytes, uint32_t bat
     return SCCSUM_OK;
 }
 
-int sccsum_burst_submit(sccsum_burst* b, const sccsum_fragment* frags, uint32_t nfrag, uint32_t seed,
-                        uint64_t* ticket) {
+// Both submits: validate, find room in the open slot (launching it when the
+// packet does not fit), then place the packet by copy or by descriptor.
+static int submit(sccsum_burst* b, const sccsum_fragment* frags, uint32_t nfrag, uint32_t seed, uint64_t* ticket,
+                  bool mapped) {
     if (!b || (nfrag && !frags)) return SCCSUM_EINVAL;
     uint64_t L = 0;
+    uint32_t nd = 0;
     for (uint32_t j = 0; j < nfrag; ++j) {
         if ((!frags[j].base && frags[j].size) || frags[j].size > b->batch_bytes) return SCCSUM_EINVAL;
         L += frags[j].size;
+        nd += frags[j].size != 0;
     }
     if (L > b->batch_bytes || L > UINT32_MAX) return SCCSUM_EINVAL;  // never fits a batch
-    SCCSUM_TRY(hipSetDevice(b->device));
+    if (mapped && nd > desc_cap(b)) return SCCSUM_EINVAL;
     for (int attempt = 0; attempt < 2; ++attempt) {
         if (b->open == SIZE_MAX) {
             auto& s = b->slots[b->next_launch];
@@ -219,16 +257,24 @@ int sccsum_burst_submit(sccsum_burst* b, const sccsum_fragment* frags, uint32_t 
         }
         auto& s = b->slots[b->open];
         const uint64_t at = (s.used + 15) & ~uint64_t(15);  // 16-byte aligned starts: full-rate loads
-        if (s.npk == b->batch_packets || at + L > b->batch_bytes) {
+        if (s.npk == b->batch_packets || at + L > b->batch_bytes || (mapped && s.ndesc + nd > desc_cap(b))) {
             const int rc = launch_slot(b, s);  // full: send it, open the next slot
             if (rc != SCCSUM_OK) return rc;
             continue;
         }
         uint64_t pos = at;
         for (uint32_t j = 0; j < nfrag; ++j) {
-            if (frags[j].size) std::memcpy(s.h_bytes + pos, frags[j].base, frags[j].size);
+            if (frags[j].size) {
+                if (mapped) {
+                    s.h_desc[s.ndesc++] = {frags[j].base, static_cast<uint32_t>(pos),
+                                           static_cast<uint32_t>(frags[j].size)};
+                } else {
+                    std::memcpy(s.h_stage + pos, frags[j].base, frags[j].size);
+                }
+            }
             pos += frags[j].size;
         }
+        s.copied |= !mapped && L;
         s.h_off[s.npk] = at;
         s.h_len[s.npk] = static_cast<uint32_t>(L);
         s.h_seed[s.npk] = seed;
@@ -240,6 +286,16 @@ int sccsum_burst_submit(sccsum_burst* b, const sccsum_fragment* frags, uint32_t 
         return SCCSUM_OK;
     }
     return SCCSUM_EBUSY;
+}
+
+int sccsum_burst_submit(sccsum_burst* b, const sccsum_fragment* frags, uint32_t nfrag, uint32_t seed,
+                        uint64_t* ticket) {
+    return submit(b, frags, nfrag, seed, ticket, false);
+}
+
+int sccsum_burst_submit_mapped(sccsum_burst* b, const sccsum_fragment* frags, uint32_t nfrag, uint32_t seed,
+                               uint64_t* ticket) {
+    return submit(b, frags, nfrag, seed, ticket, true);
 }
 
 int sccsum_burst_poll(sccsum_burst* b, int* did_work) {

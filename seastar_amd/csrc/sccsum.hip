@@ -1673,6 +1673,37 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
     return static_cast<int>(hipGetLastError());
 }
 
+// ---- gather: fragments from device-readable memory (HBM, or pinned host
+// memory read over PCIe) into one device buffer.  The burst queue's zero-copy
+// submit (burst.cc) uses it so that no host thread touches packet bytes.
+// One wave per fragment, grid-stride; interior 16-byte blocks of the
+// destination move as one (possibly unaligned) 16-byte load + one aligned
+// store, the two edge blocks byte by byte (neighbouring fragments are written
+// by other waves at the same time).
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+
+__global__ __launch_bounds__(kBlock) void gather_kernel(const sccsum_gather_desc* __restrict__ desc, uint64_t n,
+                                                        uint8_t* __restrict__ dst) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+    for (uint64_t w = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6; w < n; w += nw) {
+        const sccsum_gather_desc d = desc[w];
+        const uint8_t* src = static_cast<const uint8_t*>(d.src);
+        uint8_t* o = dst + d.dst_off;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(o), e = a + d.len;
+        for (uintptr_t blk = (a & ~uintptr_t(15)) + 16u * lane; blk < e; blk += 1024u) {
+            if (blk >= a && blk + 16u <= e) {
+                *reinterpret_cast<u32x4*>(blk) = *reinterpret_cast<const u32x4u*>(src + (blk - a));
+            } else {
+                for (uint32_t k = 0; k < 16u; ++k) {
+                    const uintptr_t p = blk + k;
+                    if (p >= a && p < e) *reinterpret_cast<uint8_t*>(p) = src[p - a];
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
 }  // namespace sccsum
 
@@ -1754,6 +1785,15 @@ int sccsum_ipv4_frames_rss(const void* d_bytes, uint64_t bytes_len, const uint64
     const sccsum::RssParams P = sccsum::make_rss(key, key_len, static_cast<uint32_t>(rss_mode), d_hash);
     return sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len, stream, 0u,
                                 P);
+}
+
+int sccsum_gather(const sccsum_gather_desc* d_desc, uint64_t n, void* d_dst, void* stream) {
+    if (n == 0) return SCCSUM_OK;
+    if (!d_desc || !d_dst || (reinterpret_cast<uintptr_t>(d_desc) & 7u)) return SCCSUM_EINVAL;
+    const uint64_t blocks = std::min<uint64_t>((n + 3) / 4, 65536);
+    sccsum::gather_kernel<<<dim3(static_cast<unsigned>(blocks)), dim3(sccsum::kBlock), 0,
+                            static_cast<hipStream_t>(stream)>>>(d_desc, n, static_cast<uint8_t*>(d_dst));
+    return static_cast<int>(hipGetLastError());
 }
 
 uint64_t sccsum_fragments_workspace(uint64_t nfrag) { return ((2 * nfrag + 15) & ~uint64_t(15)) + nfrag + 16; }

@@ -6,6 +6,8 @@
 // an odd offset (the `odd` carry of checksummer::sum(const packet&),
 // ip_checksum.cc:64-68).  Every result is checked against the per-packet API;
 // the hook's throughput is printed.  Usage: burst_gpu [frames] [depth]
+// [max_delay_ns] [copy|mapped]: mapped = the pool is pinned (as a DPDK mempool
+// registered with the device) and frames go in by zero-copy submit_mapped.
 #include <seastar/net/ip_checksum.hh>
 #include <seastar/net/ip_checksum_batch.hh>
 
@@ -23,15 +25,21 @@ using namespace seastar::net;
 int main(int argc, char** argv) {
     const uint64_t n = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 50000;
     const int depth = argc > 2 ? std::atoi(argv[2]) : 4;
+    const uint64_t delay_ns = argc > 3 ? std::strtoull(argv[3], nullptr, 0) : 100000;
     constexpr uint32_t kSlot = 2304, kData = 256;
     const uint32_t pool_n = static_cast<uint32_t>(n < 65536 ? n : 65536);  // slots, reused round robin
     std::mt19937 rng(11);
-    std::vector<uint8_t> pool(size_t(pool_n) * kSlot);
+    const bool mapped = argc > 4 && std::strcmp(argv[4], "mapped") == 0;
+    uint8_t* pool = nullptr;
+    if (sccsum_host_alloc(reinterpret_cast<void**>(&pool), uint64_t(pool_n) * kSlot) != SCCSUM_OK) {
+        std::printf("FAILED: sccsum_host_alloc\n");
+        return 2;
+    }
     std::vector<uint32_t> len(pool_n);
     std::vector<uint16_t> want(2 * size_t(pool_n));
     for (uint32_t i = 0; i < pool_n; ++i) {
         const uint32_t L = 28 + rng() % 1473;  // 20 B IPv4 + 8 B UDP + payload, up to 1500
-        uint8_t* f = pool.data() + size_t(i) * kSlot + kData;
+        uint8_t* f = pool + size_t(i) * kSlot + kData;
         for (uint32_t k = 0; k < L; ++k) f[k] = uint8_t(rng());
         const uint32_t src = rng(), dst = rng();
         f[0] = 0x45;
@@ -69,11 +77,11 @@ int main(int argc, char** argv) {
     uint64_t busy = 0, bytes = 0;
     double secs = 0;
     try {
-        burst_queue<decltype(done)> q(0, SCCSUM_PIPE_IPV4, 16u << 20, 16384, 100000, depth, done);
+        burst_queue<decltype(done)> q(0, SCCSUM_PIPE_IPV4, 16u << 20, 16384, delay_ns, depth, done);
         const auto t0 = std::chrono::steady_clock::now();
         for (uint64_t i = 0; i < n; ++i) {
             const uint32_t k = static_cast<uint32_t>(i % pool_n);
-            const uint8_t* f = pool.data() + size_t(k) * kSlot + kData;
+            const uint8_t* f = pool + size_t(k) * kSlot + kData;
             sccsum_fragment fr[2] = {{f, len[k]}, {nullptr, 0}};
             uint32_t nf = 1;
             if (i % 7 == 3 && len[k] > 333) {  // a chained mbuf with an odd-length first segment
@@ -82,7 +90,7 @@ int main(int argc, char** argv) {
                 nf = 2;
             }
             uint64_t t = 0;
-            while (!q.submit(fr, nf, 0, &t)) {
+            while (!(mapped ? q.submit_mapped(fr, nf, 0, &t) : q.submit(fr, nf, 0, &t))) {
                 ++busy;
                 q.poll();
             }
@@ -107,10 +115,11 @@ int main(int argc, char** argv) {
                         want[2 * k], want[2 * k + 1]);
         }
     }
-    std::printf("burst_gpu: %llu frames, %.1f MB, %llu batches, depth %d, %.3f s: %.2f Mpkt/s, %.2f GiB/s of packet "
+    std::printf("burst_gpu: %llu frames, %.1f MB, %llu batches, depth %d, delay %llu ns, %s, %.3f s: %.2f Mpkt/s, %.2f GiB/s of packet "
                 "bytes, %llu busy polls\n",
-                (unsigned long long)n, bytes / 1e6, (unsigned long long)batches, depth, secs, n / secs / 1e6,
+                (unsigned long long)n, bytes / 1e6, (unsigned long long)batches, depth, (unsigned long long)delay_ns, mapped ? "mapped" : "copy", secs, n / secs / 1e6,
                 bytes / secs / (1u << 30), (unsigned long long)busy);
+    sccsum_host_free(pool);
     if (bad) {
         std::printf("FAILED: %d mismatches\n", bad);
         return 1;

@@ -111,6 +111,10 @@ def test_burst_argument_validation_without_device():
         assert lib.sccsum_burst_create(*args, cb, None, ctypes.byref(out)) == native.SCCSUM_EINVAL
     assert lib.sccsum_burst_create(0, 0, 1 << 20, 64, 0, 2, None, None, ctypes.byref(out)) == native.SCCSUM_EINVAL
     assert lib.sccsum_burst_submit(None, None, 0, 0, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_burst_submit_mapped(None, None, 0, 0, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_gather(None, 0, None, None) == native.SCCSUM_OK  # nothing to do
+    assert lib.sccsum_gather(None, 1, None, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_gather(ctypes.c_void_p(12), 1, ctypes.c_void_p(64), None) == native.SCCSUM_EINVAL  # desc align
     assert lib.sccsum_burst_poll(None, None) == native.SCCSUM_EINVAL
     assert lib.sccsum_burst_drain(None) == native.SCCSUM_EINVAL
     assert lib.sccsum_burst_destroy(None) == native.SCCSUM_OK

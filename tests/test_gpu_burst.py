@@ -79,3 +79,94 @@ def test_burst_frames_and_backpressure(dev):
     with pytest.raises(native.SccsumError):
         q1.submit([np.zeros((64 << 10) + 1, np.uint8)])  # longer than a batch
     q1.close()
+
+
+def _pinned_copy(buf):
+    from seastar_amd import pipeline
+
+    pool = pipeline.pinned_empty(buf.size + 64)
+    pool[: buf.size] = buf
+    return pool
+
+
+def test_burst_mapped_zero_copy(dev):
+    """sccsum_burst_submit_mapped: fragments in pinned host memory, gathered
+    over PCIe by the device; odd fragment cuts, empty packets, seeds."""
+    rng = np.random.default_rng(55)
+    lens = np.concatenate([rng.integers(0, 2100, 2500), [0, 1, 9000, 65535]]).astype(np.uint32)
+    off, total = synth.pack(lens, seed=56, max_gap=5)
+    host = rng.integers(0, 256, size=max(int(total), 1), dtype=np.uint8)
+    buf = _pinned_copy(host)
+    seeds = rng.integers(0, 65536, lens.size).astype(np.uint32)
+    q = BurstQueue(native.PIPE_SPANS, batch_bytes=256 << 10, batch_packets=150, max_delay_ns=0, depth=3)
+    tickets = []
+    for i in range(lens.size):
+        pkt = buf[int(off[i]):int(off[i]) + int(lens[i])]
+        while (t := q.submit(_split(rng, pkt), int(seeds[i]), mapped=True)) is None:
+            q.poll()
+        tickets.append(t)
+        if i % 5 == 0:
+            q.poll()
+    q.drain()
+    assert tickets == list(range(lens.size))
+    got = np.array([int(q.results[t]) for t in tickets], np.uint16)
+    assert np.array_equal(got, oracle.batch_spans(host, off, lens, seeds))
+    q.close()
+
+
+def test_burst_mixed_copy_and_mapped(dev):
+    """Copied and zero-copy packets alternate inside the same batches (the
+    H2D then carries the staged bytes and the gather fills the rest)."""
+    host, off, lens, _ = synth.mixed_udp_frames(1200, seed=57, max_gap=3)
+    want, want_st = oracle.batch_ipv4(host, off, lens)
+    buf = _pinned_copy(host)
+    rng = np.random.default_rng(58)
+    q = BurstQueue(native.PIPE_IPV4, batch_bytes=1 << 20, batch_packets=100, max_delay_ns=10**12, depth=2)
+    for i in range(lens.size):
+        src = buf if i % 3 else host
+        pkt = src[int(off[i]):int(off[i]) + int(lens[i])]
+        while q.submit(_split(rng, pkt), mapped=bool(i % 3)) is None:
+            q.poll()
+    q.drain()
+    got = np.stack([q.results[t] for t in range(lens.size)])
+    st = np.array([q.status[t] for t in range(lens.size)], np.uint8)
+    assert np.array_equal(got, want) and np.array_equal(st, want_st)
+    q.close()
+
+
+def test_gather_kernel_any_alignment(dev):
+    """sccsum_gather from pinned host memory and from device memory into odd
+    destination offsets; bytes between the fragments stay untouched."""
+    import ctypes
+
+    import torch
+
+    lib = native.load()
+    rng = np.random.default_rng(59)
+    n = 3000
+    lens = rng.integers(0, 3000, n).astype(np.uint32)
+    lens[:5] = [0, 1, 15, 16, 17]
+    src_off, stotal = synth.pack(lens, seed=60, max_gap=7)
+    host = rng.integers(0, 256, size=int(stotal) + 64, dtype=np.uint8)
+    pinned = _pinned_copy(host)
+    gaps = rng.integers(0, 9, n)
+    dst_off = np.zeros(n, np.uint64)
+    pos = 3
+    for i in range(n):
+        dst_off[i] = pos
+        pos += int(lens[i]) + int(gaps[i])
+    d_src = torch.from_numpy(host).to(dev)
+    for base in (pinned.ctypes.data, d_src.data_ptr()):
+        desc = np.zeros(n, dtype=[("src", "<u8"), ("dst_off", "<u4"), ("len", "<u4")])
+        desc["src"] = base + src_off
+        desc["dst_off"] = dst_off
+        desc["len"] = lens
+        d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+        dst = torch.full((pos + 16,), 0xA5, dtype=torch.uint8, device=dev)
+        assert lib.sccsum_gather(ctypes.c_void_p(d_desc.data_ptr()), n, ctypes.c_void_p(dst.data_ptr()),
+                                 None) == native.SCCSUM_OK
+        torch.cuda.synchronize()
+        want = np.full(pos + 16, 0xA5, np.uint8)
+        for i in range(n):
+            want[int(dst_off[i]):int(dst_off[i]) + int(lens[i])] = host[int(src_off[i]):int(src_off[i]) + int(lens[i])]
+        assert np.array_equal(dst.cpu().numpy(), want)
