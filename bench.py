@@ -9,9 +9,22 @@ that traffic when offload is off, both directions:
   verify:   sccsum_ipv4_frames over the rx batch (checksums stored, 1 % of
             frames corrupted) -> per-frame pass/fail status (ip.cc:121-127, tcp.hh:876-883)
 value = bytes checksummed by all ranks / max-over-ranks wall time, GiB/s.
+
 Multi-GPU: one process per GPU, each with its own independent shard (weak
 scaling, no data-path collective; the only collectives are the timing
-barrier and the max-over-ranks reduction).
+barrier and the max-over-ranks reduction, on gloo).  Under torchrun the ranks
+come from the environment; `python bench.py --gpus N` without it starts the N
+rank processes itself (launch_ranks).
+
+Other configs (--config): mixed = cfg 3, tcp64k = cfg 4 (one GPU's shard),
+fill = cfg 2 tx with in-place write-back, e2e = cfg 5 (PCIe-inclusive, pinned
+mbuf-shaped host buffers), sweep = device-resident rate against batch size at
+the reference's batch boundaries.
+
+Every kernel-timed line carries "roofline" with "trace_select": which
+dispatches of which kernel in this process were the timed ones, so
+tools/prof_timed.py can cut exactly those out of a rocprofv3 kernel trace (or
+a PMC pass) of the same command.
 """
 from __future__ import annotations
 
@@ -19,22 +32,28 @@ import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
-from seastar_amd import batch, devsynth, native  # noqa: E402
-
 METRIC = "GiB/s device-resident Internet checksum, 1500B-packet batches, 1/2/4/8 GPUs"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 FRAME = 1500
 META_BYTES = 12  # u64 offset + u32 length per packet
 SEED = 0x5EA57A2C
+
+
+def flat_kernel(ipv4: bool, fill: bool, n: int, nbytes: int) -> str:
+    """The flat-kernel instantiation the library's default picks (sccsum.hip
+    launch(): U = 16 for >= 512 Ki packets and >= 256 MiB, else U = 8 with
+    the next chunk in flight), as rocprofv3 names it."""
+    big = n >= (512 << 10) and nbytes >= (256 << 20)
+    u, pipe = (16, "false") if big else (8, "true")
+    return f"csum_flat_kernel<{u}, {str(ipv4).lower()}, {str(fill).lower()}, {pipe}>"
 
 
 def parse():
@@ -46,14 +65,50 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the pre-timing parity check (A/B builds only)")
-    ap.add_argument("--pmc", default=None, help="PMC summary JSON for roofline.traffic (default: newest in profiles/)")
+    ap.add_argument("--pmc", default=None, help="PMC summary JSON for roofline.traffic (default: newest for the config)")
     ap.add_argument("--rotate", type=int, default=4,
                     help="distinct batches (pairs for udp1500) launched in turn, so no launch replays cached lines")
-    ap.add_argument("--config", default="udp1500", choices=["udp1500", "mixed", "tcp64k", "e2e", "fill"],
+    ap.add_argument("--config", default="udp1500", choices=["udp1500", "mixed", "tcp64k", "e2e", "fill", "sweep"],
                     help="udp1500 = the metric's config (cfg 2, default); mixed = cfg 3; tcp64k = cfg 4 "
                          "(per-GPU shard); e2e = cfg 5 (pinned host mbufs, PCIe-inclusive); fill = cfg 2 tx "
-                         "generate with in-place write-back (sccsum_ipv4_fill)")
+                         "generate with in-place write-back (sccsum_ipv4_fill); sweep = rate against batch size")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="multi-rank plumbing only: launch, rendezvous, barrier, max-over-ranks, one line; "
+                         "no device call (the CPU test of the launcher)")
     return ap.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` without a torch.distributed launcher: start
+    N rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set, one GPU each), wait for all and return the worst exit code.
+    This process never touches HIP (nothing has imported torch yet) and never
+    execs: the ranks are children.  Rank 0 prints the JSON line on the shared
+    stdout.  Reference analogue: one independent engine per shard,
+    src/net/net.cc:309-341."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("GLOO_SOCKET_IFNAME", "lo")  # one node: the control plane stays on loopback
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+def _imports():
+    """torch and the engine are imported only in a rank process (the
+    multi-rank launcher must not touch HIP before it starts the ranks)."""
+    global np, torch, batch, devsynth, native
+    import numpy as np
+    import torch
+
+    from seastar_amd import batch, devsynth, native
 
 
 # The path exchanges no data between GPUs (independent shards, SURVEY.md §8(e)):
@@ -63,10 +118,16 @@ def parse():
 BACKEND = os.environ.get("SCCSUM_DIST_BACKEND", "gloo")
 
 
-def dist_setup():
+def dist_setup(dry_run=False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if dry_run:
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.init_process_group("gloo")
+        return world, rank, local
     ndev = torch.cuda.device_count()
     dev = local % max(ndev, 1)
     torch.cuda.set_device(dev)
@@ -98,6 +159,17 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
+def cpu_threads() -> tuple[int, str]:
+    """Host threads for the CPU baseline: the cores this process may run on,
+    capped by OMP_NUM_THREADS when the environment sets it (the GPU box sets
+    16 = its CPU share per GPU; os.cpu_count() there shows the whole host)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < aff:
+        return int(omp), f"OMP_NUM_THREADS={omp} (of {aff} schedulable)"
+    return aff, f"{aff} schedulable cores"
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -110,8 +182,8 @@ def cpu_model() -> str:
 
 def cpu_baseline(tx, budget_s: float):
     """Oracle (C restatement of src/net/ip_checksum.cc, -O2) on a bounded
-    sample of the same frames, on this host's cores: threads = cores we may
-    use (capped at 16, the box's CPU share), plus the 1-thread rate."""
+    sample of the same frames, on this host's cores (cpu_threads), plus the
+    1-thread rate."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # cpu_baseline leg only
 
@@ -119,7 +191,7 @@ def cpu_baseline(tx, budget_s: float):
     host = tx.data[: n_sample * FRAME].cpu().numpy()
     off = np.arange(n_sample, dtype=np.uint64) * FRAME
     length = np.full(n_sample, FRAME, dtype=np.uint32)
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads, why = cpu_threads()
 
     def rate(nt, seconds):
         oracle.batch_ipv4(host, off, length, nthreads=nt)  # warm
@@ -140,6 +212,7 @@ def cpu_baseline(tx, budget_s: float):
         "value": round(vn, 3),
         "unit": "GiB/s",
         "cores": threads,
+        "cores_source": why,
         "kind": "port",
         "sample": f"{n_sample} x {FRAME} B IPv4/UDP frames ({n_sample * FRAME / 1e6:.0f} MB) from the same batch, "
                   f"IPv4 header + UDP checksum per frame, {rn} passes on {threads} threads "
@@ -149,28 +222,45 @@ def cpu_baseline(tx, budget_s: float):
     }
 
 
-def pmc_traffic(path: str | None, kernel_substr: str):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary (see
-    tools/pmc_summary.py); None when no summary exists."""
-    cands = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))
+def pmc_traffic(path: str | None, config: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
+    summary for this config (tools/pmc_summary.py: profiles/rNN_pmc_<config>.json);
+    None when no summary exists."""
+    cands = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", f"*pmc_{config}.json")))
     for p in reversed(cands):
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        k = d.get("kernels", {}).get(kernel_substr)
+        k = d.get("kernels", {}).get(kernel)
         if k and k.get("hbm_bytes_per_launch"):
             return float(k["hbm_bytes_per_launch"]), os.path.relpath(p, REPO)
     return None, None
 
 
-def timed(step, steps, warmup, world, stream, launches_per_step=1):
+class Launches:
+    """Counts this process's launches per kernel, so a line can name which
+    dispatches were timed (trace_select)."""
+
+    def __init__(self):
+        self.n = {}
+
+    def add(self, kernel: str, k: int = 1):
+        self.n[kernel] = self.n.get(kernel, 0) + k
+
+    def select(self, kernel: str, count: int) -> dict:
+        return {"kernel": kernel, "skip": self.n.get(kernel, 0), "count": count}
+
+
+LAUNCHES = Launches()
+
+
+def timed(step, steps, warmup, world, stream):
     """Warm up, then time `steps` calls bracketed by barrier + sync; returns
-    (max-over-ranks wall seconds, mean seconds per launch).  The launch mean
-    comes from ONE pair of HIP events around the timed launches on their
-    stream: an event between every two launches leaves the GPU idle ~5 us at
-    each (a timestamp packet), which the old per-launch events added to the
-    wall time (profiles/r01_kernel_stats_bench.csv gap analysis)."""
+    (max-over-ranks wall seconds, seconds per step from ONE pair of HIP events
+    around the timed launches on their stream).  An event between every two
+    launches leaves the GPU idle ~5 us at each (a timestamp packet), which
+    per-launch events would add to the wall time."""
     for k in range(warmup):
         step(k)
     torch.cuda.synchronize()
@@ -179,24 +269,110 @@ def timed(step, steps, warmup, world, stream, launches_per_step=1):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(stream)
-    for k in range(steps):
+    for k in range(warmup, warmup + steps):
         step(k)
     e1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()  # this rank's end, before the closing barrier's own latency
     barrier(world)
     wall = max_over_ranks(t1 - t0, world)
-    return wall, e0.elapsed_time(e1) / 1e3 / (steps * launches_per_step)
+    return wall, e0.elapsed_time(e1) / 1e3 / steps
 
 
-def line(metric, value, unit, args, world, wall, dtype, config, roofline=None, cpu=None, extra=None):
+def roofline(alg_bytes_launch: float, launch_s: float, config: str, kernel: str, sel: dict, args, extra=None):
+    traffic, src = pmc_traffic(args.pmc, config, "csum_flat_kernel")
+    achieved = alg_bytes_launch / launch_s / 1e9
+    d = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": src,
+         "alg_bytes_per_launch": int(alg_bytes_launch), "avg_launch_us": round(launch_s * 1e6, 2),
+         "trace_select": sel}
+    if extra:
+        d.update(extra)
+    return d
+
+
+def emit(metric, value, unit, args, world, wall, dtype, config, roof=None, cpu=None, extra=None):
     d = {"metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": world, "steps": args.steps,
          "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
          "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic", "config": config,
-         "roofline": roofline, "cpu_baseline": cpu}
+         "roofline": roof, "cpu_baseline": cpu}
     if extra:
         d.update(extra)
     print(json.dumps(d), flush=True)
+
+
+def read_ceiling(data, nbytes, stream, reps=10):
+    """Measured HBM read ceiling: the plain nt stream over the same bytes."""
+    sink = torch.zeros(native.load().sccsum_read_probe_blocks(), dtype=torch.int64, device=data.device)
+    for _ in range(3):
+        batch.read_probe(data, nbytes, sink=sink, stream=stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        batch.read_probe(data, nbytes, sink=sink, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return (nbytes & ~15) * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+
+
+def run_udp1500(args, world, rank, dev):
+    n = args.packets
+    # R distinct tx/rx batch pairs launched in turn: 2R x 1.5 GB per rank, so no
+    # launch finds its batch's lines left in the 256 MB MALL by an earlier one
+    # (a replay of one resident batch would measure cache reuse, not streaming)
+    R = max(1, args.rotate)
+    kern = flat_kernel(True, False, n, n * FRAME)
+    txs, rxs, sts = [], [], []
+    out_tx = torch.empty(2 * n, dtype=torch.int16, device=dev)
+    out_rx = torch.empty(2 * n, dtype=torch.int16, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED + rank)
+    bad = torch.randperm(n, device=dev, generator=g)[: n // 100]
+    for r in range(R):
+        tx = devsynth.udp_frames(n, FRAME, seed=SEED + 7919 * rank + 104723 * r, device=dev)
+        first = batch.ipv4_frames(tx, out2=out_tx)
+        LAUNCHES.add(kern)
+        rx = devsynth.store_checksums(tx, first)
+        devsynth.corrupt(rx, bad, byte=700)
+        txs.append(tx)
+        rxs.append(rx)
+        sts.append(torch.empty(n, dtype=torch.uint8, device=dev))
+    stream = torch.cuda.current_stream()
+
+    def step(k):
+        r = k % R
+        batch.ipv4_frames(txs[r], out2=out_tx, stream=stream)
+        batch.ipv4_frames(rxs[r], out2=out_rx, status=sts[r], stream=stream)
+
+    warm = max(args.warmup, R)
+    for k in range(warm):
+        step(k)
+    LAUNCHES.add(kern, 2 * warm)
+    torch.cuda.synchronize()
+    # sanity: every uncorrupted rx frame verifies, every corrupted one fails
+    for st_rx in sts:
+        n_fail = int(((st_rx & 2) == 0).sum())
+        assert n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
+    sel = LAUNCHES.select(kern, 2 * args.steps)
+    wall, step_s = timed(step, args.steps, 0, world, stream)
+    LAUNCHES.add(kern, 2 * args.steps)
+    avg_launch_s = step_s / 2
+
+    value = world * 2 * n * FRAME * args.steps / wall / 2**30
+    alg = n * (FRAME + META_BYTES + 4) + n // 2  # + status byte on the rx launch (avg)
+    ceiling = read_ceiling(txs[0].data, txs[0].bytes_len, stream)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(txs[0], args.cpu_seconds)
+    if rank == 0:
+        emit(METRIC, value, "GiB/s", args, world, wall, "u8",
+             {"workload": "cfg2: 1,048,576 x 1500 B IPv4/UDP frames per GPU in HBM (offset/length array); "
+                          "step = generate (IP+UDP csum) + verify (1% corrupted) pass",
+              "packets_per_gpu": n, "frame_bytes": FRAME,
+              "rotation": f"{R} distinct tx/rx batch pairs launched in turn ({2 * R * n * FRAME / 1e9:.1f} GB per GPU)",
+              "global_batch": n * world, "parallelism": f"{world} independent shards, no collective"},
+             roofline(alg, avg_launch_s, "udp1500", kern + " (sccsum_ipv4_frames)", sel, args,
+                      {"measured_read_ceiling_GBps": round(ceiling, 1)}), cpu)
 
 
 def run_tcp64k(args, world, rank, dev):
@@ -210,20 +386,25 @@ def run_tcp64k(args, world, rank, dev):
     batch.spans(b, seeds=seeds, out=out)  # generate
     devsynth.store_tcp_checksums(b, out)
     batch.spans(b, seeds=seeds, out=out, status=st)  # verify: every segment must pass
+    kern = flat_kernel(False, False, n, b.bytes_len)
+    LAUNCHES.add(kern, 2)
     torch.cuda.synchronize()
     assert int((st != 1).sum()) == 0, "tcp64k verify failed"
     stream = torch.cuda.current_stream()
+    LAUNCHES.add(kern, args.warmup)
+    sel = LAUNCHES.select(kern, args.steps)
     wall, launch_s = timed(lambda k: batch.spans(b, seeds=seeds, out=out, status=st, stream=stream),
                            args.steps, args.warmup, world, stream)
-    alg = n * (seg + 12 + 4 + 2 + 1)
+    alg = n * (seg + META_BYTES + 4 + 2 + 1)  # + seed in, result + status out
+    cbytes = min(b.bytes_len, 16 << 30)
+    ceiling = read_ceiling(b.data, cbytes, stream, reps=3)
     if rank == 0:
-        line("GiB/s device-resident Internet checksum, 64 KiB TCP segments (cfg 4)",
+        emit("GiB/s device-resident Internet checksum, 64 KiB TCP segments (cfg 4)",
              world * n * seg * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": "cfg4: 65536 B TCP segments + pseudo-header seed per segment, verify pass",
               "segments_per_gpu": n, "segment_bytes": seg, "parallelism": f"{world} independent shards"},
-             {"bound": "hbm", "achieved": round(alg / launch_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-              "frac": round(alg / launch_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-              "avg_launch_us": round(launch_s * 1e6, 2)})
+             roofline(alg, launch_s, "tcp64k", kern + " (sccsum_spans)", sel, args,
+                      {"measured_read_ceiling_GBps": round(ceiling, 1), "read_ceiling_bytes": cbytes}))
 
 
 def run_mixed(args, world, rank, dev):
@@ -237,29 +418,32 @@ def run_mixed(args, world, rank, dev):
     bs = [devsynth.mixed_frames(lens, seed=SEED + 31 * rank + 7 * r, device=dev) for r in range(R)]
     out = torch.empty(2 * n, dtype=torch.int16, device=dev)
     stream = torch.cuda.current_stream()
-    wall, launch_s = timed(lambda k: batch.ipv4_frames(bs[k % R], out2=out, stream=stream), args.steps,
-                           max(args.warmup, R), world, stream)
+    warm = max(args.warmup, R)
+    kern = flat_kernel(True, False, n, bs[0].bytes_len)
+    LAUNCHES.add(kern, warm)
+    sel = LAUNCHES.select(kern, args.steps)
+    wall, launch_s = timed(lambda k: batch.ipv4_frames(bs[k % R], out2=out, stream=stream), args.steps, warm, world,
+                           stream)
     total = int(lens.sum())
-    alg = total + n * (12 + 4)
+    alg = total + n * (META_BYTES + 4)
+    ceiling = read_ceiling(bs[0].data, bs[0].bytes_len, stream)
     if rank == 0:
-        line("GiB/s device-resident Internet checksum, mixed-MTU Zipf batches (cfg 3)",
+        emit("GiB/s device-resident Internet checksum, mixed-MTU Zipf batches (cfg 3)",
              world * total * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": "cfg3: Zipf(s=1.2) IPv4/UDP frames 64..9000 B, packed back to back (odd offsets)",
               "packets_per_gpu": n, "bytes_per_gpu": total, "mean_len": round(total / n, 1),
-              "rotation": f"{R} distinct batches launched in turn",
-              "parallelism": f"{world} independent shards"},
-             {"bound": "hbm", "achieved": round(alg / launch_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-              "frac": round(alg / launch_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-              "avg_launch_us": round(launch_s * 1e6, 2)})
+              "rotation": f"{R} distinct batches launched in turn", "parallelism": f"{world} independent shards"},
+             roofline(alg, launch_s, "mixed", kern + " (sccsum_ipv4_frames)", sel, args,
+                      {"measured_read_ceiling_GBps": round(ceiling, 1)}))
 
 
 def run_fill(args, world, rank, dev):
     """cfg 2 tx side with in-place write-back: IPv4 header +
-    UDP checksums generated and stored into the frames (wire-ready), every
-    step over the same 1 M x 1500 B batch (generate ignores the fields' old
-    contents, so repeated steps are identical work)."""
+    UDP checksums generated and stored into the frames (wire-ready), over R
+    rotated 1 M x 1500 B batches (generate ignores the fields' old contents,
+    so repeated steps are identical work)."""
     n = args.packets
-    R = max(1, args.rotate)  # distinct batches launched in turn (no cached-line replay)
+    R = max(1, args.rotate)
     bs = [devsynth.udp_frames(n, FRAME, seed=SEED + 7 * rank + 13 * r, device=dev) for r in range(R)]
     mode = native.FILL_IP | native.FILL_L4
     st = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -268,19 +452,84 @@ def run_fill(args, world, rank, dev):
         batch.ipv4_frames(b, status=st)
         torch.cuda.synchronize()
         assert args.no_check or int((st != 3).sum()) == 0, "filled frames do not verify"
+    kern = flat_kernel(True, True, n, n * FRAME)
+    LAUNCHES.add(kern, R)
     stream = torch.cuda.current_stream()
-    wall, launch_s = timed(lambda k: batch.ipv4_fill(bs[k % R], mode, stream=stream), args.steps,
-                           max(args.warmup, R), world, stream)
+    warm = max(args.warmup, R)
+    LAUNCHES.add(kern, warm)
+    sel = LAUNCHES.select(kern, args.steps)
+    wall, launch_s = timed(lambda k: batch.ipv4_fill(bs[k % R], mode, stream=stream), args.steps, warm, world, stream)
     alg = n * (FRAME + META_BYTES + 4)  # read every byte + metadata, write the two 2-byte fields
     if rank == 0:
-        line("GiB/s device-resident Internet checksum, 1500B-packet batches, in-place generate (cfg 2 tx)",
+        emit("GiB/s device-resident Internet checksum, 1500B-packet batches, in-place generate (cfg 2 tx)",
              world * n * FRAME * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": "cfg2 tx: 1500 B IPv4/UDP frames, IP + UDP checksums generated and stored in place",
               "packets_per_gpu": n, "rotation": f"{R} distinct batches launched in turn",
               "parallelism": f"{world} independent shards"},
-             {"bound": "hbm", "achieved": round(alg / launch_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-              "frac": round(alg / launch_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-              "avg_launch_us": round(launch_s * 1e6, 2)})
+             roofline(alg, launch_s, "fill", kern + " (sccsum_ipv4_fill)", sel, args))
+
+
+def run_sweep(args, world, rank, dev):
+    """Device-resident rate against batch size, at the reference's batch
+    boundaries: 32-packet DPDK rx bursts (src/net/dpdk.cc:2190-2204), <= 128-
+    packet tx refills (src/net/net.cc:81-105), the burst queue's 1 Ki / 16 Ki
+    batches, up to 1 M.  Each size launches back to back over distinct slices
+    of a 1.5 GB batch (no slice is reread while cached), eager and as one
+    captured HIP graph of the same launches."""
+    n_all = 1 << 20
+    big = devsynth.udp_frames(n_all, FRAME, seed=SEED + rank, device=dev)
+    sizes = [32, 128, 1024, 16384, 65536, 262144, 1048576]
+    stream = torch.cuda.Stream(device=dev)
+    res = []
+    for B in sizes:
+        nb = n_all // B
+        k = min(nb, max(8, (64 << 20) // (B * FRAME)))  # launches per timed pass: >= 64 MB or all slices
+        slices = [batch.PacketBatch(data=big.data[j * B * FRAME:], off=big.off[:B], length=big.length[:B],
+                                    bytes_len=B * FRAME, max_len=FRAME) for j in range(nb)]
+        out = torch.empty(2 * B, dtype=torch.int16, device=dev)
+        st = torch.empty(B, dtype=torch.uint8, device=dev)
+        for j in range(min(nb, 4)):
+            batch.ipv4_frames(slices[j], out2=out, status=st, stream=stream)
+        torch.cuda.synchronize()
+        # eager: k launches, rotating over the slices
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for j in range(k):
+            batch.ipv4_frames(slices[j % nb], out2=out, status=st, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        host_s = time.perf_counter() - t0
+        eager_s = e0.elapsed_time(e1) / 1e3 / k
+        # graph: the same k launches captured once, replayed
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for j in range(k):
+                batch.ipv4_frames(slices[j % nb], out2=out, status=st, stream=stream)
+        reps = 3
+        with torch.cuda.stream(stream):  # replay() launches on the current stream
+            g.replay()
+            torch.cuda.synchronize()
+            e0.record(stream)
+            for _ in range(reps):
+                g.replay()
+            e1.record(stream)
+        torch.cuda.synchronize()
+        graph_s = e0.elapsed_time(e1) / 1e3 / (reps * k)
+        bytes_b = B * FRAME
+        res.append({"packets": B, "bytes": bytes_b, "launches": k,
+                    "eager_us": round(eager_s * 1e6, 2), "eager_GiBps": round(bytes_b / eager_s / 2**30, 1),
+                    "eager_host_us_per_launch": round(host_s / k * 1e6, 2),
+                    "graph_us": round(graph_s * 1e6, 2), "graph_GiBps": round(bytes_b / graph_s / 2**30, 1),
+                    "graph_frac_of_8TBps": round(B * (FRAME + META_BYTES + 5) / graph_s / 1e9 / HBM_PEAK_GBPS, 4)})
+        del g, slices
+    if rank == 0:
+        best = res[-1]
+        emit("GiB/s device-resident Internet checksum vs batch size (1500 B frames, verify pass)",
+             best["graph_GiBps"] * world, "GiB/s", args, world, best["graph_us"] / 1e6 * args.steps, "u8",
+             {"workload": "sweep: 1500 B IPv4/UDP frames, one sccsum_ipv4_frames per batch, batch = "
+                          + "/".join(str(s) for s in sizes) + " packets",
+              "parallelism": f"{world} independent shards"}, extra={"sweep": res})
 
 
 def run_e2e(args, world, rank, dev):
@@ -321,142 +570,40 @@ def run_e2e(args, world, rank, dev):
                      "pcie_GBps_h2d_plus_d2h": round(pcie / t / 1e9, 2)}
     if rank == 0:
         best = max(res.values(), key=lambda r: r["GiBps_packet_bytes"])
-        line("GiB/s Internet checksum incl. PCIe: pinned mbuf-shaped host buffers -> HBM -> host (cfg 5)",
+        emit("GiB/s Internet checksum incl. PCIe: pinned mbuf-shaped host buffers -> HBM -> host (cfg 5)",
              world * best["GiBps_packet_bytes"], "GiB/s", args, world, best["ms_per_batch"] / 1e3 * args.steps, "u8",
              {"workload": "cfg5: 1,048,576 x 1500 B IPv4/UDP frames in 2304-B mbuf slots (pinned), "
                           "H2D + kernel + D2H of 4 B/frame, 3-deep pipeline, 64Ki-frame chunks",
               "parallelism": f"{world} independent shards"}, extra={"variants": res})
 
 
+def run_dry(args, world, rank):
+    """--dry-run: the multi-rank control plane without a device."""
+    import torch.distributed as dist
+
+    t0 = time.perf_counter()
+    barrier(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid(), "local": os.environ.get("LOCAL_RANK")})
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "ranks": ranks,
+                          "barrier_s": round(wall, 6)}), flush=True)
+
+
 def main():
     args = parse()
-    world, rank, local = dist_setup()
-    dev = torch.device("cuda", local)
-    if args.config != "udp1500":
-        {"tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e, "fill": run_fill}[args.config](args, world, rank, dev)
-        if world > 1:
-            import torch.distributed as dist
-
-            dist.destroy_process_group()
-        return
-    n = args.packets
-
-    # R distinct tx/rx batch pairs launched in turn: 2R x 1.5 GB per rank, so no
-    # launch finds its batch's lines left in the 256 MB MALL by an earlier one
-    # (a replay of one resident batch would measure cache reuse, not streaming)
-    R = max(1, args.rotate)
-    txs, rxs, sts = [], [], []
-    out_tx = torch.empty(2 * n, dtype=torch.int16, device=dev)
-    out_rx = torch.empty(2 * n, dtype=torch.int16, device=dev)
-    g = torch.Generator(device=dev)
-    g.manual_seed(SEED + rank)
-    bad = torch.randperm(n, device=dev, generator=g)[: n // 100]
-    for r in range(R):
-        tx = devsynth.udp_frames(n, FRAME, seed=SEED + 7919 * rank + 104723 * r, device=dev)
-        first = batch.ipv4_frames(tx, out2=out_tx)
-        rx = devsynth.store_checksums(tx, first)
-        devsynth.corrupt(rx, bad, byte=700)
-        txs.append(tx)
-        rxs.append(rx)
-        sts.append(torch.empty(n, dtype=torch.uint8, device=dev))
-    tx = txs[0]
-    torch.cuda.synchronize()
-
-    stream = torch.cuda.current_stream()
-
-    def step(k):
-        r = k % R
-        batch.ipv4_frames(txs[r], out2=out_tx, stream=stream)
-        batch.ipv4_frames(rxs[r], out2=out_rx, status=sts[r], stream=stream)
-
-    for k in range(max(args.warmup, R)):
-        step(k)
-    torch.cuda.synchronize()
-    # sanity: every uncorrupted rx frame verifies, every corrupted one fails
-    for st_rx in sts:
-        n_fail = int(((st_rx & 2) == 0).sum())
-        assert n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
-
-    # timed region: barrier + sync on both sides, one HIP event pair around the
-    # launches on their stream (see timed())
-    e_start, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e_start.record(stream)
-    for k in range(args.steps):
-        step(k)
-    e_end.record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0  # this rank's end, before the closing barrier's own latency
-    barrier(world)
-    wall_max = max_over_ranks(wall, world)
-    avg_launch_s = e_start.elapsed_time(e_end) / 1e3 / (2 * args.steps)
-
-    bytes_per_step = 2 * n * FRAME  # per rank
-    value = world * bytes_per_step * args.steps / wall_max / 2**30
-    alg_bytes_launch = n * (FRAME + META_BYTES + 4) + n // 2  # + status byte on the rx launch (avg)
-    achieved = alg_bytes_launch / avg_launch_s / 1e9
-
-    # measured HBM read ceiling with the same load shape over the tx bytes
-    sink = torch.zeros(native.load().sccsum_read_probe_blocks(), dtype=torch.int64, device=dev)
-    for _ in range(3):
-        batch.read_probe(tx.data, tx.bytes_len, sink=sink, stream=stream)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    reps = 10
-    for _ in range(reps):
-        batch.read_probe(tx.data, tx.bytes_len, sink=sink, stream=stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    ceiling = (tx.bytes_len & ~15) * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
-
-    traffic, traffic_src = pmc_traffic(args.pmc, "csum_flat_kernel")
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(tx, args.cpu_seconds)
-
-    if rank == 0:
-        line = {
-            "metric": METRIC,
-            "value": round(value, 3),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic",
-            "config": {
-                "workload": "cfg2: 1,048,576 x 1500 B IPv4/UDP frames per GPU in HBM (offset/length array); "
-                            "step = generate (IP+UDP csum) + verify (1% corrupted) pass",
-                "packets_per_gpu": n,
-                "frame_bytes": FRAME,
-                "rotation": f"{R} distinct tx/rx batch pairs launched in turn ({2 * R * n * FRAME / 1e9:.1f} GB per GPU)",
-                "global_batch": n * world,
-                "parallelism": f"{world} independent shards, no collective",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "csum_flat_kernel<16,true,false,false,nt> (sccsum_ipv4_frames)",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "alg_bytes_per_launch": alg_bytes_launch,
-                "avg_launch_us": round(avg_launch_s * 1e6, 2),
-                "measured_read_ceiling_GBps": round(ceiling, 1),
-            },
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    _imports()
+    world, rank, local = dist_setup(args.dry_run)
+    if args.dry_run:
+        run_dry(args, world, rank)
+    else:
+        dev = torch.device("cuda", local)
+        {"udp1500": run_udp1500, "tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e, "fill": run_fill,
+         "sweep": run_sweep}[args.config](args, world, rank, dev)
     if world > 1:
         import torch.distributed as dist
 

@@ -40,10 +40,13 @@
  *   - d_bytes must be 16-byte aligned, d_off 8-byte aligned, d_len/d_seed/d_out2 4-byte aligned,
  *     d_out 2-byte aligned.
  *   - Launches are asynchronous on `stream` (a hipStream_t; NULL = the
- *     device's null stream), one kernel each.  No allocation, no host
- *     synchronisation: the calls are safe inside hipStreamBeginCapture.  At
- *     most 256 launches may be in flight per device at once (the ring of tile
- *     counters they dequeue from).
+ *     device's null stream), one kernel each.  No allocation on the launch
+ *     path (a stream's first launch may allocate its 16 KiB of tile
+ *     counters once), no host synchronisation: the calls are safe inside
+ *     hipStreamBeginCapture.  Any number of launches may be in flight: each
+ *     stream has its own tile counters (launches on one stream run in order);
+ *     captured launches, and streams beyond the first 4096 of a device, use a
+ *     static tile order instead (same results).
  *
  * Threading: one host thread per device (Seastar's shard-per-core model).
  * Calls are re-entrant per stream.
@@ -81,10 +84,10 @@ const char* sccsum_strerror(int err);
 int sccsum_device_count(int* count);
 
 /* Bind the calling host thread to `device` (hipSetDevice), cache its
- * compute-unit count for launch sizing and allocate (once per device) the
- * small ring of tile counters the batch kernel dequeues from.  Call it on
- * every thread that launches; launches made without it fall back to static
- * tile order. */
+ * compute-unit count for launch sizing and enable the per-stream tile
+ * counters the flat kernel dequeues from.  Call it on every thread that
+ * launches; launches on a device nobody initialised use the static tile
+ * order (same results). */
 int sccsum_init(int device);
 
 /* Pseudo-header partial sum exactly as ipv4_traits::*_pseudo_header_checksum
@@ -194,57 +197,8 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len,
                      uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len,
                      uint32_t mode, void* stream);
 
-/* Diagnostic: select the kernel family for later launches in this process.
- * 0 = default: flat kernel, 16 (>= 512 Ki packets and >= 256 MiB) else 15.
- * 1 = one packet per wave, per-lane byte masks (independent second
- *     implementation, kept for cross-checking).
- * 2-9 = batch kernel (round-1 default before the flat kernel): one packet per
- *     pass; 3 = next packet in flight, 4 / 5 = 2 / 3 with default-policy
- *     loads, 6 / 7 = 2 / 3 with each packet's last 128-byte line
- *     default-policy, 8 / 9 = 2 / 6 with short packets sharing passes.
- * 10-16 = flat kernel: each tile's byte extent streamed densely, unit sums
- *     prefix-scanned across the wave; U = 2 (10, 11), 4 (12, 13), 8 (14, 15),
- *     16 (16) units per lane per chunk, odd = next chunk in flight.
- * All variants produce identical results; the knob exists for in-process A/B
- * timing and cross-checking.  SCCSUM_EINVAL for an unknown one. */
-int sccsum_set_kernel_variant(int variant);
-
-/* Diagnostic: cap the launch grid at `blocks` 256-thread workgroups per
- * compute unit (default 8 = 32 waves/CU).  Occupancy A/B knob; results are
- * unaffected.  Returns SCCSUM_EINVAL outside 1..32. */
-int sccsum_set_blocks_per_cu(int blocks);
-
-/* Diagnostic: force U, the 16-byte units each lane loads per step of a packet
- * (1, 2, 4 or 8; 0 = choose from max_len).  Results are unaffected. */
-int sccsum_set_group_units(int units);
-
-/* Diagnostic: cap the batch kernel's tile (packets a wave plans at once) at
- * 1..64 (default 64).  Results are unaffected. */
-int sccsum_set_tile_packets(int packets);
-
-/* Diagnostic: target bytes per flat-kernel tile (variants 10-16; default
- * 0 = only the packet cap).  Results are unaffected. */
-int sccsum_set_tile_bytes(int bytes);
-
-/* Diagnostic: the flat kernel's guided tail — the last tiles hold
- * B / divisor packets and cover about per_slot such tiles per wave slot
- * (default 1 = uniform tiles, 4).  Results are unaffected. */
-int sccsum_set_tail_tiles(int divisor, int per_slot);
-
-/* Diagnostic: batch-kernel tiles dequeued from per-XCD counters (1, the
- * default) or dealt round robin (0).  Results are unaffected. */
-int sccsum_set_dynamic_tiles(int on);
-
 /* Wait for all work queued on `stream`. */
 int sccsum_sync(void* stream);
-
-/* Diagnostic: stream-read `bytes` (multiple of 16) from d_src with the same
- * load width as the checksum kernels and write one 64-bit word per workgroup
- * to d_sink (capacity >= sccsum_read_probe_blocks()).  Used by bench.py as
- * the measured HBM read ceiling. */
-int sccsum_read_probe(const void* d_src, uint64_t bytes, uint64_t* d_sink, void* stream);
-int sccsum_read_probe_blocks(void);
-
 
 /* ---------------------------------------------------------------------------
  * Host pipeline: batches that live in HOST memory (DPDK mbuf pools, socket
@@ -304,10 +258,14 @@ typedef struct sccsum_burst sccsum_burst;
 /* Completion, called from sccsum_burst_poll / _drain on the caller's thread:
  * the packets with tickets first_ticket .. first_ticket + count - 1, in submit
  * order; results / status point into the queue's pinned memory, valid until
- * the callback returns. */
+ * the callback returns.  The callback may submit (a queue never reuses the
+ * batch being delivered before the callback returns); poll, drain and
+ * destroy called from inside it return SCCSUM_EINVAL and do nothing. */
 typedef void (*sccsum_burst_done_fn)(void* user, uint64_t first_ticket, uint32_t count, const uint16_t* results,
                                      const uint8_t* status);
 
+/* batch_bytes: 64 .. 4 GiB - 16 (a batch's byte offsets are 32-bit);
+ * depth: 1 .. 64 slots.  SCCSUM_EINVAL otherwise. */
 int sccsum_burst_create(int device, int mode, uint64_t batch_bytes, uint32_t batch_packets, uint64_t max_delay_ns,
                         int depth, sccsum_burst_done_fn fn, void* user, sccsum_burst** out);
 
@@ -339,7 +297,10 @@ int sccsum_burst_submit_mapped(sccsum_burst* b, const sccsum_fragment* frags, ui
                                uint64_t* ticket);
 
 /* Reactor poller: launch the open batch if full or aged; deliver every
- * finished batch.  *did_work (may be NULL) = 1 when it launched or delivered. */
+ * finished batch.  *did_work (may be NULL) = 1 when it launched or delivered.
+ * If a launch fails (an error code from any call that launches: submit, poll,
+ * drain), its batch stays staged, nothing of it still runs on the device, and
+ * the next poll / drain launches it again. */
 int sccsum_burst_poll(sccsum_burst* b, int* did_work);
 
 /* Launch what is staged, wait for every batch in flight, deliver them all. */

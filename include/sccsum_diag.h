@@ -1,0 +1,67 @@
+/*
+ * sccsum_diag.h — DIAGNOSTIC knobs of libsccsum (A/B timing, cross-checks,
+ * bench's read ceiling).  Not part of the production boundary in sccsum.h:
+ * nothing a caller of the checksum API needs is here.  Every knob applies to
+ * launches made later by the CALLING HOST THREAD only (thread-local), so one
+ * shard's experiment never changes another thread's launches.  Results never
+ * depend on a knob: every setting computes the same bits.
+ */
+#ifndef SCCSUM_DIAG_H
+#define SCCSUM_DIAG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Kernel family for this thread's later launches.
+ * 0 = default: flat kernel, form 16 (>= 512 Ki packets and >= 256 MiB) else 15.
+ * 1 = one packet per wave, per-lane byte masks (an independent second
+ *     implementation kept for cross-checking; in-place fill uses the flat
+ *     kernel whatever the variant).
+ * 10-16 = flat kernel forms: each tile's byte extent streamed densely, unit
+ *     sums prefix-scanned across the wave; U = 2 (10, 11), 4 (12, 13),
+ *     8 (14, 15), 16 (16) units per lane per chunk, odd = next chunk in flight.
+ * 17-19 = flat kernel with rolling rows: U = 8 / 12 / 16 rows of 64 units
+ *     in flight, each pair of rows scanned as it lands and its registers
+ *     reloaded with the next chunk's rows at once (A/B: slower than 16 on
+ *     1500 B frames, profiles/r02g_ab_roll.log).
+ * SCCSUM_EINVAL for anything else. */
+int sccsum_set_kernel_variant(int variant);
+
+/* Cap the launch grid at `blocks` 256-thread workgroups per compute unit
+ * (default 8).  SCCSUM_EINVAL outside 1..32. */
+int sccsum_set_blocks_per_cu(int blocks);
+
+/* Simple kernel (variant 1): force U, the 16-byte units each lane loads per
+ * step (1, 2, 4 or 8; 0 = choose from max_len). */
+int sccsum_set_group_units(int units);
+
+/* Flat kernel: cap a tile (packets a wave plans at once) at 1..64 (default 64). */
+int sccsum_set_tile_packets(int packets);
+
+/* Flat kernel: target bytes per tile (default 0 = only the packet cap). */
+int sccsum_set_tile_bytes(int bytes);
+
+/* Flat kernel guided tail: the last tiles hold B / divisor packets and cover
+ * about per_slot such tiles per wave slot (default 1 = uniform tiles, 4). */
+int sccsum_set_tail_tiles(int divisor, int per_slot);
+
+/* Flat kernel: tiles dequeued from per-stream counters (1, the default) or
+ * dealt round robin (0). */
+int sccsum_set_dynamic_tiles(int on);
+
+/* Stream-read `bytes` (multiple of 16) from d_src with the same
+ * load width as the checksum kernels and write one 64-bit word per workgroup
+ * to d_sink (capacity >= sccsum_read_probe_blocks()).  Used by bench.py as
+ * the measured HBM read ceiling. */
+int sccsum_read_probe(const void* d_src, uint64_t bytes, uint64_t* d_sink, void* stream);
+int sccsum_read_probe_blocks(void);
+
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SCCSUM_DIAG_H */

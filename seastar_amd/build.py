@@ -26,7 +26,8 @@ def hipcc_cmd(out: str = LIB_PATH) -> list[str]:
 
 def build(force: bool = False, verbose: bool = True) -> str:
     os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
-    newest = max(os.path.getmtime(p) for p in SOURCES + [os.path.join(REPO_DIR, "include", "sccsum.h")])
+    headers = [os.path.join(REPO_DIR, "include", h) for h in ("sccsum.h", "sccsum_diag.h")]
+    newest = max(os.path.getmtime(p) for p in SOURCES + headers)
     if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= newest:
         return LIB_PATH
     cmd = hipcc_cmd()

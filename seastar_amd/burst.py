@@ -10,7 +10,7 @@ import ctypes
 
 import numpy as np
 
-from . import native
+from . import native, pipeline
 
 DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                            ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(ctypes.c_uint8))
@@ -33,6 +33,7 @@ class BurstQueue:
         self.status: dict[int, int] = {}
         self.batches = 0
         self._user = on_done
+        self._held: dict[int, list] = {}  # mapped submits: fragment arrays kept alive until completion
         self._cb = DONE_FN(self._done)  # lives as long as the queue
         h = ctypes.c_void_p()
         native.check(self._lib.sccsum_burst_create(device, mode, batch_bytes, batch_packets, max_delay_ns, depth,
@@ -46,6 +47,8 @@ class BurstQueue:
         if self.width == 2:
             r = r.reshape(count, 2)
         self.batches += 1
+        for k in range(count):
+            self._held.pop(first + k, None)
         if self._user is not None:
             self._user(int(first), r, s)
             return
@@ -61,8 +64,15 @@ class BurstQueue:
         memory (pipeline.pinned_empty) and stay untouched until completion."""
         bufs = [np.ascontiguousarray(np.frombuffer(f, np.uint8) if isinstance(f, (bytes, bytearray)) else f,
                                      dtype=np.uint8) for f in fragments]
-        if mapped and not all(isinstance(f, np.ndarray) and f.flags.c_contiguous for f in fragments):
-            raise ValueError("mapped fragments must be contiguous views of pinned memory")
+        if mapped:
+            # the device reads these bytes at their host address: they must be
+            # contiguous views of a live pinned block (pipeline.pinned_empty);
+            # pageable memory would fault the GPU
+            for f in fragments:
+                if not (isinstance(f, np.ndarray) and f.dtype == np.uint8 and f.flags.c_contiguous):
+                    raise ValueError("mapped fragments must be contiguous uint8 views of pinned memory")
+                if not pipeline.is_pinned(f):
+                    raise ValueError("mapped fragments must lie in pinned memory (pipeline.pinned_empty)")
         frags = (native.Fragment * max(len(bufs), 1))()
         for j, b in enumerate(bufs):
             frags[j].base = b.ctypes.data if b.size else None
@@ -73,6 +83,8 @@ class BurstQueue:
         if code == native.SCCSUM_EBUSY:
             return None
         native.check(code, "sccsum_burst_submit")
+        if mapped:
+            self._held[ticket.value] = bufs
         return ticket.value
 
     def poll(self) -> bool:

@@ -40,7 +40,7 @@
 #include "sccsum.h"
 
 struct sccsum_burst {
-    enum class state { free, open, inflight };
+    enum class state { free, open, inflight, delivering };
     struct Slot {
         state st = state::free;
         hipStream_t stream = nullptr;
@@ -76,6 +76,7 @@ struct sccsum_burst {
     size_t next_deliver = 0;
     uint64_t next_ticket = 0;
     uint64_t inflight = 0;
+    bool in_callback = false;  // a completion callback is running (poll / drain / destroy refuse)
 };
 
 namespace {
@@ -113,8 +114,19 @@ uint64_t stage_bytes(const sccsum_burst* b) {
 }
 
 // One H2D (packets + metadata packed behind them), the kernel, one D2H
-// (results + status), an event: 4 stream operations per batch.
+// (results + status), an event: 4 stream operations per batch.  On failure
+// the slot is left exactly as before the call (still open, its packets
+// staged) once whatever part of the batch reached the stream has finished,
+// so a later poll / drain retries the launch.
+int launch_slot_ops(sccsum_burst* b, sccsum_burst::Slot& s);
+
 int launch_slot(sccsum_burst* b, sccsum_burst::Slot& s) {
+    const int rc = launch_slot_ops(b, s);
+    if (rc != SCCSUM_OK) (void)hipStreamSynchronize(s.stream);
+    return rc;
+}
+
+int launch_slot_ops(sccsum_burst* b, sccsum_burst::Slot& s) {
     SCCSUM_TRY(hipSetDevice(b->device));
     const hipStream_t st = s.stream;
     const uint64_t n = s.npk;
@@ -165,16 +177,23 @@ int deliver(sccsum_burst* b, bool wait, bool* did) {
             if (q == hipErrorNotReady) break;
             SCCSUM_TRY(q);
         }
-        b->fn(b->user, s.first_ticket, s.npk, reinterpret_cast<const uint16_t*>(s.h_res),
-              s.h_res + 2 * width(b) * s.npk);
-        s.st = sccsum_burst::state::free;
+        // bookkeeping first, so the queue is consistent whatever the callback
+        // does; the slot stays out of use (its results are what the callback
+        // reads) until the callback returns
+        const uint64_t first = s.first_ticket;
+        const uint32_t npk = s.npk;
+        s.st = sccsum_burst::state::delivering;
+        --b->inflight;
+        b->next_deliver = (b->next_deliver + 1) % b->slots.size();
+        b->in_callback = true;
+        b->fn(b->user, first, npk, reinterpret_cast<const uint16_t*>(s.h_res), s.h_res + 2 * width(b) * npk);
+        b->in_callback = false;
         s.used = 0;
         s.npk = 0;
         s.ndesc = 0;
         s.copied = false;
         s.max_len = 0;
-        --b->inflight;
-        b->next_deliver = (b->next_deliver + 1) % b->slots.size();
+        s.st = sccsum_burst::state::free;
         *did = true;
     }
     return SCCSUM_OK;
@@ -186,8 +205,9 @@ extern "C" {
 
 int sccsum_burst_create(int device, int mode, uint64_t batch_bytes, uint32_t batch_packets, uint64_t max_delay_ns,
                         int depth, sccsum_burst_done_fn fn, void* user, sccsum_burst** out) {
+    // batch offsets travel as 32-bit gather destinations (sccsum_gather_desc)
     if (!out || !fn || (mode != SCCSUM_PIPE_SPANS && mode != SCCSUM_PIPE_IPV4) || batch_bytes < 64 ||
-        batch_packets < 1 || depth < 1 || depth > 64) {
+        batch_bytes > (UINT32_MAX & ~uint64_t(15)) || batch_packets < 1 || depth < 1 || depth > 64) {
         return SCCSUM_EINVAL;
     }
     *out = nullptr;
@@ -299,7 +319,7 @@ int sccsum_burst_submit_mapped(sccsum_burst* b, const sccsum_fragment* frags, ui
 }
 
 int sccsum_burst_poll(sccsum_burst* b, int* did_work) {
-    if (!b) return SCCSUM_EINVAL;
+    if (!b || b->in_callback) return SCCSUM_EINVAL;
     SCCSUM_TRY(hipSetDevice(b->device));
     bool did = false;
     if (b->open != SIZE_MAX) {
@@ -319,7 +339,7 @@ int sccsum_burst_poll(sccsum_burst* b, int* did_work) {
 }
 
 int sccsum_burst_drain(sccsum_burst* b) {
-    if (!b) return SCCSUM_EINVAL;
+    if (!b || b->in_callback) return SCCSUM_EINVAL;
     SCCSUM_TRY(hipSetDevice(b->device));
     if (b->open != SIZE_MAX) {
         auto& s = b->slots[b->open];
@@ -337,6 +357,7 @@ int sccsum_burst_drain(sccsum_burst* b) {
 
 int sccsum_burst_destroy(sccsum_burst* b) {
     if (!b) return SCCSUM_OK;
+    if (b->in_callback) return SCCSUM_EINVAL;
     (void)hipSetDevice(b->device);
     for (auto& s : b->slots) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);

@@ -11,25 +11,29 @@
 // reorder and widen freely — it loads aligned 16-byte units.
 //
 // Layout: packets live anywhere inside one byte buffer behind an
-// offset (u64) / length (u32) array.  Default kernel (csum_batch_kernel): a
-// wavefront takes a tile of up to 64 packets, plans them one per lane, then
-// streams them one packet at a time — every lane loads 16-byte units of the
-// packet through a raw buffer descriptor sized to the packet's unit span
-// (lanes past it read zeros, no per-lane masking), sums them with v_sad_u16,
-// folds the 64 lanes with DPP row ops + 4 readlanes — and finally each lane
-// finishes one packet (edge-byte correction from units stashed in LDS, IPv4
-// header decode, pseudo-header, complement) with one coalesced store per
-// tile.  No MFMA: a byte reduction at the HBM read roofline.
-// csum_kernel is a deliberately plain second implementation (one packet per
-// wave, per-lane byte masks) kept for cross-checking.
+// offset (u64) / length (u32) array.  Default kernel (csum_flat_kernel): a
+// wavefront takes a tile of up to 64 packets (one per lane), splits it into
+// runs of packets that lie forward in memory, streams each run's 16-byte units
+// densely through one raw buffer descriptor (nt loads), sums every unit with
+// v_sad_u16, prefix-scans the unit sums across the wave (DPP) and lets each
+// packet lane pick up the two prefix values that bound its units; each lane
+// then finishes its packet (edge-byte correction, IPv4 header decode,
+// pseudo-header, complement) with one coalesced store per tile.  No MFMA: a
+// byte reduction at the HBM read roofline.  csum_kernel is a deliberately
+// plain second implementation (one packet per wave, per-lane byte masks) kept
+// for cross-checking.
 
 #include <hip/hip_runtime.h>
 
 #include <atomic>
 #include <cstdint>
+#include <mutex>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "sccsum.h"
+#include "sccsum_diag.h"
 
 namespace sccsum {
 namespace {
@@ -235,7 +239,7 @@ __global__ __launch_bounds__(kBlock) void csum_kernel(
     }
 }
 
-// ---------------------------------------------------------------- batch-kernel helpers
+// ---------------------------------------------------------------- flat-kernel helpers
 
 // Keep bytes [lo, hi) of a 64-bit half unit (half-relative byte indices).
 __device__ __forceinline__ uint64_t keep_half(uint64_t q, int lo, int hi) {
@@ -281,44 +285,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* base, uint
     return __builtin_amdgcn_make_buffer_rsrc(p, static_cast<short>(0), static_cast<int>(nb), kRsrcFlags);
 }
 
-// ---------------------------------------------------------------- batch kernel (default)
-
-// Put a wave-uniform value into lane `k` of `v` (compare + select; gfx9's
-// v_writelane cannot read both a value and a lane select from SGPRs).
-__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t value, uint32_t k, uint32_t lane) {
-    return lane == k ? value : v;
-}
-
 // Sum of the bytes [lo, hi) of a 16-byte unit as little-endian 16-bit words
 // at their unit-relative positions (sad4 of the masked unit).
 __device__ __forceinline__ uint32_t unit_part(const u32x4& v, int lo, int hi) {
     return sad4_masked(v, lo, hi, 0u);
 }
 
-constexpr uint32_t kStashHead = 4;      // frames: units 0..3 (IPv4 header + the TCP/UDP checksum field)
-constexpr uint32_t kStashLast = 64;     // byte offset of the packet's last unit in its row
-constexpr uint32_t kStashUnits = 5;     // head units + the last unit
-constexpr uint32_t kStashStride = 80;   // bytes per packet row (5 x 16 B: conflict-free ds_read_b128)
 constexpr uint32_t kExactMax = 131072;  // fast path keeps exact 32-bit sums up to this length
+#ifndef SCCSUM_FILL_WHOLE
+#define SCCSUM_FILL_WHOLE 1  // in-place fill: store whole 16-byte units where safe (else the field bytes alone)
+#endif
 // tile-head counters: each on its own 256-byte line (atomics to one line
 // serialise at the memory side: ~12 ns each chip-wide)
 constexpr uint32_t kHeadStride = 64;                      // uint32 words between counters
 constexpr uint32_t kGroups = 64;                            // tile-dequeue counters per launch
 constexpr uint32_t kHeadSlotWords = kGroups * kHeadStride;  // one launch's counters
-#ifndef SCCSUM_LONG_GROUPS
-#define SCCSUM_LONG_GROUPS 3
-#endif
-constexpr int kLongGroups = SCCSUM_LONG_GROUPS;  // groups in flight per step of a long packet
-#ifndef SCCSUM_BATCH_MIN_WAVES
-#define SCCSUM_BATCH_MIN_WAVES 1  // __launch_bounds__ waves per SIMD floor (8 = cap VGPRs at 64)
-#endif
-#ifndef SCCSUM_FILL_MIN_WAVES
-#define SCCSUM_FILL_MIN_WAVES SCCSUM_BATCH_MIN_WAVES
-#endif
-static_assert(kStashStride >= 16 * kStashUnits && kStashStride % 16 == 0, "stash row layout");
 
 // Exact folded sum (little-endian domain relative to a0) of [rs, re), one
-// wave, any length: the slow path for packets the batch pass cannot take.
+// wave, any length: the slow path for packets the flat pass cannot take.
 __device__ uint32_t exact_range_sum(const uint8_t* a0, uint64_t rs, uint64_t re, uint32_t lane) {
     uint64_t acc = 0;
     if (re > rs) {
@@ -335,426 +319,6 @@ __device__ uint32_t exact_range_sum(const uint8_t* a0, uint64_t rs, uint64_t re,
         }
     }
     return fold16(wave_sum(fold16(acc)));
-}
-
-// Batch kernel.  Wave w owns tiles t = w, w + W, ... of B consecutive packets.
-//  A: lane i takes packet i of the tile: offset, length, seed, unit span.
-//  B: per packet (wave-uniform loop): 3 readlanes, one raw buffer descriptor
-//     sized to the packet's 16-byte unit span (lanes past it read zeros),
-//     unmasked v_sad_u16 sums, DPP row sums + 4 readlanes -> exact 32-bit
-//     sum written into lane k; units 0..2 and the last unit are stashed in LDS.
-//  C: lane i finishes packet i: subtracts the stashed bytes outside the
-//     summed range, decodes the IPv4 header (frames), folds, adds the seed or
-//     pseudo-header, complements; one coalesced store for the tile.
-//  D: packets the fast path cannot take (frames with options or a trimmed
-//     IP length, spans longer than 128 KiB) are redone exactly, one wave each.
-template <int U, bool IPV4, bool PIPE, int AUX, bool HYB, bool MULTI, bool FILL = false>
-__global__ __launch_bounds__(kBlock, FILL ? SCCSUM_FILL_MIN_WAVES : SCCSUM_BATCH_MIN_WAVES) void csum_batch_kernel(
-    const uint8_t* __restrict__ bytes, uint64_t bytes_len,
-    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
-    const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
-    uint8_t* __restrict__ status, uint64_t n, uint32_t B, uint32_t* __restrict__ heads, uint32_t flags) {
-    const bool raw = !IPV4 && (flags & kFlagRaw);
-    static_assert(!FILL || IPV4, "in-place generate is a frames mode");
-    constexpr bool fill = FILL;                          // generate L4 checksums and store them in place
-    const bool fill_ip = FILL && (flags & kFlagFillIp);  // ... and the IPv4 header checksum
-    __shared__ __attribute__((aligned(16))) uint8_t stash_all[kWavesPerBlock][kWave * kStashStride];
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    uint8_t* stash = stash_all[wv];
-    const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
-    const uint64_t ntiles = (n + B - 1) / B;
-    const bool has_seed = !IPV4 && seed != nullptr;
-    const uint32_t vo = 16u * lane;  // this lane's byte offset inside a 1 KiB slice
-
-    // Tile order.  Wave w first takes tile w (static: no start-up contention).
-    // With `heads`, the remaining tiles [W, ntiles) are split over kGroups
-    // counters (each on its own line) and dequeued: wave w pulls
-    // tile W + g + kGroups * atomicAdd(heads[g], 1) with g = w % kGroups, so
-    // waves that drew short tiles take more (Zipf batches).  Each group's
-    // dequeue count is known — one per remaining tile of the group plus one
-    // failing dequeue per wave of the group — so the wave that draws the last
-    // number zeroes the counter for the next launch on this slot (no memset,
-    // graph-replay safe).  Without `heads`: static round robin.
-    const uint64_t wglob = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
-    const uint32_t grp = static_cast<uint32_t>(wglob % kGroups);
-    const uint64_t rest = ntiles > nwaves ? ntiles - nwaves : 0;
-    const uint32_t tiles_g = rest > grp ? static_cast<uint32_t>((rest - grp + kGroups - 1) / kGroups) : 0u;
-    const uint32_t waves_g = static_cast<uint32_t>(nwaves / kGroups);  // host keeps nwaves % kGroups == 0
-    auto next_tile = [&](uint64_t prev) -> uint64_t {
-        if (heads == nullptr) return prev + nwaves;
-        uint32_t d = 0;
-        if (lane == 0) {
-            uint32_t* h = heads + grp * kHeadStride;
-            d = __hip_atomic_fetch_add(h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (d == tiles_g + waves_g - 1) __hip_atomic_store(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        d = __builtin_amdgcn_readfirstlane(d);
-        return d < tiles_g ? nwaves + grp + static_cast<uint64_t>(kGroups) * d : ntiles;
-    };
-    // the next tile is dequeued when a tile starts, so the atomic's round trip
-    // hides under the tile's loads; a wave stops after its one failing dequeue
-    uint64_t t = wglob;
-    if (t >= ntiles && heads != nullptr) t = next_tile(t);
-    while (t < ntiles) {
-        const uint64_t t_next = next_tile(t);
-        // ---- A: per-lane packet plan
-        const uint64_t base = t * B;
-        const uint64_t left = n - base;
-        const uint32_t cnt = left < B ? static_cast<uint32_t>(left) : B;
-        const bool mine = lane < cnt;
-        const uint64_t q = base + (mine ? lane : 0);
-        const uint64_t o = off[q];
-        const uint32_t L = mine ? len[q] : 0u;
-        const uint32_t sd = has_seed ? seed[q] : 0u;
-        const bool range_bad = o > bytes_len || L > bytes_len - o;
-        const bool short_frame = IPV4 && L < 20;
-        const bool huge = L > kExactMax;
-        const uint8_t* ptr = bytes + (range_bad ? 0 : o);
-        const uint32_t head = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ptr) & 15u);
-        const uint64_t a0 = reinterpret_cast<uint64_t>(ptr - head);
-        const bool fast = mine && !range_bad && !short_frame && !huge;
-        const uint32_t nunits = (fast && L) ? (head + L + 15u) >> 4 : 0u;
-
-        // ---- B: one packet at a time
-        // HYB: the units of the packet's last 128-byte line (shared with the
-        // next packet when packets are packed back to back) are loaded with
-        // the default cache policy so the next packet's first line hits in
-        // L2; all other units stream nontemporally.
-        uint32_t res = 0;
-        struct PktLoad {
-            __amdgpu_buffer_rsrc_t r;  // units [0, s)
-            uint32_t nu, s;
-            u32x4 v[U];
-            u32x4 w;  // HYB: lane i <- unit s + i of the last line (i < 8)
-        };
-        auto issue = [&](uint32_t k, bool valid, PktLoad& P) {
-            P.nu = valid ? __builtin_amdgcn_readlane(nunits, k) : 0u;
-            const uint32_t alo = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0), k);
-            const uint32_t ahi = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0 >> 32), k);
-            const uint8_t* pa = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(ahi) << 32) | alo);
-            if (HYB) {
-                const uint32_t f = (alo >> 4) & 7u;  // first unit's slot in its 128-byte line
-                const uint32_t ls = P.nu ? ((f + P.nu - 1) & ~7u) : 0u;
-                P.s = ls > f ? ls - f : 0u;
-                const auto rw = rsrc(pa + 16u * P.s, 16u * (P.nu - P.s));
-                P.w = __builtin_amdgcn_raw_buffer_load_b128(rw, static_cast<int>(vo), 0, 0);
-            } else {
-                P.s = P.nu;
-                P.w = u32x4{0, 0, 0, 0};
-            }
-            P.r = rsrc(pa, 16u * P.s);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                P.v[u] = __builtin_amdgcn_raw_buffer_load_b128(P.r, static_cast<int>(vo + 1024u * u), 0, AUX);
-        };
-        auto body = [&](uint32_t k, PktLoad& P) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int u = 0; u < U; ++u) acc = sad4(P.v[u], acc);
-            if (HYB) acc = sad4(P.w, acc);
-            uint8_t* row = stash + k * kStashStride;
-            constexpr uint32_t kHead = FILL ? kStashHead : (IPV4 ? 3u : 1u);
-            if (lane < kHead && lane < P.s) *reinterpret_cast<u32x4*>(row + 16u * lane) = P.v[0];
-            if (HYB && lane + P.s < kHead) *reinterpret_cast<u32x4*>(row + 16u * (lane + P.s)) = P.w;
-            const uint32_t gu = static_cast<uint32_t>(U) * kWave;
-            uint32_t g = gu;
-            // long packets: kLongGroups groups of loads in flight per step;
-            // the final group always goes through the single-group loop below
-            // so P.v ends up holding it (tail stash)
-            constexpr int kLG = (PIPE || MULTI) ? 2 : kLongGroups;  // leave registers for the second load set / shared passes
-            for (; g + kLG * gu < P.s; g += kLG * gu) {
-                u32x4 w[kLG][U];
-#pragma unroll
-                for (int q = 0; q < kLG; ++q)
-#pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        w[q][u] = __builtin_amdgcn_raw_buffer_load_b128(
-                            P.r, static_cast<int>(16u * (g + q * gu) + vo + 1024u * u), 0, AUX);
-#pragma unroll
-                for (int q = 0; q < kLG; ++q)
-#pragma unroll
-                    for (int u = 0; u < U; ++u) acc = sad4(w[q][u], acc);
-            }
-            for (; g < P.s; g += gu) {
-                u32x4 w[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    w[u] = __builtin_amdgcn_raw_buffer_load_b128(P.r, static_cast<int>(16u * g + vo + 1024u * u), 0,
-                                                                 AUX);
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    acc = sad4(w[u], acc);
-                    P.v[u] = w[u];
-                }
-            }
-            // last unit of the span -> the row's last slot
-            if (P.nu) {
-                const uint32_t last = P.nu - 1;
-                if (HYB) {
-                    if (lane + P.s == last) *reinterpret_cast<u32x4*>(row + kStashLast) = P.w;
-                } else {
-                    const uint32_t slot = (last >> 6) % U;
-                    u32x4 lu = P.v[0];
-#pragma unroll
-                    for (int u = 1; u < U; ++u) lu = slot == static_cast<uint32_t>(u) ? P.v[u] : lu;
-                    if (lane == (last & 63u)) *reinterpret_cast<u32x4*>(row + kStashLast) = lu;
-                }
-            }
-            const uint32_t S = wave_sum(acc);
-            res = writelane(res, S, k, lane);
-        };
-
-        // MULTI: several short packets share one pass — NP packets x (64/NP)
-        // lanes x U units; per-lane packet addresses come from the plan lanes by
-        // ds_bpermute and 16-lane DPP row sums give one total per packet, so
-        // the per-pass issue work is divided by NP.
-        auto multi = [&](auto npc, uint32_t k) {
-            constexpr uint32_t NP = decltype(npc)::value;
-            constexpr uint32_t SL = kWave / NP;  // lanes per packet (32 or 16)
-            constexpr uint32_t kHead = FILL ? kStashHead : (IPV4 ? 3u : 1u);
-            const uint32_t seg = lane / SL, j = lane % SL;
-            const int src = static_cast<int>(k + seg);
-            const uint32_t qlo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(a0)), src));
-            const uint32_t qhi = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(a0 >> 32)), src));
-            const uint32_t qnu = static_cast<uint32_t>(__shfl(static_cast<int>(nunits), src));
-            const uint8_t* qa = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(qhi) << 32) | qlo);
-            u32x4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t c = j + SL * u;
-                v[u] = u32x4{0, 0, 0, 0};
-                if (c < qnu) v[u] = load_unit(qa + 16u * c);
-            }
-            uint32_t acc = 0;
-#pragma unroll
-            for (int u = 0; u < U; ++u) acc = sad4(v[u], acc);
-            uint8_t* row = stash + static_cast<uint32_t>(src) * kStashStride;
-            if (j < kHead) *reinterpret_cast<u32x4*>(row + 16u * j) = v[0];
-            if (qnu) {
-                const uint32_t last = qnu - 1;
-                u32x4 lu = v[0];
-#pragma unroll
-                for (int u = 1; u < U; ++u) lu = last / SL == static_cast<uint32_t>(u) ? v[u] : lu;
-                if (j == last % SL) *reinterpret_cast<u32x4*>(row + kStashLast) = lu;
-            }
-            // 16-lane row sums
-            acc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc), 0xB1, 0xF, 0xF, false));
-            acc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc), 0x4E, 0xF, 0xF, false));
-            acc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc), 0x124, 0xF, 0xF, false));
-            acc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc), 0x128, 0xF, 0xF, false));
-            const uint32_t r0 = __builtin_amdgcn_readlane(acc, 0), r1 = __builtin_amdgcn_readlane(acc, 16);
-            const uint32_t r2 = __builtin_amdgcn_readlane(acc, 32), r3 = __builtin_amdgcn_readlane(acc, 48);
-            if (NP == 4) {
-                res = writelane(res, r0, k, lane);
-                res = writelane(res, r1, k + 1, lane);
-                res = writelane(res, r2, k + 2, lane);
-                res = writelane(res, r3, k + 3, lane);
-            } else {
-                res = writelane(res, r0 + r1, k, lane);
-                res = writelane(res, r2 + r3, k + 1, lane);
-            }
-        };
-
-        if (MULTI) {
-            const uint64_t quad_ok = __ballot(nunits <= 16u * U);
-            const uint64_t pair_ok = __ballot(nunits <= 32u * U);
-            uint32_t k = 0;
-            while (k < cnt) {
-                if (k + 4 <= cnt && ((quad_ok >> k) & 0xFull) == 0xFull) {
-                    multi(std::integral_constant<uint32_t, 4>{}, k);
-                    k += 4;
-                } else if (k + 2 <= cnt && ((pair_ok >> k) & 0x3ull) == 0x3ull) {
-                    multi(std::integral_constant<uint32_t, 2>{}, k);
-                    k += 2;
-                } else {
-                    PktLoad P;
-                    issue(k, true, P);
-                    body(k, P);
-                    k += 1;
-                }
-            }
-        } else if (!PIPE) {
-            for (uint32_t k = 0; k < cnt; ++k) {
-                PktLoad P;
-                issue(k, true, P);
-                body(k, P);
-            }
-        } else {
-            // ping-pong: packet k+1's loads are in flight while packet k is
-            // summed; two named load sets, no register copies (copying an
-            // in-flight load's destination would force a full vmcnt(0) wait)
-            PktLoad PA, PB;
-            issue(0, true, PA);
-            for (uint32_t k = 0; k < cnt; k += 2) {
-                const bool m1 = k + 1 < cnt;
-                issue(m1 ? k + 1 : k, m1, PB);
-                body(k, PA);
-                const bool m2 = k + 2 < cnt;
-                issue(m2 ? k + 2 : k, m2, PA);
-                if (m1) body(k + 1, PB);
-            }
-        }
-        if (IPV4 && huge && mine && !range_bad) {  // not streamed (phase D redoes its sum): head units from the frame
-            constexpr uint32_t kHeadH = FILL ? kStashHead : 3u;
-            uint8_t* hrow = stash + lane * kStashStride;
-            const auto* hu = reinterpret_cast<const u32x4*>(a0);
-#pragma unroll
-            for (uint32_t j = 0; j < kHeadH; ++j) *reinterpret_cast<u32x4*>(hrow + 16u * j) = hu[j];
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): stash writes visible to this wave's reads
-        __builtin_amdgcn_wave_barrier();
-
-        // ---- C: lane i finishes packet i
-        const int rs0 = static_cast<int>(head) + (IPV4 ? 20 : 0);
-        const int re0 = static_cast<int>(head + L);
-        const uint8_t* row = stash + lane * kStashStride;
-        const u32x4 s0 = *reinterpret_cast<const u32x4*>(row);
-        const u32x4 s1 = *reinterpret_cast<const u32x4*>(row + 16);
-        const u32x4 s2 = *reinterpret_cast<const u32x4*>(row + 32);
-        const u32x4 s3 = *reinterpret_cast<const u32x4*>(row + kStashLast);
-        const int lastu16 = 16 * (static_cast<int>(nunits) - 1);
-        uint32_t excl = unit_part(s0, 0, rs0);
-        if (IPV4) {
-            excl += unit_part(s1, 0, rs0 - 16) + unit_part(s2, 0, rs0 - 32);
-        }
-        excl += unit_part(s3, re0 - lastu16, 16);
-        // a unit that is both a head unit and the last one is excluded twice,
-        // but on disjoint byte ranges ([0, rs) and [re, 16)).
-        const uint32_t kept = nunits ? res - excl : 0u;
-        uint32_t S = fold16(kept);
-        if (head & 1u) S = swap16(S);
-        uint32_t word = 0, st = 0;
-        bool slow = huge && mine && !range_bad;
-        uint32_t ipc = 0, pseudo = 0;
-        uint32_t fpos = 0;  // fill: the L4 checksum field's byte offset from a0 (0 = no field to store)
-        int srs = 0, sre = 0;
-        if (IPV4) {
-            // header dwords at byte `head` of the stash row
-            const uint32_t* hw = reinterpret_cast<const uint32_t*>(row + (head & ~3u));
-            const uint32_t sh = head & 3u;
-            const uint32_t d0 = hw[0], d1 = hw[1], d2 = hw[2], d3 = hw[3], d4 = hw[4], d5 = hw[5];
-            const uint32_t h0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-            const uint32_t h1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-            const uint32_t h2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-            const uint32_t h3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
-            const uint32_t h4 = __builtin_amdgcn_alignbyte(d5, d4, sh);
-            // generate (fill) treats the header checksum field (bytes 10-11) as zero (ip.cc:270-276)
-            ipc = ~fold16(static_cast<uint64_t>(h0) + h1 + (fill ? h2 & 0xffffu : h2) + h3 + h4) & 0xffffu;
-            const uint32_t ihl = h0 & 0xfu;
-            const uint32_t ip_len = swap16(h0 >> 16);
-            const uint32_t proto = (h2 >> 8) & 0xffu;
-            const uint32_t l4_off = 4u * ihl;
-            const uint32_t l4_end = ip_len < L ? ip_len : L;
-            uint32_t l4_len = 0;
-            if (L < ip_len) st |= SCCSUM_ST_MALFORMED;
-            if (l4_off > l4_end) {
-                st |= SCCSUM_ST_MALFORMED;
-            } else {
-                l4_len = l4_end - l4_off;
-            }
-            pseudo = fold16(static_cast<uint64_t>(h3 & 0xffffu) + (h3 >> 16) + (h4 & 0xffffu) + (h4 >> 16) +
-                            (proto << 8) + swap16(l4_len & 0xffffu));
-            slow = slow || (fast && (ihl != 5u || ip_len != L));
-            srs = static_cast<int>(head + l4_off);
-            sre = srs + static_cast<int>(l4_len);
-            if (fill) {
-                // the L4 checksum field (UDP +6, udp.cc:184-195; TCP +16, tcp.hh:283-285) counts as
-                // zero: subtract its current value (ones' complement: add ~field).  The pseudo-header
-                // is never zero, so the fold lands in [1, 0xffff] exactly like the reference's.
-                const uint32_t fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
-                const bool has_field = fo != 0u && l4_len >= fo + 2u && (st & SCCSUM_ST_MALFORMED) == 0u;
-                fpos = has_field ? static_cast<uint32_t>(srs) + fo : 0u;
-                uint32_t fv = 0;
-                if (has_field && !slow) {  // ihl == 5 here: the field is inside head units 0..3
-                    fv = static_cast<uint32_t>(row[fpos]) | (static_cast<uint32_t>(row[fpos + 1]) << 8);
-                }
-                const uint32_t r = ~fold16(static_cast<uint64_t>(S) + pseudo + (~fv & 0xffffu)) & 0xffffu;
-                word = (fill_ip ? ipc : 0u) | (has_field ? r << 16 : 0u);
-                st |= (fill_ip ? SCCSUM_ST_OK : 0u) | (has_field ? SCCSUM_ST_L4_OK : 0u);
-            } else {
-                const uint32_t r = ~fold16(static_cast<uint64_t>(S) + pseudo) & 0xffffu;
-                word = ipc | (r << 16);
-                st |= (ipc == 0 ? SCCSUM_ST_OK : 0u) | (r == 0 ? SCCSUM_ST_L4_OK : 0u);
-            }
-        } else {
-            const uint32_t r = raw ? S : ~fold16(static_cast<uint64_t>(S) + swap16(fold16(sd))) & 0xffffu;
-            word = r;
-            st = (!raw && r == 0) ? SCCSUM_ST_OK : 0u;
-        }
-        if (range_bad) {
-            word = 0;
-            st = SCCSUM_ST_RANGE;
-        } else if (short_frame) {
-            word = 0;
-            st = SCCSUM_ST_MALFORMED;
-        }
-
-        // ---- D: exact redo of the packets the fast path could not take
-        uint64_t todo = __ballot(slow);
-        while (todo) {
-            const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(todo));
-            todo &= todo - 1;
-            const uint32_t jlo = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0), j);
-            const uint32_t jhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0 >> 32), j);
-            const uint8_t* ja0 = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(jhi) << 32) | jlo);
-            const uint32_t jhead = __builtin_amdgcn_readlane(head, j);
-            uint64_t rs, re;
-            if (IPV4) {
-                rs = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(srs), j));
-                re = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(sre), j));
-            } else {
-                rs = jhead;
-                re = static_cast<uint64_t>(jhead) + static_cast<uint32_t>(__builtin_amdgcn_readlane(L, j));
-            }
-            uint32_t SJ = exact_range_sum(ja0, rs, re, lane);
-            if (jhead & 1u) SJ = swap16(SJ);
-            if (lane == j) {
-                if (IPV4 && fill) {
-                    if (fpos) {
-                        const uint8_t* fp = reinterpret_cast<const uint8_t*>(a0) + fpos;
-                        const uint32_t fv = static_cast<uint32_t>(fp[0]) | (static_cast<uint32_t>(fp[1]) << 8);
-                        const uint32_t r = ~fold16(static_cast<uint64_t>(SJ) + pseudo + (~fv & 0xffffu)) & 0xffffu;
-                        word = (word & 0xffffu) | (r << 16);
-                    }
-                } else if (IPV4) {
-                    const uint32_t r = ~fold16(static_cast<uint64_t>(SJ) + pseudo) & 0xffffu;
-                    word = ipc | (r << 16);
-                    st = (st & ~SCCSUM_ST_L4_OK) | (r == 0 ? SCCSUM_ST_L4_OK : 0u);
-                } else {
-                    const uint32_t r = raw ? SJ : ~fold16(static_cast<uint64_t>(SJ) + swap16(fold16(sd))) & 0xffffu;
-                    word = r;
-                    st = (!raw && r == 0) ? SCCSUM_ST_OK : 0u;
-                }
-            }
-        }
-
-        if (fill && mine && !range_bad && !short_frame) {
-            // in-place write-back: wire-ready frames (network-order bytes = the LE store of the sum).
-            // ~1 M scattered 2-byte stores per 1.5 GB batch cost ~75 us on top of the read stream
-            // whatever their form (byte, nontemporal, full 64-byte blocks, a separate pass): HBM
-            // read/write turnarounds, DESIGN.md §5.5.
-            uint8_t* wp = reinterpret_cast<uint8_t*>(a0);
-            if (fill_ip) {
-                wp[head + 10] = static_cast<uint8_t>(word);
-                wp[head + 11] = static_cast<uint8_t>(word >> 8);
-            }
-            if (fpos) {
-                wp[fpos] = static_cast<uint8_t>(word >> 16);
-                wp[fpos + 1] = static_cast<uint8_t>(word >> 24);
-            }
-        }
-        if (mine) {
-            if (IPV4) {
-                if (out) reinterpret_cast<uint32_t*>(out)[base + lane] = word;
-            } else {
-                out[base + lane] = static_cast<uint16_t>(word);
-            }
-            if (status) status[base + lane] = static_cast<uint8_t>(st);
-        }
-        __builtin_amdgcn_wave_barrier();  // stash rows are rewritten by the next tile
-        t = t_next;
-    }
 }
 
 // ---------------------------------------------------------------- RSS (Toeplitz)
@@ -900,8 +464,8 @@ __device__ __forceinline__ uint32_t header_dword(const u32x4 (&h)[4], uint32_t h
 
 constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B) between packets
 
-// Flat kernel.  Same tiles, tile order and outputs as csum_batch_kernel, but
-// the bytes are streamed per RUN instead of per packet: a run is a maximal
+// Flat kernel.  Wave w owns tiles of B <= 64 consecutive packets (one per
+// lane); the bytes are streamed per RUN, not per packet: a run is a maximal
 // sequence of tile packets whose 16-byte unit spans go forward with gaps of
 // at most kGapUnits (packed batches: the whole tile).  The wave reads the
 // run's unit extent densely — U units per lane per chunk, no empty lane
@@ -912,11 +476,11 @@ constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B)
 // finishing step needs (the first 1/3/4 units, the last), when they pass.  A
 // packet's sum of units is the difference of its two prefix values (exact
 // mod 2^32; sums stay below 2^32 up to kExactMax bytes), after which the
-// finishing step is the batch kernel's (edge bytes, IPv4 header,
-// pseudo-header, exact redo of the packets the fast path cannot take).
+// finishing step (edge bytes, IPv4 header, pseudo-header) runs lane-parallel
+// and the packets the fast path cannot take are redone exactly, one wave each.
 // Layouts that do not run forward (shuffled offsets) degrade to one run per
-// packet — the per-packet cost of the batch kernel.
-template <int U, bool IPV4, bool FILL, bool PIPE>
+// packet.
+template <int U, bool IPV4, bool FILL, bool PIPE, bool ROLL = false>
 __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
@@ -924,12 +488,14 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
     uint8_t* __restrict__ status, uint64_t n, uint32_t B, uint32_t B2, uint64_t T1, uint32_t* __restrict__ heads,
     uint32_t flags, const RssParams rss) {
     static_assert(!FILL || IPV4, "in-place generate is a frames mode");
+    static_assert(!ROLL || (!PIPE && U % 2 == 0), "rolling rows: pairs of rows, no chunk double buffer");
     constexpr uint32_t C = kWave * U;  // units per chunk
+    constexpr uint32_t kLdsUnits = ROLL ? 2 * kWave : C;  // ROLL parks one pair of rows at a time
     constexpr int kHead = FILL ? 4 : (IPV4 ? 3 : 1);
     const bool raw = !IPV4 && (flags & kFlagRaw);
     const bool fill_ip = FILL && (flags & kFlagFillIp);
-    __shared__ u32x4 ubuf_all[kWavesPerBlock][C];
-    __shared__ uint32_t pbuf_all[kWavesPerBlock][C];
+    __shared__ u32x4 ubuf_all[kWavesPerBlock][kLdsUnits];
+    __shared__ uint32_t pbuf_all[kWavesPerBlock][kLdsUnits];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     u32x4* ubuf = ubuf_all[wv];
@@ -942,7 +508,15 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
     const bool has_seed = !IPV4 && seed != nullptr;
     const uint32_t vo = 16u * lane;
 
-    // tile order: as csum_batch_kernel (static first tile, then dequeued)
+    // Tile order.  Wave w first takes tile w (static: no start-up contention).
+    // With `heads`, the remaining tiles [W, ntiles) are split over kGroups
+    // counters (each on its own line) and dequeued: wave w pulls
+    // tile W + g + kGroups * atomicAdd(heads[g], 1) with g = w % kGroups, so
+    // waves that drew short tiles take more (Zipf batches).  Each group's
+    // dequeue count is known — one per remaining tile of the group plus one
+    // failing dequeue per wave of the group — so the wave that draws the last
+    // number zeroes the counter for the next launch on this slot (no memset,
+    // graph-replay safe).  Without `heads`: static round robin.
     const uint64_t wglob = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
     const uint32_t grp = static_cast<uint32_t>(wglob % kGroups);
     const uint64_t rest = ntiles > nwaves ? ntiles - nwaves : 0;
@@ -1105,7 +679,49 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
                 }
                 __builtin_amdgcn_wave_barrier();  // this chunk's LDS reads precede the next chunk's writes
             };
-            if (PIPE) {
+            if (ROLL) {
+                // Rolling rows: U rows of 64 units stay in flight; each pair
+                // of rows is summed, scanned and parked in LDS as soon as it
+                // lands, and its registers take the same rows of the next
+                // chunk at once, so the wave never drains its loads between
+                // chunks (rows past the extent read as zeros, no memory access).
+                u32x4 v[U];
+                load(r, 0, v);
+                for (uint32_t g = 0; g < ext; g += C) {
+#pragma unroll
+                    for (int u = 0; u < U; u += 2) {
+                        const uint32_t row = g + kWave * static_cast<uint32_t>(u);
+                        uint32_t x[2] = {sad4(v[u], 0u), sad4(v[u + 1], 0u)};
+                        wave_scan_n<2>(x);
+                        pbuf[lane] = carry + x[0];
+                        ubuf[lane] = v[u];
+                        carry += __builtin_amdgcn_readlane(x[0], 63);
+                        pbuf[kWave + lane] = carry + x[1];
+                        ubuf[kWave + lane] = v[u + 1];
+                        carry += __builtin_amdgcn_readlane(x[1], 63);
+                        v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(16u * (row + C) + vo), 0, kNT);
+                        v[u + 1] = __builtin_amdgcn_raw_buffer_load_b128(
+                            r, static_cast<int>(16u * (row + C + kWave) + vo), 0, kNT);
+                        __builtin_amdgcn_wave_barrier();
+                        const int a = rf - static_cast<int>(row);
+                        if (static_cast<uint32_t>(a) < 2 * kWave) {
+                            const u32x4 w = ubuf[a];
+                            pst = pbuf[a] - sad4(w, 0u);
+                            hs[0] = w;
+                        }
+#pragma unroll
+                        for (int j = 1; j < kHead; ++j) {
+                            if (static_cast<uint32_t>(a + j) < 2 * kWave) hs[j] = ubuf[a + j];
+                        }
+                        const int b = rl - static_cast<int>(row);
+                        if (static_cast<uint32_t>(b) < 2 * kWave) {
+                            pend = pbuf[b];
+                            hl = ubuf[b];
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+            } else if (PIPE) {
                 u32x4 va[U], vb[U];
                 load(r, 0, va);
                 for (uint32_t g = 0; g < ext; g += 2 * C) {
@@ -1129,7 +745,7 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
             for (int j = 0; j < kHead; ++j) hs[j] = hu[j];
         }
 
-        // ---- C: lane i finishes packet i (as csum_batch_kernel, stash in registers)
+        // ---- C: lane i finishes packet i
         const int rs0 = static_cast<int>(head) + (IPV4 ? 20 : 0);
         const int re0 = static_cast<int>(head + L);
         const int lastu16 = 16 * (static_cast<int>(nunits) - 1);
@@ -1245,15 +861,84 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
             }
         }
 
-        if (FILL && mine && !range_bad && !short_frame) {
-            uint8_t* wp = reinterpret_cast<uint8_t*>(a0);
-            if (fill_ip) {
-                wp[head + 10] = static_cast<uint8_t>(word);
-                wp[head + 11] = static_cast<uint8_t>(word >> 8);
-            }
-            if (fpos) {
-                wp[fpos] = static_cast<uint8_t>(word >> 16);
-                wp[fpos + 1] = static_cast<uint8_t>(word >> 24);
+        if (FILL) {
+            // In-place write-back: wire-ready frames.  A store into a line the
+            // L2 does not hold goes to memory as a partial (byte-masked) write,
+            // and those cost like a read-write turnaround each: 2 M 2-byte
+            // stores after the nt read stream add ~120 us to a 1.5 GB batch
+            // (tools/dev/store_probe.hip, profiles/r02_store_probe.log).  The
+            // stream's nt loads leave no line behind, so each 16-byte unit
+            // holding a field is first read again (default policy: the line
+            // is fetched whole and held), the fields are patched into it and,
+            // where nobody else writes its other bytes, the unit is stored
+            // whole; otherwise the field bytes are stored alone into the
+            // now-resident line.  Whole units: units 0..3 from a0 lie inside
+            // the frame when L >= 64, except unit 0 reaching up to 15 bytes
+            // before the frame (head > 0); those bytes are the tail of the
+            // previous packet of this tile when it ends exactly where this
+            // frame starts and is at least 96 bytes long (its own stores stay
+            // within its first 78 bytes); frames do not overlap, so no other
+            // frame lies there.
+            const int pl = lane ? static_cast<int>(lane) - 1 : 0;
+            const uint64_t po = (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(cur.o >> 32), pl))) << 32) |
+                                static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(cur.o)), pl));
+            const uint32_t pL = static_cast<uint32_t>(__shfl(static_cast<int>(L), pl));
+            const bool prev_ok = lane != 0 && po + pL == cur.o && pL >= 96u;
+            if (mine && !range_bad && !short_frame) {
+                const int fb[4] = {fill_ip ? static_cast<int>(head) + 10 : -1, fill_ip ? static_cast<int>(head) + 11 : -1,
+                                   fpos ? static_cast<int>(fpos) : -1, fpos ? static_cast<int>(fpos) + 1 : -1};
+                const uint32_t fv[4] = {word & 0xffu, (word >> 8) & 0xffu, (word >> 16) & 0xffu, word >> 24};
+                uint8_t* wp = reinterpret_cast<uint8_t*>(a0);
+                u32x4* wu = reinterpret_cast<u32x4*>(a0);
+                if (!slow) {  // ihl 5: every field within units 0..3
+                    uint32_t need = 0;
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) need |= fb[f] >= 0 ? 1u << (fb[f] >> 4) : 0u;
+                    u32x4 w[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (need & (1u << k)) w[k] = wu[k];  // re-read: the line comes back whole
+                    }
+#if SCCSUM_FILL_WHOLE
+                    const uint32_t whole = L >= 64u ? need & ((head == 0u || prev_ok) ? 0xfu : 0xeu) : 0u;
+#else
+                    const uint32_t whole = 0u;
+#endif
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) {
+                        if (fb[f] >= 0) {
+                            const int d = fb[f] >> 2;
+                            const uint32_t sh = 8u * static_cast<uint32_t>(fb[f] & 3);
+#pragma unroll
+                            for (int k = 0; k < 16; ++k) {
+                                if (d == k) w[k >> 2][k & 3] = (w[k >> 2][k & 3] & ~(0xffu << sh)) | (fv[f] << sh);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (whole & (1u << k)) {
+                            wu[k] = w[k];
+                        } else if (need & (1u << k)) {
+                            // bytes alone, after the re-read (the stores wait on it)
+#pragma unroll
+                            for (int f = 0; f < 4; ++f) {
+                                if (fb[f] >= 0 && (fb[f] >> 4) == k) {
+                                    const int d = fb[f] >> 2;
+                                    uint32_t x = 0;
+#pragma unroll
+                                    for (int j = 0; j < 16; ++j) x = d == j ? w[j >> 2][j & 3] : x;
+                                    wp[fb[f]] = static_cast<uint8_t>(x >> (8u * static_cast<uint32_t>(fb[f] & 3)));
+                                }
+                            }
+                        }
+                    }
+                } else {  // IP options / trimmed length (phase D frames): bytes alone
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) {
+                        if (fb[f] >= 0) wp[fb[f]] = static_cast<uint8_t>(fv[f]);
+                    }
+                }
             }
         }
         if (mine) {
@@ -1360,21 +1045,16 @@ __global__ __launch_bounds__(kBlock) void fill_header_kernel(uint8_t* __restrict
     if (status) status[i] = static_cast<uint8_t>(st);
 }
 
-// Plain stream-read of the same load shape (16 B per lane, nontemporal).
+// Plain stream-read of the same load width (16 B per lane, nontemporal): one
+// load per lane per step, grid-stride in launch order.  This simple form is the
+// fastest plain read measured (tools/dev/store_probe.hip: 226 us per 1.57 GB =
+// 6.95 TB/s; an earlier 4-loads-per-step form with an XCD block remap ran
+// 6.7 TB/s), so it is the measured ceiling bench.py reports.
 __global__ __launch_bounds__(kBlock) void read_probe_kernel(const u32x4* __restrict__ src, uint64_t units,
                                                              uint64_t* __restrict__ sink) {
     uint64_t acc = 0;
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock;
-    uint64_t i = static_cast<uint64_t>(xcd_block_id()) * kBlock + threadIdx.x;
-    for (; i + 3 * stride < units; i += 4 * stride) {
-        const u32x4 a = __builtin_nontemporal_load(src + i);
-        const u32x4 b = __builtin_nontemporal_load(src + i + stride);
-        const u32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
-        const u32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
-        acc += static_cast<uint64_t>(a.x) + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
-        acc += static_cast<uint64_t>(c.x) + c.y + c.z + c.w + d.x + d.y + d.z + d.w;
-    }
-    for (; i < units; i += stride) {
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < units; i += stride) {
         const u32x4 a = __builtin_nontemporal_load(src + i);
         acc += static_cast<uint64_t>(a.x) + a.y + a.z + a.w;
     }
@@ -1398,51 +1078,113 @@ int cu_count() {
     return c;
 }
 
-std::atomic<int> g_blocks_per_cu{kBlocksPerCU};
+// Diagnostic knobs (include/sccsum_diag.h): per host thread, so one shard's
+// A/B settings never leak into another thread's launches.
+struct Knobs {
+    int variant = 0;                 // 0 = default; 1 = simple kernel; 10-16 = flat-kernel forms
+    int blocks_per_cu = kBlocksPerCU;  // grid cap in workgroups per CU
+    int group_units = 0;             // simple kernel: U override (0 = by max_len)
+    int tile_packets = kWave;        // flat kernel: max packets per tile
+    int dynamic = 1;                 // flat kernel: dequeue tiles (1) or static round robin (0)
+    int tile_bytes = 0;              // flat kernel: target bytes per tile (0 = packets cap only)
+    int tail_div = 1;                // flat kernel: tail tiles hold B / tail_div packets (1 = no guided tail)
+    int tail_tiles = 4;              // ... and cover about this many tail tiles per wave slot
+};
+thread_local Knobs t_knobs;
 
 unsigned grid_for(uint64_t n) {
-    const uint64_t cap = static_cast<uint64_t>(cu_count()) * g_blocks_per_cu.load(std::memory_order_relaxed);
+    const uint64_t cap = static_cast<uint64_t>(cu_count()) * t_knobs.blocks_per_cu;
     uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
     if (want > cap) want = cap;
     want = (want + 7) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
     return static_cast<unsigned>(want);
 }
 
-std::atomic<int> g_group_units{0};  // diagnostic override of U (0 = by max_len)
-std::atomic<int> g_tile_packets{kWave};  // max packets per batch-kernel tile
-std::atomic<int> g_dynamic{1};           // batch kernel: dequeue tiles (1) or static round robin (0)
+// Tile-head counters for the flat kernel's dequeue: one slot (kGroups
+// counters, each on its own 256-byte line) per STREAM.  Launches on one stream
+// run one after another, and each launch leaves its slot zeroed (the last
+// dequeue of each group resets it), so a stream can reuse its slot with no
+// memset and any number of launches may be queued; streams never share a
+// slot.  Slots are allocated per device in chunks of kSlotChunk as new
+// streams appear (zeroed once, synchronously), up to kMaxSlotChunks chunks;
+// a launch that cannot have a slot — more streams than that, a stream being
+// captured into a graph (a replay may run anywhere, any time), a thread that
+// never called sccsum_init — uses the static tile order instead: the same
+// results, without the dynamic load balance.
+constexpr uint32_t kSlotChunk = 256;
+constexpr uint32_t kMaxSlotChunks = 16;
 
-// Per-device ring of tile-head slots (kGroups heads, each on its own line),
-// allocated and zeroed once in sccsum_init; each launch takes the next slot
-// and leaves it zeroed again (the last dequeue of each group resets it), so
-// launches need no memset and launches on different streams do not share
-// counters (up to kHeadSlots launches in flight per device).
-constexpr int kHeadSlots = 256;
-uint32_t* g_heads[kMaxDevices];
-std::atomic<uint32_t> g_head_next[kMaxDevices];
+struct DeviceSlots {
+    std::mutex mu;
+    bool ready = false;  // sccsum_init ran for this device
+    uint32_t* chunk[kMaxSlotChunks] = {};
+    uint32_t used = 0;
+    std::vector<std::pair<uintptr_t, uint32_t*>> by_stream;
+};
+DeviceSlots g_slots[kMaxDevices];
 
 int ensure_heads(int dev) {
     if (dev < 0 || dev >= kMaxDevices) return SCCSUM_ENODEV;
-    if (g_heads[dev] != nullptr) return SCCSUM_OK;
-    void* p = nullptr;
-    const size_t bytes = size_t(kHeadSlots) * kHeadSlotWords * sizeof(uint32_t);
-    hipError_t e = hipMalloc(&p, bytes);
-    if (e != hipSuccess) return static_cast<int>(e);
-    e = hipMemset(p, 0, bytes);  // once: from here on every launch leaves its slot zeroed
-    if (e != hipSuccess) return static_cast<int>(e);
-    g_heads[dev] = static_cast<uint32_t*>(p);
+    std::lock_guard<std::mutex> g(g_slots[dev].mu);
+    g_slots[dev].ready = true;
     return SCCSUM_OK;
 }
 
-uint32_t* next_heads() {
+uintptr_t stream_key(hipStream_t s) {
+    // hipStreamPerThread names a different stream on every host thread
+    static std::atomic<uintptr_t> next_id{1};
+    thread_local const uintptr_t tid = next_id.fetch_add(1);
+    return s == hipStreamPerThread ? (tid << 1) | 1u : reinterpret_cast<uintptr_t>(s);
+}
+
+uint32_t* heads_for(hipStream_t s) {
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices || g_heads[dev] == nullptr) return nullptr;
-    const uint32_t slot = g_head_next[dev].fetch_add(1, std::memory_order_relaxed) % kHeadSlots;
-    return g_heads[dev] + kHeadSlotWords * slot;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    const uintptr_t key = stream_key(s);
+    thread_local int c_dev = -1;
+    thread_local uintptr_t c_key = 0;
+    thread_local uint32_t* c_ptr = nullptr;
+    if (c_dev == dev && c_key == key) return c_ptr;
+    DeviceSlots& D = g_slots[dev];
+    uint32_t* p = nullptr;
+    {
+        std::lock_guard<std::mutex> g(D.mu);
+        if (!D.ready) return nullptr;
+        for (const auto& e : D.by_stream) {
+            if (e.first == key) {
+                p = e.second;
+                break;
+            }
+        }
+        if (p == nullptr && D.used < kSlotChunk * kMaxSlotChunks) {
+            const uint32_t c = D.used / kSlotChunk;
+            if (D.chunk[c] == nullptr) {
+                void* m = nullptr;
+                const size_t bytes = size_t(kSlotChunk) * kHeadSlotWords * sizeof(uint32_t);
+                if (hipMalloc(&m, bytes) != hipSuccess) return nullptr;
+                if (hipMemset(m, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+                    (void)hipFree(m);
+                    return nullptr;
+                }
+                D.chunk[c] = static_cast<uint32_t*>(m);
+            }
+            p = D.chunk[c] + size_t(kHeadSlotWords) * (D.used % kSlotChunk);
+            ++D.used;
+            D.by_stream.emplace_back(key, p);
+        }
+    }
+    if (p != nullptr) {
+        c_dev = dev;
+        c_key = key;
+        c_ptr = p;
+    }
+    return p;
 }
 
 int units_class(uint32_t max_len) {
-    const int forced = g_group_units.load(std::memory_order_relaxed);
+    const int forced = t_knobs.group_units;
     if (forced) return forced;
     if (max_len == 0) return 4;
     const uint64_t units = (static_cast<uint64_t>(max_len) + 30) / 16;  // worst-case head of 15
@@ -1452,25 +1194,12 @@ int units_class(uint32_t max_len) {
     return 8;
 }
 
-// Kernel variant: 0 = default (the flat kernel: 16 for batches of >= 512 Ki
-// packets and >= 256 MiB, else 15), 10-16 = the flat kernel's forms (launch_u),
-// 1 = simple one-packet-per-wave loop (independent second implementation),
-// 2 = batch kernel, 3 = batch kernel with the next packet in flight (both
-// with nontemporal loads), 4 / 5 = 2 / 3 with default-policy loads,
-// 6 / 7 = 2 / 3 with each packet's last 128-byte line loaded default-policy,
-// 8 / 9 = 2 / 6 with short packets sharing passes (4 x 16 or 2 x 32 lanes).
-std::atomic<int> g_variant{0};
-
-std::atomic<int> g_tile_bytes{0};  // flat kernel: target bytes per tile (0 = packets cap only)
-
 // Flat-kernel launch: the grid is what the chip holds at once (the kernel's
 // occupancy, from its VGPR and LDS use, capped by the blocks-per-CU knob), so
 // every wave's static first tile starts at launch; tiles hold about
-// g_tile_bytes of packets (mean length from bytes_len / n), capped at 64.
+// tile_bytes of packets (mean length from bytes_len / n), capped at 64.
 using FlatKernel = void (*)(const uint8_t*, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*, uint16_t*,
                             uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t, uint32_t*, uint32_t, const RssParams);
-std::atomic<int> g_tail_div{1};    // flat kernel: tail tiles hold B / g_tail_div packets (1 = no guided tail)
-std::atomic<int> g_tail_tiles{4};  // ... and cover about this many tail tiles per wave slot
 
 int flat_occupancy(FlatKernel k) {
     constexpr int kSlots = 16;
@@ -1497,13 +1226,13 @@ int flat_occupancy(FlatKernel k) {
 void launch_flat(FlatKernel kern, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
                  const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
                  uint32_t flags, const RssParams& rss) {
+    const Knobs& K = t_knobs;
     const int occ = flat_occupancy(kern);
-    const int knob = g_blocks_per_cu.load(std::memory_order_relaxed);
-    const uint64_t bpc = static_cast<uint64_t>(occ < knob ? occ : knob);
+    const uint64_t bpc = static_cast<uint64_t>(occ < K.blocks_per_cu ? occ : K.blocks_per_cu);
     const uint64_t cap = static_cast<uint64_t>(cu_count()) * bpc;
     const uint64_t slots = cap * kWavesPerBlock;
-    uint64_t bmax = static_cast<uint64_t>(g_tile_packets.load(std::memory_order_relaxed));
-    const uint64_t tb = static_cast<uint64_t>(g_tile_bytes.load(std::memory_order_relaxed));
+    uint64_t bmax = static_cast<uint64_t>(K.tile_packets);
+    const uint64_t tb = static_cast<uint64_t>(K.tile_bytes);
     if (tb) {
         const uint64_t mean = bytes_len / n ? bytes_len / n : 1;
         const uint64_t bb = tb / mean ? tb / mean : 1;
@@ -1511,102 +1240,53 @@ void launch_flat(FlatKernel kern, hipStream_t s, const uint8_t* b, uint64_t byte
     }
     uint64_t B = (n + slots - 1) / slots;
     B = B < 1 ? 1 : (B > bmax ? bmax : B);
-    // guided tail: the last ~g_tail_tiles small tiles per wave slot hold B / g_tail_div packets each
-    const int div = g_tail_div.load(std::memory_order_relaxed);
-    const uint64_t B2 = div > 1 && B / div ? B / div : B;
-    const uint64_t tail = B2 < B ? slots * B2 * static_cast<uint64_t>(g_tail_tiles.load(std::memory_order_relaxed)) : 0;
+    // guided tail: the last ~tail_tiles small tiles per wave slot hold B / tail_div packets each
+    const uint64_t B2 = K.tail_div > 1 && B / K.tail_div ? B / K.tail_div : B;
+    const uint64_t tail = B2 < B ? slots * B2 * static_cast<uint64_t>(K.tail_tiles) : 0;
     const uint64_t T1 = tail < n ? (n - tail) / B : 0;
     const uint64_t tiles = T1 + (n - T1 * B + B2 - 1) / B2;
     uint64_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     blocks = blocks < cap ? blocks : cap;
     blocks = (blocks + 15) & ~uint64_t(15);  // multiple of 16: XCD mapping, waves divide into kGroups
-    uint32_t* heads = g_dynamic.load(std::memory_order_relaxed) ? next_heads() : nullptr;
+    uint32_t* heads = K.dynamic ? heads_for(s) : nullptr;
     kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
         b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, static_cast<uint32_t>(B), static_cast<uint32_t>(B2), T1,
         heads, flags, rss);
 }
 
-template <int U, bool IPV4>
-void launch_u(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
-              const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
-              uint32_t flags, const RssParams& rss) {
-    if (variant == 1) {
-        csum_kernel<U, IPV4>
-            <<<dim3(grid_for(n)), dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
-        return;
+template <bool IPV4>
+void launch_simple(int uc, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
+                   const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
+                   uint32_t flags) {
+    const dim3 g(grid_for(n)), t(kBlock);
+    switch (uc) {
+        case 1: csum_kernel<1, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags); break;
+        case 2: csum_kernel<2, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags); break;
+        case 4: csum_kernel<4, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags); break;
+        default: csum_kernel<8, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags); break;
     }
-    if (variant >= 10) {  // flat kernel: 10 / 11 = U 2, 12 / 13 = U 4, 14 / 15 = U 8 (odd: next chunk in flight), 16 = U 16
-        auto go = [&](auto kern) {
-            launch_flat(kern, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
-        };
-        constexpr bool F = IPV4;  // frames may fill in place; spans never do
-        const bool fill = IPV4 && (flags & kFlagFillL4);
-        switch (variant) {
-            case 10: fill ? go(csum_flat_kernel<2, IPV4, F, false>) : go(csum_flat_kernel<2, IPV4, false, false>); break;
-            case 11: fill ? go(csum_flat_kernel<2, IPV4, F, true>) : go(csum_flat_kernel<2, IPV4, false, true>); break;
-            case 12: fill ? go(csum_flat_kernel<4, IPV4, F, false>) : go(csum_flat_kernel<4, IPV4, false, false>); break;
-            case 13: fill ? go(csum_flat_kernel<4, IPV4, F, true>) : go(csum_flat_kernel<4, IPV4, false, true>); break;
-            case 14: fill ? go(csum_flat_kernel<8, IPV4, F, false>) : go(csum_flat_kernel<8, IPV4, false, false>); break;
-            case 15: fill ? go(csum_flat_kernel<8, IPV4, F, true>) : go(csum_flat_kernel<8, IPV4, false, true>); break;
-            default: fill ? go(csum_flat_kernel<16, IPV4, F, false>) : go(csum_flat_kernel<16, IPV4, false, false>); break;
-        }
-        return;
-    }
-    // batch kernel: tiles of B <= 64 packets, enough tiles to fill every wave slot
-    const uint64_t slots = static_cast<uint64_t>(cu_count()) * g_blocks_per_cu.load() * kWavesPerBlock;
-    const uint64_t bmax = static_cast<uint64_t>(g_tile_packets.load(std::memory_order_relaxed));
-    uint64_t B = (n + slots - 1) / slots;
-    B = B < 1 ? 1 : (B > bmax ? bmax : B);
-    // grid: multiple of 16 workgroups so the wave count divides into kGroups
-    const dim3 grid((grid_for((n + B - 1) / B) + 15u) & ~15u);
-    const uint32_t b32 = static_cast<uint32_t>(B);
-    uint32_t* heads = nullptr;
-    if (g_dynamic.load(std::memory_order_relaxed)) heads = next_heads();
-    if constexpr (IPV4) {
-        if (flags & kFlagFillL4) {
-            if (variant == 8 || variant == 9) {
-                csum_batch_kernel<U, true, false, kNT, false, true, true><<<grid, dim3(kBlock), 0, s>>>(
-                    b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
-            } else {
-                csum_batch_kernel<U, true, false, kNT, true, false, true><<<grid, dim3(kBlock), 0, s>>>(
-                    b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
-            }
-            return;
-        }
-    }
+}
+
+// Flat-kernel forms: 10 / 11 = U 2, 12 / 13 = U 4, 14 / 15 = U 8 (odd: the
+// next chunk in flight), 16 = U 16.  Frames may fill in place; spans never do.
+template <bool IPV4>
+void launch_flat_variant(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
+                         const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
+                         uint32_t flags, const RssParams& rss) {
+    auto go = [&](auto kern) { launch_flat(kern, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss); };
+    constexpr bool F = IPV4;
+    const bool fill = IPV4 && (flags & kFlagFillL4);
     switch (variant) {
-        case 8:
-            csum_batch_kernel<U, IPV4, false, kNT, false, true>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
-            break;
-        case 9:
-            csum_batch_kernel<U, IPV4, false, kNT, true, true>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
-            break;
-        case 6:
-            csum_batch_kernel<U, IPV4, false, kNT, true, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
-            break;
-        case 7:
-            csum_batch_kernel<U, IPV4, true, kNT, true, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
-            break;
-        case 2:
-            csum_batch_kernel<U, IPV4, false, kNT, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
-            break;
-        case 4:
-            csum_batch_kernel<U, IPV4, false, 0, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
-            break;
-        case 5:
-            csum_batch_kernel<U, IPV4, true, 0, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
-            break;
-        default:
-            csum_batch_kernel<U, IPV4, true, kNT, false, false>
-                <<<grid, dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, b32, heads, flags);
-            break;
+        case 10: fill ? go(csum_flat_kernel<2, IPV4, F, false>) : go(csum_flat_kernel<2, IPV4, false, false>); break;
+        case 11: fill ? go(csum_flat_kernel<2, IPV4, F, true>) : go(csum_flat_kernel<2, IPV4, false, true>); break;
+        case 12: fill ? go(csum_flat_kernel<4, IPV4, F, false>) : go(csum_flat_kernel<4, IPV4, false, false>); break;
+        case 13: fill ? go(csum_flat_kernel<4, IPV4, F, true>) : go(csum_flat_kernel<4, IPV4, false, true>); break;
+        case 14: fill ? go(csum_flat_kernel<8, IPV4, F, false>) : go(csum_flat_kernel<8, IPV4, false, false>); break;
+        case 15: fill ? go(csum_flat_kernel<8, IPV4, F, true>) : go(csum_flat_kernel<8, IPV4, false, true>); break;
+        case 17: fill ? go(csum_flat_kernel<8, IPV4, F, false, true>) : go(csum_flat_kernel<8, IPV4, false, false, true>); break;
+        case 18: fill ? go(csum_flat_kernel<12, IPV4, F, false, true>) : go(csum_flat_kernel<12, IPV4, false, false, true>); break;
+        case 19: fill ? go(csum_flat_kernel<16, IPV4, F, false, true>) : go(csum_flat_kernel<16, IPV4, false, false, true>); break;
+        default: fill ? go(csum_flat_kernel<16, IPV4, F, false>) : go(csum_flat_kernel<16, IPV4, false, false>); break;
     }
 }
 
@@ -1639,36 +1319,23 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
         (reinterpret_cast<uintptr_t>(d_out) & (IPV4 ? 3u : 1u))) {
         return SCCSUM_EINVAL;
     }
-    int variant = g_variant.load(std::memory_order_relaxed);
+    int variant = t_knobs.variant;
     // default: the flat kernel, all loads nontemporal — 16 units per lane per
     // chunk for big batches (>= 512 Ki packets and 256 MiB), else 8 units with
     // the next chunk in flight: the 16-unit form runs 2 waves per SIMD, too
     // few tiles per wave on smaller batches (DESIGN.md §5.1 has the A/B)
-    if (variant == 0) variant = (n >= (512u << 10) && bytes_len >= (256ull << 20)) ? 16 : 15;
-    if (variant == 1 && (flags & kFlagFillL4)) variant = 6;  // in-place write-back lives in the batch kernel
+    const int dflt = (n >= (512u << 10) && bytes_len >= (256ull << 20)) ? 16 : 15;
+    if (variant == 0 || (variant == 1 && (flags & kFlagFillL4))) variant = dflt;  // in-place write-back: flat only
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
-    // batch kernel: U = 2 for every size (long packets keep 4 groups in flight
-    // in their loop); the simple kernel sizes U by max_len.
-    const int forced = g_group_units.load(std::memory_order_relaxed);
-    const int uc = variant == 1 ? units_class(max_len) : (forced ? forced : 2);
-    switch (uc) {
-        case 1:
-            launch_u<1, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
-            break;
-        case 2:
-            launch_u<2, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
-            break;
-        case 4:
-            launch_u<4, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
-            break;
-        default:
-            launch_u<8, IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
-            break;
-    }
-    if (IPV4 && rss.hash != nullptr && variant < 10) {  // RSS is fused only in the flat kernel
-        rss_kernel<<<dim3(static_cast<unsigned>((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s>>>(
-            b, bytes_len, d_off, d_len, nullptr, n, rss);
+    if (variant == 1) {
+        launch_simple<IPV4>(units_class(max_len), s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+        if (IPV4 && rss.hash != nullptr) {  // RSS is fused only in the flat kernel
+            rss_kernel<<<dim3(static_cast<unsigned>((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s>>>(
+                b, bytes_len, d_off, d_len, nullptr, n, rss);
+        }
+    } else {
+        launch_flat_variant<IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
     }
     return static_cast<int>(hipGetLastError());
 }
@@ -1846,45 +1513,45 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
 }
 
 int sccsum_set_kernel_variant(int variant) {
-    if (variant < 0 || variant > 16) return SCCSUM_EINVAL;
-    sccsum::g_variant.store(variant, std::memory_order_relaxed);
+    if (!(variant == 0 || variant == 1 || (variant >= 10 && variant <= 19))) return SCCSUM_EINVAL;
+    sccsum::t_knobs.variant = variant;
     return SCCSUM_OK;
 }
 
 int sccsum_set_blocks_per_cu(int blocks) {
     if (blocks < 1 || blocks > 32) return SCCSUM_EINVAL;
-    sccsum::g_blocks_per_cu.store(blocks, std::memory_order_relaxed);
+    sccsum::t_knobs.blocks_per_cu = blocks;
     return SCCSUM_OK;
 }
 
 int sccsum_set_group_units(int units) {
     if (units != 0 && units != 1 && units != 2 && units != 4 && units != 8) return SCCSUM_EINVAL;
-    sccsum::g_group_units.store(units, std::memory_order_relaxed);
+    sccsum::t_knobs.group_units = units;
     return SCCSUM_OK;
 }
 
 int sccsum_set_tile_packets(int packets) {
     if (packets < 1 || packets > sccsum::kWave) return SCCSUM_EINVAL;
-    sccsum::g_tile_packets.store(packets, std::memory_order_relaxed);
+    sccsum::t_knobs.tile_packets = packets;
     return SCCSUM_OK;
 }
 
 int sccsum_set_tile_bytes(int bytes) {
     if (bytes < 0) return SCCSUM_EINVAL;
-    sccsum::g_tile_bytes.store(bytes, std::memory_order_relaxed);
+    sccsum::t_knobs.tile_bytes = bytes;
     return SCCSUM_OK;
 }
 
 int sccsum_set_tail_tiles(int divisor, int per_slot) {
     if (divisor < 1 || divisor > 64 || per_slot < 0 || per_slot > 64) return SCCSUM_EINVAL;
-    sccsum::g_tail_div.store(divisor, std::memory_order_relaxed);
-    sccsum::g_tail_tiles.store(per_slot, std::memory_order_relaxed);
+    sccsum::t_knobs.tail_div = divisor;
+    sccsum::t_knobs.tail_tiles = per_slot;
     return SCCSUM_OK;
 }
 
 int sccsum_set_dynamic_tiles(int on) {
     if (on != 0 && on != 1) return SCCSUM_EINVAL;
-    sccsum::g_dynamic.store(on, std::memory_order_relaxed);
+    sccsum::t_knobs.dynamic = on;
     return SCCSUM_OK;
 }
 

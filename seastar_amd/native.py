@@ -15,6 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libsccsum.so")
 HEADER_PATH = os.path.join(REPO_DIR, "include", "sccsum.h")
+DIAG_HEADER_PATH = os.path.join(REPO_DIR, "include", "sccsum_diag.h")
 
 SCCSUM_OK = 0
 SCCSUM_EINVAL = -1
@@ -101,8 +102,8 @@ class Fragment(ctypes.Structure):
 
 
 def header_symbols() -> list[str]:
-    """Every function declared in include/sccsum.h."""
-    text = open(HEADER_PATH).read()
+    """Every function declared in include/sccsum.h and include/sccsum_diag.h."""
+    text = open(HEADER_PATH).read() + open(DIAG_HEADER_PATH).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(sccsum_[a-z0-9_]+)\s*\(", text)))
 

@@ -3,7 +3,9 @@ the end-to-end path of BASELINE cfg 5 — DPDK-mbuf-shaped pinned host buffers,
 hipMemcpyAsync in and out on side streams, overlapped with the kernels."""
 from __future__ import annotations
 
+import bisect
 import ctypes
+import threading
 import weakref
 
 import numpy as np
@@ -14,14 +16,66 @@ MBUF_SLOT = 128 + 128 + 2048  # rte_mbuf + headroom + data room (src/net/dpdk.cc
 MBUF_DATA_OFF = 256
 
 
+class _PinnedBlock:
+    """Owner of one sccsum_host_alloc block, exposed through the array
+    interface: numpy arrays made from it (and every view of those) hold a
+    reference to the block, so the memory is freed only when the last of them
+    is gone."""
+
+    def __init__(self, nbytes: int):
+        self._lib = native.load()
+        p = ctypes.c_void_p()
+        native.check(self._lib.sccsum_host_alloc(ctypes.byref(p), max(int(nbytes), 1)), "sccsum_host_alloc")
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+        self.__array_interface__ = {"data": (self.ptr, False), "shape": (self.nbytes,), "typestr": "|u1",
+                                    "version": 3}
+        _register(self)
+
+    def __del__(self):
+        _unregister(self.ptr)
+        self._lib.sccsum_host_free(self.ptr)
+
+
+# live pinned blocks by start address, for is_pinned (mapped burst submits)
+_pinned_lock = threading.Lock()
+_pinned_starts: list[int] = []
+_pinned_blocks: dict[int, weakref.ref] = {}
+
+
+def _register(b: _PinnedBlock) -> None:
+    with _pinned_lock:
+        bisect.insort(_pinned_starts, b.ptr)
+        _pinned_blocks[b.ptr] = weakref.ref(b)
+
+
+def _unregister(ptr: int) -> None:
+    with _pinned_lock:
+        i = bisect.bisect_left(_pinned_starts, ptr)
+        if i < len(_pinned_starts) and _pinned_starts[i] == ptr:
+            del _pinned_starts[i]
+        _pinned_blocks.pop(ptr, None)
+
+
+def is_pinned(a: np.ndarray) -> bool:
+    """a's bytes lie inside one live pinned_empty block (device-readable at
+    the same address: what a zero-copy burst submit needs)."""
+    if a.size == 0:
+        return True
+    lo = a.ctypes.data
+    hi = lo + a.nbytes
+    with _pinned_lock:
+        i = bisect.bisect_right(_pinned_starts, lo) - 1
+        if i < 0:
+            return False
+        b = _pinned_blocks[_pinned_starts[i]]()
+        return b is not None and hi <= b.ptr + b.nbytes
+
+
 def pinned_empty(nbytes: int) -> np.ndarray:
-    """uint8 array in page-locked host memory (freed with the array)."""
-    lib = native.load()
-    p = ctypes.c_void_p()
-    native.check(lib.sccsum_host_alloc(ctypes.byref(p), max(int(nbytes), 1)), "sccsum_host_alloc")
-    arr = np.ctypeslib.as_array((ctypes.c_uint8 * max(int(nbytes), 1)).from_address(p.value))[: int(nbytes)]
-    weakref.finalize(arr, lib.sccsum_host_free, p.value)
-    return arr
+    """uint8 array in page-locked host memory, freed when the array and every
+    view of it are gone."""
+    return np.asarray(_PinnedBlock(nbytes))
 
 
 def mbuf_pool(frames: np.ndarray, lengths: np.ndarray, offsets: np.ndarray):

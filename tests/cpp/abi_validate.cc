@@ -1,0 +1,106 @@
+// Argument validation of every C-ABI entry point (include/sccsum.h,
+// include/sccsum_diag.h) without a device: each bad call must return its
+// error code and touch nothing.  Built by tests/test_sanitize.py with host
+// AddressSanitizer + UndefinedBehaviorSanitizer (the reference's `sanitize`
+// build mode, cmake/FindSanitizers.cmake:37-43) over the library sources.
+// Exit status 0 = every check held.
+#include "sccsum.h"
+#include "sccsum_diag.h"
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+static int failures = 0;
+#define EXPECT(cond)                                                       \
+    do {                                                                   \
+        if (!(cond)) {                                                     \
+            ++failures;                                                    \
+            std::printf("FAILED %s (line %d)\n", #cond, __LINE__);         \
+        }                                                                  \
+    } while (0)
+
+static void noop(void*, uint64_t, uint32_t, const uint16_t*, const uint8_t*) {}
+
+int main() {
+    void* const d16 = reinterpret_cast<void*>(uintptr_t(0x10000));  // aligned non-null stand-ins, never dereferenced
+    void* const odd = reinterpret_cast<void*>(uintptr_t(0x10002));
+    // n == 0 is a no-op whatever the pointers
+    EXPECT(sccsum_spans(nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr) == SCCSUM_OK);
+    EXPECT(sccsum_ipv4_frames(nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr) == SCCSUM_OK);
+    EXPECT(sccsum_fragments(nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr,
+                            nullptr) == SCCSUM_OK);
+    EXPECT(sccsum_gather(nullptr, 0, nullptr, nullptr) == SCCSUM_OK);
+    // null / misaligned pointers
+    EXPECT(sccsum_spans(nullptr, 64, nullptr, nullptr, nullptr, nullptr, nullptr, 3, 0, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_spans(odd, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr,
+                        static_cast<uint16_t*>(d16), nullptr, 3, 0, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_ipv4_frames(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16),
+                              static_cast<uint16_t*>(odd), nullptr, 3, 0, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_fragments(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), 4,
+                            static_cast<const uint32_t*>(d16), nullptr, static_cast<uint16_t*>(d16), nullptr, 2, 0,
+                            nullptr, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_fragments_workspace(1000) >= 3000);
+    EXPECT(sccsum_gather(static_cast<const sccsum_gather_desc*>(odd), 1, d16, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_read_probe(nullptr, 16, nullptr, nullptr) == SCCSUM_EINVAL);
+    // fill modes
+    EXPECT(sccsum_ipv4_fill(nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_ipv4_fill(nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, 0,
+                            SCCSUM_FILL_L4 | SCCSUM_FILL_L4_PSEUDO, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_ipv4_fill(nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, 0, SCCSUM_FILL_TSO, nullptr) ==
+           SCCSUM_EINVAL);
+    EXPECT(sccsum_ipv4_fill(nullptr, 64, nullptr, nullptr, nullptr, nullptr, 3, 0, SCCSUM_FILL_IP, nullptr) ==
+           SCCSUM_EINVAL);
+    // RSS
+    const uint8_t key3[3] = {1, 2, 3};
+    EXPECT(sccsum_ipv4_rss(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), key3, 3, 0,
+                           static_cast<uint32_t*>(d16), nullptr, 1, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_ipv4_frames_rss(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16),
+                                  static_cast<uint16_t*>(d16), nullptr, 1, 0, key3, 40, 7,
+                                  static_cast<uint32_t*>(d16), nullptr) == SCCSUM_EINVAL);
+    // burst queue: arguments are checked before any device call
+    sccsum_burst* b = reinterpret_cast<sccsum_burst*>(1);
+    EXPECT(sccsum_burst_create(0, 7, 1 << 20, 64, 0, 2, noop, nullptr, &b) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_create(0, 0, 1 << 20, 64, 0, 0, noop, nullptr, &b) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_create(0, 0, 1 << 20, 64, 0, 65, noop, nullptr, &b) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_create(0, 0, 1 << 20, 0, 0, 2, noop, nullptr, &b) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_create(0, 0, 32, 64, 0, 2, noop, nullptr, &b) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_create(0, 0, uint64_t(1) << 32, 64, 0, 2, noop, nullptr, &b) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_create(0, 0, 1 << 20, 64, 0, 2, nullptr, nullptr, &b) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_create(0, 0, 1 << 20, 64, 0, 2, noop, nullptr, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_submit(nullptr, nullptr, 0, 0, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_submit_mapped(nullptr, nullptr, 0, 0, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_poll(nullptr, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_drain(nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_burst_destroy(nullptr) == SCCSUM_OK);
+    // host pipeline
+    sccsum_pipeline* p = nullptr;
+    EXPECT(sccsum_pipeline_create(0, 1 << 20, 1024, 0, &p) == SCCSUM_EINVAL);
+    EXPECT(sccsum_pipeline_create(0, 1 << 20, 1024, 17, &p) == SCCSUM_EINVAL);
+    EXPECT(sccsum_pipeline_create(0, 32, 1024, 2, &p) == SCCSUM_EINVAL);
+    EXPECT(sccsum_pipeline_create(0, 1 << 20, 0, 2, &p) == SCCSUM_EINVAL);
+    EXPECT(sccsum_pipeline_create(0, 1 << 20, 1024, 2, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_host_alloc(nullptr, 64) == SCCSUM_EINVAL);
+    // diagnostics: thread-local knobs validate their ranges
+    EXPECT(sccsum_set_kernel_variant(5) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_kernel_variant(20) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_kernel_variant(16) == SCCSUM_OK && sccsum_set_kernel_variant(0) == SCCSUM_OK);
+    EXPECT(sccsum_set_blocks_per_cu(0) == SCCSUM_EINVAL && sccsum_set_blocks_per_cu(33) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_group_units(3) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_tile_packets(65) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_tile_bytes(-1) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_tail_tiles(0, 4) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_dynamic_tiles(2) == SCCSUM_EINVAL);
+    // host arithmetic and strings
+    EXPECT(sccsum_pseudo_seed(1, 2, 17, 8) == 28u);
+    EXPECT(sccsum_pseudo_seed(0xffffffffu, 0xffffffffu, 255, 0xffff) <= 0xffffu);
+    EXPECT(std::strcmp(sccsum_strerror(SCCSUM_EBUSY), "every batch slot is in flight") == 0);
+    EXPECT(std::strcmp(sccsum_strerror(-99), "unknown sccsum error") == 0);
+    EXPECT(sccsum_abi_version() == SCCSUM_ABI_VERSION);
+    if (failures) {
+        std::printf("abi_validate: %d FAILED\n", failures);
+        return 1;
+    }
+    std::printf("abi_validate: OK\n");
+    return 0;
+}

@@ -1,0 +1,41 @@
+"""bench.py --gpus N without torchrun starts N rank processes itself
+(bench.launch_ranks): independent shards, gloo control plane, rank 0 prints
+one line with n_gpus = N (reference analogue: one engine per
+shard, src/net/net.cc:309-341)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    return lines[0]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_starts_n_ranks_without_device(n):
+    d = _bench("--gpus", str(n), "--dry-run")
+    assert d["dry_run"] and d["n_gpus"] == n
+    assert [r["rank"] for r in d["ranks"]] == list(range(n))
+    assert [r["local"] for r in d["ranks"]] == [str(i) for i in range(n)]
+    assert len({r["pid"] for r in d["ranks"]}) == n  # one process per rank
+
+
+@pytest.mark.gpu
+def test_launcher_two_ranks_on_the_gpu():
+    """Two rank processes on the box's one GPU (a rehearsal of the driver's
+    --gpus N run: each rank builds, checks and times its own shard)."""
+    d = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--packets", "65536", "--rotate", "1", "--no-cpu",
+               timeout=300)
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["config"]["global_batch"] == 2 * 65536

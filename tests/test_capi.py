@@ -107,7 +107,8 @@ def test_burst_argument_validation_without_device():
                  (0, 0, 1 << 20, 64, 0, 0),     # depth 0
                  (0, 0, 1 << 20, 64, 0, 65),    # depth > 64
                  (0, 0, 1 << 20, 0, 0, 2),      # no packets per batch
-                 (0, 1, 32, 64, 0, 2)):         # batch under 64 bytes
+                 (0, 1, 32, 64, 0, 2),          # batch under 64 bytes
+                 (0, 1, 1 << 32, 64, 0, 2)):    # batch offsets are 32-bit: 4 GiB is too large
         assert lib.sccsum_burst_create(*args, cb, None, ctypes.byref(out)) == native.SCCSUM_EINVAL
     assert lib.sccsum_burst_create(0, 0, 1 << 20, 64, 0, 2, None, None, ctypes.byref(out)) == native.SCCSUM_EINVAL
     assert lib.sccsum_burst_submit(None, None, 0, 0, None) == native.SCCSUM_EINVAL

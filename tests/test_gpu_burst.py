@@ -170,3 +170,72 @@ def test_gather_kernel_any_alignment(dev):
         for i in range(n):
             want[int(dst_off[i]):int(dst_off[i]) + int(lens[i])] = host[int(src_off[i]):int(src_off[i]) + int(lens[i])]
         assert np.array_equal(dst.cpu().numpy(), want)
+
+
+def test_pinned_view_outlives_pool(dev):
+    """A view of a pinned_empty pool keeps the pinned block alive after the
+    pool array itself is dropped (the block is freed with its last view)."""
+    import gc
+
+    from seastar_amd import pipeline
+
+    pool = pipeline.pinned_empty(1 << 20)
+    pool[:] = 7
+    view = pool[4096:8192]
+    addr = view.ctypes.data
+    del pool
+    gc.collect()
+    assert pipeline.is_pinned(view)
+    view[:] = np.arange(view.size, dtype=np.uint8)
+    assert view.ctypes.data == addr and int(view[255]) == 255
+    # the view is still good for a zero-copy submit
+    q = BurstQueue(native.PIPE_SPANS, batch_bytes=64 << 10, batch_packets=8, max_delay_ns=0, depth=2)
+    q.submit([view[:1500]], 0, mapped=True)
+    q.drain()
+    assert int(q.results[0]) == int(oracle.batch_spans(view.copy(), np.zeros(1, np.uint64),
+                                                       np.full(1, 1500, np.uint32))[0])
+    q.close()
+    del view
+    gc.collect()
+
+
+def test_mapped_submit_rejects_pageable_memory(dev):
+    q = BurstQueue(native.PIPE_SPANS, batch_bytes=64 << 10, batch_packets=8, max_delay_ns=0, depth=2)
+    with pytest.raises(ValueError):
+        q.submit([np.zeros(100, np.uint8)], mapped=True)  # ordinary pageable numpy memory
+    with pytest.raises(ValueError):
+        q.submit([b"\x00" * 100], mapped=True)
+    q.close()
+
+
+def test_callback_reentrancy(dev):
+    """A completion callback that polls / drains is refused (SCCSUM_EINVAL),
+    one that submits works; every batch is delivered exactly once, in order."""
+    import ctypes
+
+    lib = native.load()
+    seen, inner = [], []
+    holder = {}
+
+    def on_done(first, r, s):
+        seen.append((first, r.copy()))
+        inner.append(lib.sccsum_burst_poll(holder["q"]._h, None))
+        inner.append(lib.sccsum_burst_drain(holder["q"]._h))
+        if first < 40:  # resubmit from inside the callback
+            holder["q"].submit([np.full(64, first, np.uint8)])
+
+    q = BurstQueue(native.PIPE_SPANS, batch_bytes=64 << 10, batch_packets=4, max_delay_ns=0, depth=3, on_done=on_done)
+    holder["q"] = q
+    for i in range(20):
+        while q.submit([np.full(64, i, np.uint8)]) is None:
+            q.poll()
+        q.poll()
+    for _ in range(20):
+        q.drain()
+    firsts = [f for f, _ in seen]
+    assert firsts == sorted(firsts) and len(set(firsts)) == len(firsts)
+    total = sum(r.size for _, r in seen)
+    assert firsts[0] == 0 and total == firsts[-1] + seen[-1][1].size  # consecutive tickets, none lost or repeated
+    assert all(code == native.SCCSUM_EINVAL for code in inner)
+    q.close()
+    assert ctypes.sizeof(ctypes.c_void_p) == 8

@@ -1,0 +1,253 @@
+// store_probe — what do the in-place fill's scattered field stores cost?
+// (development probe, not part of libsccsum)
+//
+// 1,048,576 "frames" of 1500 B back to back in each of R = 4 rotated 1.5 GB
+// buffers.  Variants (one launch per buffer, R launches timed with events):
+//   read      nt 16-B stream of the whole buffer (the verify kernel's floor)
+//   st2       store-only: one 2-byte store at frame+10 and one at frame+26
+//   st16      store-only: the aligned 16-B unit(s) holding those fields, rewritten whole
+//   st64      store-only: the aligned 64-B line holding frame+10, written whole by 4 lanes
+//   st128     store-only: the aligned 128-B line, written whole by 8 lanes
+//   rd+st2    each wave streams a tile of 64 frames (nt), then lane i stores frame i's two fields
+//   rd+st16   ... and rewrites the 16-B units holding them from the loaded bytes
+//   rd+st64   ... rewrites the aligned 64-B line holding frame+10 (bytes as read)
+//   rd+st2d   as rd+st2, but the tile's first line of each frame is loaded default-policy
+// usage: store_probe [reps]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            std::exit(1);                                                                  \
+        }                                                                                  \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint64_t kFrames = 1 << 20;
+constexpr uint64_t kFrame = 1500;
+constexpr uint64_t kBytes = kFrames * kFrame;
+
+__global__ __launch_bounds__(256) void k_read(const u32x4* __restrict__ src, uint64_t units, uint64_t* sink) {
+    uint64_t acc = 0;
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < units; i += stride) {
+        const u32x4 a = __builtin_nontemporal_load(src + i);
+        acc += uint64_t(a.x) + a.y + a.z + a.w;
+    }
+    if (acc == 0x123456789ull) sink[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_st2(uint8_t* buf, uint64_t n, uint16_t v) {
+    const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint8_t* f = buf + i * kFrame;
+    *reinterpret_cast<uint16_t*>(f + 10) = v;
+    *reinterpret_cast<uint16_t*>(f + 26) = v;
+}
+
+__global__ __launch_bounds__(256) void k_st16(uint8_t* buf, uint64_t n, uint32_t v) {
+    const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a = reinterpret_cast<uint64_t>(buf) + i * kFrame;
+    u32x4* u0 = reinterpret_cast<u32x4*>((a + 10) & ~15ull);
+    u32x4* u1 = reinterpret_cast<u32x4*>((a + 26) & ~15ull);
+    *u0 = u32x4{v, v, v, v};
+    if (u1 != u0) *u1 = u32x4{v, v, v, v};
+}
+
+template <int LINE>
+__global__ __launch_bounds__(256) void k_stline(uint8_t* buf, uint64_t n, uint32_t v) {
+    constexpr int P = LINE / 16;  // lanes per frame
+    const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    const uint64_t i = t / P;
+    if (i >= n) return;
+    const uint64_t a = (reinterpret_cast<uint64_t>(buf) + i * kFrame + 10) & ~uint64_t(LINE - 1);
+    reinterpret_cast<u32x4*>(a)[t % P] = u32x4{v, v, v, v};
+}
+
+// second pass: 4 lanes per frame read-modify-write the aligned 64-B line holding frame+10
+__global__ __launch_bounds__(256) void k_st64rw(uint8_t* buf, uint64_t n, uint32_t v) {
+    const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    const uint64_t i = t / 4;
+    if (i >= n) return;
+    const uint64_t a = (reinterpret_cast<uint64_t>(buf) + i * kFrame + 10) & ~uint64_t(63);
+    u32x4* L = reinterpret_cast<u32x4*>(a);
+    u32x4 x = L[t % 4];
+    x.z ^= v;
+    L[t % 4] = x;
+}
+
+// MODE 0 = 2-byte field stores, 1 = whole 16-B units re-read first, 2 = whole 64-B line re-read first,
+// 4 = 2-byte stores after a re-read of their units, 5 = whole 16-B units from registers (no re-read);
+// DFL = frame's first line default policy
+template <int MODE, bool DFL>
+__global__ __launch_bounds__(256) void k_rdst(uint8_t* buf, uint64_t n, uint64_t* sink) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t(blockIdx.x) * 256 + threadIdx.x) >> 6;
+    const uint64_t nw = uint64_t(gridDim.x) * 4;
+    const uint64_t tiles = n / 64;
+    uint32_t acc = 0;
+    for (uint64_t t = wave; t < tiles; t += nw) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(buf + t * 64 * kFrame);
+        constexpr uint32_t units = 64 * kFrame / 16;  // 6000
+        for (uint32_t u = lane; u < units; u += 64 * 8) {
+            u32x4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t uu = u + 64 * k;
+                if (uu < units) {
+                    const bool head = DFL && ((uu * 16u) % kFrame) < 16u;
+                    v[k] = head ? base[uu] : __builtin_nontemporal_load(base + uu);
+                } else {
+                    v[k] = u32x4{0, 0, 0, 0};
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
+        }
+        uint8_t* f = buf + (t * 64 + lane) * kFrame;
+        const uint16_t w = uint16_t(acc);
+        if (MODE == 0) {
+            *reinterpret_cast<uint16_t*>(f + 10) = w;
+            *reinterpret_cast<uint16_t*>(f + 26) = w;
+        } else if (MODE == 1) {
+            const uint64_t a = reinterpret_cast<uint64_t>(f);
+            u32x4* u0 = reinterpret_cast<u32x4*>((a + 10) & ~15ull);
+            u32x4* u1 = reinterpret_cast<u32x4*>((a + 26) & ~15ull);
+            u32x4 x = *u0;
+            x.x ^= acc | 1u;  // re-read and rewrite whole (modified: the store cannot be elided)
+            *u0 = x;
+            if (u1 != u0) {
+                u32x4 y = *u1;
+                y.y ^= acc | 1u;
+                *u1 = y;
+            }
+        } else if (MODE == 4) {
+            const uint64_t a = reinterpret_cast<uint64_t>(f);
+            const u32x4 x0 = *reinterpret_cast<const u32x4*>((a + 10) & ~15ull);
+            const u32x4 x1 = *reinterpret_cast<const u32x4*>((a + 26) & ~15ull);
+            const uint16_t w2 = uint16_t(w + (x0.x == 0x5a5a5a5au) + (x1.y == 0x5a5a5a5au));  // stores wait for the loads
+            *reinterpret_cast<uint16_t*>(f + 10) = w2;
+            *reinterpret_cast<uint16_t*>(f + 26) = w2;
+        } else if (MODE == 5) {
+            const uint64_t a = reinterpret_cast<uint64_t>(f);
+            u32x4* u0 = reinterpret_cast<u32x4*>((a + 10) & ~15ull);
+            u32x4* u1 = reinterpret_cast<u32x4*>((a + 26) & ~15ull);
+            *u0 = u32x4{acc, acc, acc, acc};
+            if (u1 != u0) *u1 = u32x4{acc, w, acc, w};
+        } else if (MODE == 9) {  // nontemporal 2-byte stores
+            __builtin_nontemporal_store(w, reinterpret_cast<uint16_t*>(f + 10));
+            __builtin_nontemporal_store(w, reinterpret_cast<uint16_t*>(f + 26));
+        } else if (MODE == 6 || MODE == 7 || MODE == 8) {
+            // whole aligned 32 / 64 / 128-byte block(s) holding both fields, from registers (no re-read)
+            constexpr uint64_t B = MODE == 6 ? 32 : (MODE == 7 ? 64 : 128);
+            const uint64_t a = reinterpret_cast<uint64_t>(f);
+            const uint64_t lo = (a + 10) & ~(B - 1), hi = (a + 27) & ~(B - 1);
+            for (uint64_t blk = lo; blk <= hi; blk += B) {
+#pragma unroll
+                for (uint64_t k = 0; k < B / 16; ++k) reinterpret_cast<u32x4*>(blk)[k] = u32x4{acc, w, acc, w};
+            }
+        } else if (MODE == 2) {
+            const uint64_t a = (reinterpret_cast<uint64_t>(f) + 10) & ~63ull;
+            u32x4* L = reinterpret_cast<u32x4*>(a);
+            u32x4 x0 = L[0], x1 = L[1], x2 = L[2], x3 = L[3];
+            x0.x ^= acc | 1u;
+            L[0] = x0;
+            L[1] = x1;
+            L[2] = x2;
+            L[3] = x3;
+        }
+    }
+    if (MODE == 10 || MODE == 12) {  // deferred: this wave's stores after its whole stream
+        for (uint64_t t = wave; t < tiles; t += nw) {
+            uint8_t* f = buf + (t * 64 + lane) * kFrame;
+            if (MODE == 12) {
+                *reinterpret_cast<uint16_t*>(f + 10) = uint16_t(acc);
+                *reinterpret_cast<uint16_t*>(f + 26) = uint16_t(acc);
+            } else {
+                const uint64_t a = reinterpret_cast<uint64_t>(f);
+                u32x4* u0 = reinterpret_cast<u32x4*>((a + 10) & ~15ull);
+                u32x4* u1 = reinterpret_cast<u32x4*>((a + 26) & ~15ull);
+                *u0 = u32x4{acc, acc, acc, acc};
+                if (u1 != u0) *u1 = u32x4{acc, 1u, acc, 1u};
+            }
+        }
+    }
+    if (acc == 0x12345u) sink[0] = acc;
+}
+
+int main(int argc, char** argv) {
+    const int reps = argc > 1 ? std::atoi(argv[1]) : 3;
+    constexpr int R = 4;
+    uint8_t* bufs[R];
+    for (int r = 0; r < R; ++r) {
+        CK(hipMalloc(&bufs[r], kBytes + 4096));
+        CK(hipMemset(bufs[r], r + 1, kBytes + 4096));
+    }
+    uint64_t* sink;
+    CK(hipMalloc(&sink, 64));
+    int cus = 256;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const unsigned g_frames = unsigned((kFrames + 255) / 256);
+    auto run = [&](const char* name, auto launch) {
+        for (int r = 0; r < R; ++r) launch(bufs[r]);  // warm
+        CK(hipDeviceSynchronize());
+        float best = 1e30f;
+        for (int k = 0; k < reps; ++k) {
+            CK(hipEventRecord(e0, 0));
+            for (int r = 0; r < R; ++r) launch(bufs[r]);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            best = ms < best ? ms : best;
+        }
+        CK(hipGetLastError());
+        const double us = best * 1e3 / R;
+        std::printf("%-10s %9.1f us/launch  %7.0f GB/s of frame bytes\n", name, us, kBytes / us / 1e3);
+        std::fflush(stdout);
+    };
+    run("read", [&](uint8_t* b) { k_read<<<cus * 8, 256>>>(reinterpret_cast<const u32x4*>(b), kBytes / 16, sink); });
+    run("st2", [&](uint8_t* b) { k_st2<<<g_frames, 256>>>(b, kFrames, 0x1234); });
+    run("st16", [&](uint8_t* b) { k_st16<<<g_frames, 256>>>(b, kFrames, 0x1234); });
+    run("st64", [&](uint8_t* b) { k_stline<64><<<g_frames * 4, 256>>>(b, kFrames, 0x1234); });
+    run("st128", [&](uint8_t* b) { k_stline<128><<<g_frames * 8, 256>>>(b, kFrames, 0x1234); });
+    run("rd+st2", [&](uint8_t* b) { k_rdst<0, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd+st16", [&](uint8_t* b) { k_rdst<1, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd+st64", [&](uint8_t* b) { k_rdst<2, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd+st2d", [&](uint8_t* b) { k_rdst<0, true><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd+st16d", [&](uint8_t* b) { k_rdst<1, true><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd+st64d", [&](uint8_t* b) { k_rdst<2, true><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd+st2r", [&](uint8_t* b) { k_rdst<4, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd+st16n", [&](uint8_t* b) { k_rdst<5, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd+st32n", [&](uint8_t* b) { k_rdst<6, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd+st64n", [&](uint8_t* b) { k_rdst<7, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd+st128n", [&](uint8_t* b) { k_rdst<8, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd8w only", [&](uint8_t* b) { k_rdst<3, false><<<cus * 2, 256>>>(b, kFrames, sink); });
+    run("rd8w+st16", [&](uint8_t* b) { k_rdst<1, false><<<cus * 2, 256>>>(b, kFrames, sink); });
+    run("rd8w+st64n", [&](uint8_t* b) { k_rdst<7, false><<<cus * 2, 256>>>(b, kFrames, sink); });
+    run("rd+st2nt", [&](uint8_t* b) { k_rdst<9, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd;st2", [&](uint8_t* b) {
+        k_read<<<cus * 8, 256>>>(reinterpret_cast<const u32x4*>(b), kBytes / 16, sink);
+        k_st2<<<g_frames, 256>>>(b, kFrames, 0x1234);
+    });
+    run("rd;st64rw", [&](uint8_t* b) {
+        k_read<<<cus * 8, 256>>>(reinterpret_cast<const u32x4*>(b), kBytes / 16, sink);
+        k_st64rw<<<g_frames * 4, 256>>>(b, kFrames, 0x1234);
+    });
+    run("st64rw", [&](uint8_t* b) { k_st64rw<<<g_frames * 4, 256>>>(b, kFrames, 0x1234); });
+    run("rd+dfr16", [&](uint8_t* b) { k_rdst<10, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd+dfr2", [&](uint8_t* b) { k_rdst<12, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rd8w+dfr16", [&](uint8_t* b) { k_rdst<10, false><<<cus * 2, 256>>>(b, kFrames, sink); });
+    run("rd only", [&](uint8_t* b) { k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+    return 0;
+}
