@@ -53,7 +53,7 @@ def flat_kernel(ipv4: bool, fill: bool, n: int, nbytes: int) -> str:
     the next chunk in flight), as rocprofv3 names it."""
     big = n >= (512 << 10) and nbytes >= (256 << 20)
     u, pipe = (16, "false") if big else (8, "true")
-    return f"csum_flat_kernel<{u}, {str(ipv4).lower()}, {str(fill).lower()}, {pipe}>"
+    return f"csum_flat_kernel<{u}, {str(ipv4).lower()}, {str(fill).lower()}, {pipe}, false>"
 
 
 def parse():
@@ -72,6 +72,9 @@ def parse():
                     help="udp1500 = the metric's config (cfg 2, default); mixed = cfg 3; tcp64k = cfg 4 "
                          "(per-GPU shard); e2e = cfg 5 (pinned host mbufs, PCIe-inclusive); fill = cfg 2 tx "
                          "generate with in-place write-back (sccsum_ipv4_fill); sweep = rate against batch size")
+    ap.add_argument("--launch", default="multi", choices=["multi", "single"],
+                    help="udp1500: one sccsum_ipv4_frames_multi launch per step over the tx and rx batches (multi, "
+                         "default) or one sccsum_ipv4_frames launch per batch (single)")
     ap.add_argument("--dry-run", action="store_true",
                     help="multi-rank plumbing only: launch, rendezvous, barrier, max-over-ranks, one line; "
                          "no device call (the CPU test of the launcher)")
@@ -331,35 +334,43 @@ def run_udp1500(args, world, rank, dev):
     for r in range(R):
         tx = devsynth.udp_frames(n, FRAME, seed=SEED + 7919 * rank + 104723 * r, device=dev)
         first = batch.ipv4_frames(tx, out2=out_tx)
-        LAUNCHES.add(kern)
+        LAUNCHES.add(flat_kernel(True, False, n, n * FRAME))
         rx = devsynth.store_checksums(tx, first)
         devsynth.corrupt(rx, bad, byte=700)
         txs.append(tx)
         rxs.append(rx)
         sts.append(torch.empty(n, dtype=torch.uint8, device=dev))
     stream = torch.cuda.current_stream()
+    multi = args.launch == "multi"
+    per_step = 1 if multi else 2  # launches per step
+    if multi:  # the tx and rx batches of a step form ONE launch of 2 * n frames
+        kern = flat_kernel(True, False, 2 * n, 2 * n * FRAME)
 
     def step(k):
         r = k % R
-        batch.ipv4_frames(txs[r], out2=out_tx, stream=stream)
-        batch.ipv4_frames(rxs[r], out2=out_rx, status=sts[r], stream=stream)
+        if multi:
+            batch.ipv4_frames_multi([(txs[r], out_tx, None), (rxs[r], out_rx, sts[r])], stream=stream)
+        else:
+            batch.ipv4_frames(txs[r], out2=out_tx, stream=stream)
+            batch.ipv4_frames(rxs[r], out2=out_rx, status=sts[r], stream=stream)
 
     warm = max(args.warmup, R)
     for k in range(warm):
         step(k)
-    LAUNCHES.add(kern, 2 * warm)
+    LAUNCHES.add(kern, per_step * warm)
     torch.cuda.synchronize()
-    # sanity: every uncorrupted rx frame verifies, every corrupted one fails
+    # sanity: every uncorrupted rx frame verifies, every corrupted one fails; the tx outputs match the generate pass
     for st_rx in sts:
         n_fail = int(((st_rx & 2) == 0).sum())
         assert n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
-    sel = LAUNCHES.select(kern, 2 * args.steps)
+    sel = LAUNCHES.select(kern, per_step * args.steps)
     wall, step_s = timed(step, args.steps, 0, world, stream)
-    LAUNCHES.add(kern, 2 * args.steps)
-    avg_launch_s = step_s / 2
+    LAUNCHES.add(kern, per_step * args.steps)
+    avg_launch_s = step_s / per_step
 
     value = world * 2 * n * FRAME * args.steps / wall / 2**30
-    alg = n * (FRAME + META_BYTES + 4) + n // 2  # + status byte on the rx launch (avg)
+    # per launch: every frame byte + 12 B metadata + 4 B of results (+ 1 B status per rx frame)
+    alg = 2 * n * (FRAME + META_BYTES + 4) + n if multi else n * (FRAME + META_BYTES + 4) + n // 2
     ceiling = read_ceiling(txs[0].data, txs[0].bytes_len, stream)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -369,9 +380,12 @@ def run_udp1500(args, world, rank, dev):
              {"workload": "cfg2: 1,048,576 x 1500 B IPv4/UDP frames per GPU in HBM (offset/length array); "
                           "step = generate (IP+UDP csum) + verify (1% corrupted) pass",
               "packets_per_gpu": n, "frame_bytes": FRAME,
+              "launch": ("one sccsum_ipv4_frames_multi launch per step over the tx and rx batches" if multi
+                         else "one sccsum_ipv4_frames launch per batch (2 per step)"),
               "rotation": f"{R} distinct tx/rx batch pairs launched in turn ({2 * R * n * FRAME / 1e9:.1f} GB per GPU)",
               "global_batch": n * world, "parallelism": f"{world} independent shards, no collective"},
-             roofline(alg, avg_launch_s, "udp1500", kern + " (sccsum_ipv4_frames)", sel, args,
+             roofline(alg, avg_launch_s, "udp1500", kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi
+                                                                   else " (sccsum_ipv4_frames)"), sel, args,
                       {"measured_read_ceiling_GBps": round(ceiling, 1)}), cpu)
 
 
@@ -466,7 +480,10 @@ def run_fill(args, world, rank, dev):
              {"workload": "cfg2 tx: 1500 B IPv4/UDP frames, IP + UDP checksums generated and stored in place",
               "packets_per_gpu": n, "rotation": f"{R} distinct batches launched in turn",
               "parallelism": f"{world} independent shards"},
-             roofline(alg, launch_s, "fill", kern + " (sccsum_ipv4_fill)", sel, args))
+             roofline(alg, launch_s, "fill", kern + " + fill_store_kernel (sccsum_ipv4_fill: generate pass, "
+                                                    "then the field-store pass)", sel, args,
+                      {"trace_select_extra": [{"kernel": "fill_store_kernel", "skip": sel["skip"],
+                                               "count": sel["count"]}]}))
 
 
 def run_sweep(args, world, rank, dev):
@@ -516,8 +533,31 @@ def run_sweep(args, world, rank, dev):
             e1.record(stream)
         torch.cuda.synchronize()
         graph_s = e0.elapsed_time(e1) / 1e3 / (reps * k)
+        # 16 queues per launch (sccsum_ipv4_frames_multi): 16 slices of B packets each
+        km = max(1, k // 16)
+        outs16 = [torch.empty(2 * B, dtype=torch.int16, device=dev) for _ in range(16)]
+        sts16 = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(16)]
+        batch.ipv4_frames_multi([(slices[q % nb], outs16[q], sts16[q]) for q in range(16)], stream=stream)
+        torch.cuda.synchronize()
+        gm = torch.cuda.CUDAGraph()  # captured, so the host's Python cost per call is not on the clock
+        with torch.cuda.graph(gm, stream=stream):
+            for j in range(km):
+                batch.ipv4_frames_multi([(slices[(16 * j + q) % nb], outs16[q], sts16[q]) for q in range(16)],
+                                        stream=stream)
+        with torch.cuda.stream(stream):
+            gm.replay()
+            torch.cuda.synchronize()
+            e0.record(stream)
+            for _ in range(3):
+                gm.replay()
+            e1.record(stream)
+        torch.cuda.synchronize()
+        multi_s = e0.elapsed_time(e1) / 1e3 / (3 * km)
+        del gm
         bytes_b = B * FRAME
         res.append({"packets": B, "bytes": bytes_b, "launches": k,
+                    "multi16_us_per_launch": round(multi_s * 1e6, 2),
+                    "multi16_GiBps": round(16 * bytes_b / multi_s / 2**30, 1),
                     "eager_us": round(eager_s * 1e6, 2), "eager_GiBps": round(bytes_b / eager_s / 2**30, 1),
                     "eager_host_us_per_launch": round(host_s / k * 1e6, 2),
                     "graph_us": round(graph_s * 1e6, 2), "graph_GiBps": round(bytes_b / graph_s / 2**30, 1),

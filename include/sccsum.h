@@ -21,6 +21,7 @@
  *                             L4 pseudo-header + segment  include/seastar/net/tcp.hh:876-883 }
  *   sccsum_fragments    N x checksummer::sum(const packet&)  src/net/ip_checksum.cc:64-68
  *                       (fragment lists with the odd-byte carry) + get()
+ *   sccsum_*_multi      the above for up to 16 batches (rx queues) in one launch
  *   sccsum_pseudo_seed  ipv4_traits::{tcp,udp}_pseudo_header_checksum
  *                       include/seastar/net/ip.hh:70-75 (host arithmetic, O(1))
  *
@@ -120,6 +121,31 @@ int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len,
                        uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len,
                        void* stream);
 
+/* ---- Several batches in one launch ------------------------------------------
+ * Up to SCCSUM_MAX_BATCHES independent batches (e.g. the rx queues of a shard,
+ * or a step's tx and rx halves) checksummed by ONE kernel launch: each batch
+ * is exactly what sccsum_spans / sccsum_ipv4_frames would compute for it (its
+ * own bytes, offsets, lengths, seeds and outputs; same memory contract), but
+ * the launch's ramp and drain (~6-7 us on MI355X) are paid once.  batches is
+ * a HOST array (read before the call returns); empty batches are skipped.
+ * Frames take no seeds (d_seed must be NULL).  SCCSUM_EINVAL for nbatch >
+ * SCCSUM_MAX_BATCHES or a bad batch. */
+#define SCCSUM_MAX_BATCHES 16
+
+typedef struct sccsum_batch {
+    const void* d_bytes;
+    uint64_t bytes_len;
+    const uint64_t* d_off;
+    const uint32_t* d_len;
+    const uint32_t* d_seed; /* spans: optional per-packet seed; frames: NULL */
+    void* d_out;            /* spans: uint16_t[n]; frames: uint16_t[2n] */
+    uint8_t* d_status;      /* optional */
+    uint64_t n;
+} sccsum_batch;
+
+int sccsum_spans_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len, void* stream);
+int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len, void* stream);
+
 /* Checksum n packets that are FRAGMENT LISTS, like checksummer::sum(const
  * packet&) (src/net/ip_checksum.cc:64-68): packet i is the concatenation of
  * fragments d_pkt_first[i] .. d_pkt_first[i+1]-1, fragment j being
@@ -185,10 +211,12 @@ int sccsum_ipv4_frames_rss(const void* d_bytes, uint64_t bytes_len, const uint64
  * after 4*ihl; other protocols' L4 is left alone, as is any frame that is
  * malformed (as in sccsum_ipv4_frames) or too short to hold the field.
  *   mode: SCCSUM_FILL_IP and/or one of SCCSUM_FILL_L4 / SCCSUM_FILL_L4_PSEUDO
- *         (| SCCSUM_FILL_TSO).  FILL_L4 reads every byte (batch kernel);
- *         the others read only the 20-byte header.
+ *         (| SCCSUM_FILL_TSO).  FILL_L4 reads every byte (the flat kernel
+ *         generates into d_out2, then a second pass stores the fields); the
+ *         others read only the 20-byte header.
  *   d_out2[2i] / [2i+1] = the IP / L4 values stored (0 where nothing was
- *         stored); may be NULL.
+ *         stored); REQUIRED with SCCSUM_FILL_L4 (the two passes hand the
+ *         values over in it), else may be NULL.
  *   d_status[i] = SCCSUM_ST_OK if the IP field was written, SCCSUM_ST_L4_OK
  *         if the L4 field was written, plus MALFORMED / RANGE; may be NULL.
  * Frames must not overlap each other. */

@@ -44,10 +44,6 @@ int sccsum_set_tile_packets(int packets);
 /* Flat kernel: target bytes per tile (default 0 = only the packet cap). */
 int sccsum_set_tile_bytes(int bytes);
 
-/* Flat kernel guided tail: the last tiles hold B / divisor packets and cover
- * about per_slot such tiles per wave slot (default 1 = uniform tiles, 4). */
-int sccsum_set_tail_tiles(int divisor, int per_slot);
-
 /* Flat kernel: tiles dequeued from per-stream counters (1, the default) or
  * dealt round robin (0). */
 int sccsum_set_dynamic_tiles(int on);

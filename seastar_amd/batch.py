@@ -102,16 +102,55 @@ def ipv4_frames(batch: PacketBatch, out2: torch.Tensor | None = None, status: to
     return out2[: 2 * n].view(n, 2) if n else out2[:0].view(0, 2)
 
 
+def _multi(fn, name, items, max_len, stream, width, with_seed):
+    lib = native.load()
+    if len(items) > native.MAX_BATCHES:
+        raise ValueError(f"at most {native.MAX_BATCHES} batches per launch")
+    arr = (native.Batch * max(len(items), 1))()
+    outs = []
+    for i, it in enumerate(items):
+        b, out, status = it[0], it[1], it[2]
+        seeds = it[3] if len(it) > 3 else None
+        if out is None:
+            out = torch.empty(max(width * b.n, width), dtype=torch.int16, device=b.device)
+        if seeds is not None:
+            assert with_seed and seeds.dtype == torch.int32 and seeds.numel() >= b.n
+        arr[i] = native.Batch(ctypes_ptr(b.data), b.bytes_len, ctypes_ptr(b.off), ctypes_ptr(b.length), _ptr(seeds),
+                              ctypes_ptr(out), _ptr(status), b.n)
+        outs.append(out)
+    native.check(fn(ctypes.cast(arr, ctypes.c_void_p), len(items), max_len, _stream(stream)), name)
+    return outs
+
+
+def ipv4_frames_multi(items, stream=None) -> list:
+    """sccsum_ipv4_frames_multi: items = [(PacketBatch, out2 | None, status | None), ...]
+    (<= 16) in ONE launch; returns the [n, 2] int16 outputs per batch."""
+    ml = max((it[0].max_len for it in items), default=0)
+    outs = _multi(native.load().sccsum_ipv4_frames_multi, "sccsum_ipv4_frames_multi", items, ml, stream, 2, False)
+    return [o[: 2 * it[0].n].view(it[0].n, 2) for o, it in zip(outs, items)]
+
+
+def spans_multi(items, stream=None) -> list:
+    """sccsum_spans_multi: items = [(PacketBatch, out | None, status | None[, seeds int32]), ...]."""
+    ml = max((it[0].max_len for it in items), default=0)
+    outs = _multi(native.load().sccsum_spans_multi, "sccsum_spans_multi", items, ml, stream, 1, True)
+    return [o[: it[0].n] for o, it in zip(outs, items)]
+
+
 def ipv4_fill(batch: PacketBatch, mode: int = native.FILL_IP | native.FILL_L4, out2: torch.Tensor | None = None,
               status: torch.Tensor | None = None, stream=None) -> torch.Tensor | None:
     """sccsum_ipv4_fill: generate checksums and store them in batch.data in place.
     Returns the [n, 2] values stored when out2 is given (else None)."""
     lib = native.load()
     n = batch.n
+    given = out2
+    if out2 is None and mode & native.FILL_L4:  # the generate and store passes hand the values over in out2
+        out2 = torch.empty(max(2 * n, 2), dtype=torch.int16, device=batch.device)
     code = lib.sccsum_ipv4_fill(
         ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length),
         _ptr(out2), _ptr(status), n, batch.max_len, mode, _stream(stream),
     )
+    out2 = given
     native.check(code, "sccsum_ipv4_fill")
     return None if out2 is None else out2[: 2 * n].view(n, 2)
 

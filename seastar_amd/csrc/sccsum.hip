@@ -292,9 +292,7 @@ __device__ __forceinline__ uint32_t unit_part(const u32x4& v, int lo, int hi) {
 }
 
 constexpr uint32_t kExactMax = 131072;  // fast path keeps exact 32-bit sums up to this length
-#ifndef SCCSUM_FILL_WHOLE
-#define SCCSUM_FILL_WHOLE 1  // in-place fill: store whole 16-byte units where safe (else the field bytes alone)
-#endif
+
 // tile-head counters: each on its own 256-byte line (atomics to one line
 // serialise at the memory side: ~12 ns each chip-wide)
 constexpr uint32_t kHeadStride = 64;                      // uint32 words between counters
@@ -464,6 +462,25 @@ __device__ __forceinline__ uint32_t header_dword(const u32x4 (&h)[4], uint32_t h
 
 constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B) between packets
 
+// The batches one flat-kernel launch works through: up to kMaxQueues
+// independent batches (rx / tx queues, the tx and rx halves of a step), each
+// with its own bytes, offsets, lengths, seeds and outputs.  Tiles are numbered
+// across the batches (tile0 = prefix of their tile counts), so one grid, one
+// ramp and one drain serve them all.  Passed by value (kernel arguments).
+constexpr uint32_t kMaxQueues = 16;
+struct Queues {
+    uint32_t nq;
+    uint64_t tile0[kMaxQueues + 1];
+    const uint8_t* bytes[kMaxQueues];
+    uint64_t bytes_len[kMaxQueues];
+    const uint64_t* off[kMaxQueues];
+    const uint32_t* len[kMaxQueues];
+    const uint32_t* seed[kMaxQueues];
+    uint16_t* out[kMaxQueues];
+    uint8_t* status[kMaxQueues];
+    uint64_t n[kMaxQueues];
+};
+
 // Flat kernel.  Wave w owns tiles of B <= 64 consecutive packets (one per
 // lane); the bytes are streamed per RUN, not per packet: a run is a maximal
 // sequence of tile packets whose 16-byte unit spans go forward with gaps of
@@ -481,12 +498,8 @@ constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B)
 // Layouts that do not run forward (shuffled offsets) degrade to one run per
 // packet.
 template <int U, bool IPV4, bool FILL, bool PIPE, bool ROLL = false>
-__global__ __launch_bounds__(kBlock) void csum_flat_kernel(
-    const uint8_t* __restrict__ bytes, uint64_t bytes_len,
-    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
-    const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
-    uint8_t* __restrict__ status, uint64_t n, uint32_t B, uint32_t B2, uint64_t T1, uint32_t* __restrict__ heads,
-    uint32_t flags, const RssParams rss) {
+__global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint32_t B, uint32_t* __restrict__ heads,
+                                                          uint32_t flags, const RssParams rss) {
     static_assert(!FILL || IPV4, "in-place generate is a frames mode");
     static_assert(!ROLL || (!PIPE && U % 2 == 0), "rolling rows: pairs of rows, no chunk double buffer");
     constexpr uint32_t C = kWave * U;  // units per chunk
@@ -501,12 +514,14 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
     u32x4* ubuf = ubuf_all[wv];
     uint32_t* pbuf = pbuf_all[wv];
     const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
-    // guided tiles: T1 tiles of B packets, then tiles of B2 (< B) packets, so
-    // the dequeue's last draws are short and the launch ends evenly
-    const uint64_t big = T1 * B;
-    const uint64_t ntiles = T1 + (n - big + B2 - 1) / B2;
-    const bool has_seed = !IPV4 && seed != nullptr;
+    const uint64_t ntiles = Q.tile0[Q.nq];  // B packets per tile, numbered across the queues
     const uint32_t vo = 16u * lane;
+    // queue of (wave-uniform) tile tt: a scalar walk over <= kMaxQueues prefixes
+    auto queue_of = [&](uint64_t tt) -> uint32_t {
+        uint32_t q = 0;
+        while (q + 1 < Q.nq && tt >= Q.tile0[q + 1]) ++q;
+        return q;
+    };
 
     // Tile order.  Wave w first takes tile w (static: no start-up contention).
     // With `heads`, the remaining tiles [W, ntiles) are split over kGroups
@@ -533,7 +548,6 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
         d = __builtin_amdgcn_readfirstlane(d);
         return d < tiles_g ? nwaves + grp + static_cast<uint64_t>(kGroups) * d : ntiles;
     };
-    auto tile_base = [&](uint64_t tt) { return tt < T1 ? tt * B : big + (tt - T1) * B2; };
     // Two-deep tile pipeline: while tile t streams, the plan (offset, length,
     // seed) of the next tile is already loading and the tile after it is being
     // dequeued, so no tile starts on an exposed metadata or atomic round trip.
@@ -543,13 +557,16 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
     if (t >= ntiles && heads != nullptr) t = next_tile(t);
     uint64_t t1 = t < ntiles ? next_tile(t) : ntiles;
     auto plan_load = [&](uint64_t tt, uint64_t& o_, uint32_t& L_, uint32_t& sd_) {
-        const uint64_t b_ = tile_base(tt < ntiles ? tt : 0);
-        const uint32_t bb = tt < T1 ? B : B2;
-        const uint32_t c_ = tt < ntiles ? static_cast<uint32_t>(n - b_ < bb ? n - b_ : bb) : 0u;
+        const uint64_t t_ = tt < ntiles ? tt : 0;
+        const uint32_t qq = queue_of(t_);
+        const uint64_t b_ = (t_ - Q.tile0[qq]) * B;
+        const uint64_t nq_ = Q.n[qq];
+        const uint32_t c_ = tt < ntiles ? static_cast<uint32_t>(nq_ - b_ < B ? nq_ - b_ : B) : 0u;
         const uint64_t q_ = b_ + (lane < c_ ? lane : 0);
-        o_ = off[q_];
-        L_ = lane < c_ ? len[q_] : 0u;
-        sd_ = has_seed ? seed[q_] : 0u;
+        o_ = Q.off[qq][q_];
+        L_ = lane < c_ ? Q.len[qq][q_] : 0u;
+        const uint32_t* sq = IPV4 ? nullptr : Q.seed[qq];
+        sd_ = sq != nullptr ? sq[q_] : 0u;
     };
     // ---- A: a tile's per-lane packet plan and its runs: lane j starts a new
     // run unless packet j-1 and j both take part and j's span starts at most
@@ -557,23 +574,24 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
     // [fu of its first, lu of its last])
     struct Tile {
         uint64_t base, o, a0, fu, lu, starts, streamed;
-        uint32_t cnt, L, sd, head, nunits;
+        uint32_t q, cnt, L, sd, head, nunits;
         bool mine, range_bad, short_frame, huge, fast, part;
     };
     auto derive = [&](uint64_t tt, uint64_t o_, uint32_t L_, uint32_t sd_) {
         Tile c;
-        c.base = tile_base(tt);
-        const uint32_t bt = tt < T1 ? B : B2;
-        const uint64_t left = n - c.base;
-        c.cnt = left < bt ? static_cast<uint32_t>(left) : bt;
+        c.q = queue_of(tt);
+        c.base = (tt - Q.tile0[c.q]) * B;
+        const uint64_t left = Q.n[c.q] - c.base;
+        c.cnt = left < B ? static_cast<uint32_t>(left) : B;
         c.mine = lane < c.cnt;
         c.o = o_;
         c.L = L_;
         c.sd = sd_;
+        const uint64_t bytes_len = Q.bytes_len[c.q];
         c.range_bad = c.o > bytes_len || c.L > bytes_len - c.o;
         c.short_frame = IPV4 && c.L < 20;
         c.huge = c.L > kExactMax;
-        const uint8_t* ptr = bytes + (c.range_bad ? 0 : c.o);
+        const uint8_t* ptr = Q.bytes[c.q] + (c.range_bad ? 0 : c.o);
         c.head = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ptr) & 15u);
         c.a0 = reinterpret_cast<uint64_t>(ptr - c.head);
         c.fast = c.mine && !c.range_bad && !c.short_frame && !c.huge;
@@ -791,7 +809,7 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
                 }
                 uint32_t hv = 0;
                 rss_ipv4(rss, h0, h1, h2, h3, h4, h5, pl, L, hv);
-                if (mine) rss.hash[base + lane] = (range_bad || short_frame) ? 0u : hv;
+                if (mine) rss.hash[base + lane] = (range_bad || short_frame) ? 0u : hv;  // one queue with RSS
             }
             if (FILL) {
                 const uint32_t fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
@@ -861,86 +879,8 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(
             }
         }
 
-        if (FILL) {
-            // In-place write-back: wire-ready frames.  A store into a line the
-            // L2 does not hold goes to memory as a partial (byte-masked) write,
-            // and those cost like a read-write turnaround each: 2 M 2-byte
-            // stores after the nt read stream add ~120 us to a 1.5 GB batch
-            // (tools/dev/store_probe.hip, profiles/r02_store_probe.log).  The
-            // stream's nt loads leave no line behind, so each 16-byte unit
-            // holding a field is first read again (default policy: the line
-            // is fetched whole and held), the fields are patched into it and,
-            // where nobody else writes its other bytes, the unit is stored
-            // whole; otherwise the field bytes are stored alone into the
-            // now-resident line.  Whole units: units 0..3 from a0 lie inside
-            // the frame when L >= 64, except unit 0 reaching up to 15 bytes
-            // before the frame (head > 0); those bytes are the tail of the
-            // previous packet of this tile when it ends exactly where this
-            // frame starts and is at least 96 bytes long (its own stores stay
-            // within its first 78 bytes); frames do not overlap, so no other
-            // frame lies there.
-            const int pl = lane ? static_cast<int>(lane) - 1 : 0;
-            const uint64_t po = (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(cur.o >> 32), pl))) << 32) |
-                                static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(cur.o)), pl));
-            const uint32_t pL = static_cast<uint32_t>(__shfl(static_cast<int>(L), pl));
-            const bool prev_ok = lane != 0 && po + pL == cur.o && pL >= 96u;
-            if (mine && !range_bad && !short_frame) {
-                const int fb[4] = {fill_ip ? static_cast<int>(head) + 10 : -1, fill_ip ? static_cast<int>(head) + 11 : -1,
-                                   fpos ? static_cast<int>(fpos) : -1, fpos ? static_cast<int>(fpos) + 1 : -1};
-                const uint32_t fv[4] = {word & 0xffu, (word >> 8) & 0xffu, (word >> 16) & 0xffu, word >> 24};
-                uint8_t* wp = reinterpret_cast<uint8_t*>(a0);
-                u32x4* wu = reinterpret_cast<u32x4*>(a0);
-                if (!slow) {  // ihl 5: every field within units 0..3
-                    uint32_t need = 0;
-#pragma unroll
-                    for (int f = 0; f < 4; ++f) need |= fb[f] >= 0 ? 1u << (fb[f] >> 4) : 0u;
-                    u32x4 w[4];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        if (need & (1u << k)) w[k] = wu[k];  // re-read: the line comes back whole
-                    }
-#if SCCSUM_FILL_WHOLE
-                    const uint32_t whole = L >= 64u ? need & ((head == 0u || prev_ok) ? 0xfu : 0xeu) : 0u;
-#else
-                    const uint32_t whole = 0u;
-#endif
-#pragma unroll
-                    for (int f = 0; f < 4; ++f) {
-                        if (fb[f] >= 0) {
-                            const int d = fb[f] >> 2;
-                            const uint32_t sh = 8u * static_cast<uint32_t>(fb[f] & 3);
-#pragma unroll
-                            for (int k = 0; k < 16; ++k) {
-                                if (d == k) w[k >> 2][k & 3] = (w[k >> 2][k & 3] & ~(0xffu << sh)) | (fv[f] << sh);
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        if (whole & (1u << k)) {
-                            wu[k] = w[k];
-                        } else if (need & (1u << k)) {
-                            // bytes alone, after the re-read (the stores wait on it)
-#pragma unroll
-                            for (int f = 0; f < 4; ++f) {
-                                if (fb[f] >= 0 && (fb[f] >> 4) == k) {
-                                    const int d = fb[f] >> 2;
-                                    uint32_t x = 0;
-#pragma unroll
-                                    for (int j = 0; j < 16; ++j) x = d == j ? w[j >> 2][j & 3] : x;
-                                    wp[fb[f]] = static_cast<uint8_t>(x >> (8u * static_cast<uint32_t>(fb[f] & 3)));
-                                }
-                            }
-                        }
-                    }
-                } else {  // IP options / trimmed length (phase D frames): bytes alone
-#pragma unroll
-                    for (int f = 0; f < 4; ++f) {
-                        if (fb[f] >= 0) wp[fb[f]] = static_cast<uint8_t>(fv[f]);
-                    }
-                }
-            }
-        }
+        uint16_t* const out = Q.out[cur.q];
+        uint8_t* const status = Q.status[cur.q];
         if (mine) {
             if (IPV4) {
                 if (out) reinterpret_cast<uint32_t*>(out)[base + lane] = word;
@@ -982,6 +922,48 @@ __global__ __launch_bounds__(kBlock) void frag_combine_kernel(const uint32_t* __
     const uint32_t r = ~fold16(fold16(S) + static_cast<uint64_t>(swap16(fold16(seed ? seed[i] : 0u)))) & 0xffffu;
     out[i] = bad ? uint16_t(0) : static_cast<uint16_t>(r);
     if (status) status[i] = bad ? SCCSUM_ST_RANGE : (r == 0 ? SCCSUM_ST_OK : 0u);
+}
+
+// In-place fill, second pass: store the values the flat kernel generated
+// (FILL instantiation, words[i] = IP | L4 << 16) into the frames' fields.
+// One thread per frame; which fields it writes is decided from the frame's
+// own (unmodified) header exactly as the first pass decided it.  The stores
+// run as a pass of their own, after the read stream: interleaved with the
+// stream the same stores cost ~100 us per 1 M frames, as their own pass
+// ~70-90 us (HBM read/write turnarounds; tools/dev/store_probe.hip,
+// DESIGN.md §5.6).  Field bytes of different frames never overlap, so the
+// 2-byte stores need no coordination.
+__device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {
+    if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0u) {
+        *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(v);
+    } else {
+        p[0] = static_cast<uint8_t>(v);
+        p[1] = static_cast<uint8_t>(v >> 8);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void fill_store_kernel(uint8_t* __restrict__ bytes, uint64_t bytes_len,
+                                                            const uint64_t* __restrict__ off,
+                                                            const uint32_t* __restrict__ len,
+                                                            const uint32_t* __restrict__ words, uint64_t n,
+                                                            uint32_t mode) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t o = off[i];
+    const uint32_t L = len[i];
+    if (o > bytes_len || L > bytes_len - o || L < 20u) return;
+    uint8_t* p = bytes + o;
+    const uint32_t w = words[i];
+    const uint32_t ihl = p[0] & 0xfu;
+    const uint32_t ip_len = (static_cast<uint32_t>(p[2]) << 8) | p[3];
+    const uint32_t proto = p[9];
+    const uint32_t l4_off = 4u * ihl;
+    const uint32_t l4_end = ip_len < L ? ip_len : L;
+    const bool malformed = L < ip_len || l4_off > l4_end;
+    const uint32_t l4_len = l4_off > l4_end ? 0u : l4_end - l4_off;
+    if (mode & SCCSUM_FILL_IP) store_field(p + 10, w);
+    const uint32_t fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
+    if (fo != 0u && !malformed && l4_len >= fo + 2u) store_field(p + l4_off + fo, w >> 16);
 }
 
 // Header-only generate (no payload bytes read): the IPv4 header checksum
@@ -1087,8 +1069,6 @@ struct Knobs {
     int tile_packets = kWave;        // flat kernel: max packets per tile
     int dynamic = 1;                 // flat kernel: dequeue tiles (1) or static round robin (0)
     int tile_bytes = 0;              // flat kernel: target bytes per tile (0 = packets cap only)
-    int tail_div = 1;                // flat kernel: tail tiles hold B / tail_div packets (1 = no guided tail)
-    int tail_tiles = 4;              // ... and cover about this many tail tiles per wave slot
 };
 thread_local Knobs t_knobs;
 
@@ -1196,13 +1176,13 @@ int units_class(uint32_t max_len) {
 
 // Flat-kernel launch: the grid is what the chip holds at once (the kernel's
 // occupancy, from its VGPR and LDS use, capped by the blocks-per-CU knob), so
-// every wave's static first tile starts at launch; tiles hold about
-// tile_bytes of packets (mean length from bytes_len / n), capped at 64.
-using FlatKernel = void (*)(const uint8_t*, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*, uint16_t*,
-                            uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t, uint32_t*, uint32_t, const RssParams);
+// every wave's static first tile starts at launch; tiles hold B packets (one
+// per lane, B <= 64, about tile_bytes of packets when that knob is set),
+// numbered across the queue set.
+using FlatKernel = void (*)(const Queues, uint32_t, uint32_t*, uint32_t, const RssParams);
 
 int flat_occupancy(FlatKernel k) {
-    constexpr int kSlots = 16;
+    constexpr int kSlots = 32;
     static std::atomic<FlatKernel> keys[kSlots];
     static std::atomic<int> vals[kSlots];
     for (int i = 0; i < kSlots; ++i) {
@@ -1223,9 +1203,9 @@ int flat_occupancy(FlatKernel k) {
     return nb;
 }
 
-void launch_flat(FlatKernel kern, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
-                 const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
-                 uint32_t flags, const RssParams& rss) {
+// Q holds the queues (nq >= 1); tile0 is filled here from the tile size.
+void launch_flat(FlatKernel kern, hipStream_t s, Queues& Q, uint64_t n_total, uint64_t bytes_total, uint32_t flags,
+                 const RssParams& rss) {
     const Knobs& K = t_knobs;
     const int occ = flat_occupancy(kern);
     const uint64_t bpc = static_cast<uint64_t>(occ < K.blocks_per_cu ? occ : K.blocks_per_cu);
@@ -1234,24 +1214,20 @@ void launch_flat(FlatKernel kern, hipStream_t s, const uint8_t* b, uint64_t byte
     uint64_t bmax = static_cast<uint64_t>(K.tile_packets);
     const uint64_t tb = static_cast<uint64_t>(K.tile_bytes);
     if (tb) {
-        const uint64_t mean = bytes_len / n ? bytes_len / n : 1;
+        const uint64_t mean = bytes_total / n_total ? bytes_total / n_total : 1;
         const uint64_t bb = tb / mean ? tb / mean : 1;
         bmax = bb < bmax ? bb : bmax;
     }
-    uint64_t B = (n + slots - 1) / slots;
+    uint64_t B = (n_total + slots - 1) / slots;
     B = B < 1 ? 1 : (B > bmax ? bmax : B);
-    // guided tail: the last ~tail_tiles small tiles per wave slot hold B / tail_div packets each
-    const uint64_t B2 = K.tail_div > 1 && B / K.tail_div ? B / K.tail_div : B;
-    const uint64_t tail = B2 < B ? slots * B2 * static_cast<uint64_t>(K.tail_tiles) : 0;
-    const uint64_t T1 = tail < n ? (n - tail) / B : 0;
-    const uint64_t tiles = T1 + (n - T1 * B + B2 - 1) / B2;
+    Q.tile0[0] = 0;
+    for (uint32_t q = 0; q < Q.nq; ++q) Q.tile0[q + 1] = Q.tile0[q] + (Q.n[q] + B - 1) / B;
+    const uint64_t tiles = Q.tile0[Q.nq];
     uint64_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     blocks = blocks < cap ? blocks : cap;
     blocks = (blocks + 15) & ~uint64_t(15);  // multiple of 16: XCD mapping, waves divide into kGroups
     uint32_t* heads = K.dynamic ? heads_for(s) : nullptr;
-    kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
-        b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, static_cast<uint32_t>(B), static_cast<uint32_t>(B2), T1,
-        heads, flags, rss);
+    kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(Q, static_cast<uint32_t>(B), heads, flags, rss);
 }
 
 template <bool IPV4>
@@ -1268,12 +1244,12 @@ void launch_simple(int uc, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
 }
 
 // Flat-kernel forms: 10 / 11 = U 2, 12 / 13 = U 4, 14 / 15 = U 8 (odd: the
-// next chunk in flight), 16 = U 16.  Frames may fill in place; spans never do.
+// next chunk in flight), 16 = U 16, 17 / 18 / 19 = rolling rows U 8 / 12 / 16.
+// Frames may fill in place; spans never do.
 template <bool IPV4>
-void launch_flat_variant(int variant, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
-                         const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
+void launch_flat_variant(int variant, hipStream_t s, Queues& Q, uint64_t n_total, uint64_t bytes_total,
                          uint32_t flags, const RssParams& rss) {
-    auto go = [&](auto kern) { launch_flat(kern, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss); };
+    auto go = [&](auto kern) { launch_flat(kern, s, Q, n_total, bytes_total, flags, rss); };
     constexpr bool F = IPV4;
     const bool fill = IPV4 && (flags & kFlagFillL4);
     switch (variant) {
@@ -1308,24 +1284,34 @@ RssParams make_rss(const uint8_t* key, uint32_t key_len, uint32_t mode, uint32_t
 
 const RssParams kNoRss{};
 
+// One batch's arguments, checked as every entry point checks them.
+template <bool IPV4>
+bool batch_ok(const void* d_bytes, const uint64_t* d_off, const uint32_t* d_len, const uint32_t* d_seed,
+              const void* d_out, uint32_t flags) {
+    if (!d_bytes || !d_off || !d_len || (!d_out && !(flags & kFlagFillL4))) return false;
+    return !((reinterpret_cast<uintptr_t>(d_bytes) & 15u) || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
+             (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_seed) & 3u) ||
+             (reinterpret_cast<uintptr_t>(d_out) & (IPV4 ? 3u : 1u)));
+}
+
+// default: the flat kernel, all loads nontemporal — 16 units per lane per
+// chunk for big launches (>= 512 Ki packets and 256 MiB), else 8 units with
+// the next chunk in flight: the 16-unit form runs 2 waves per SIMD, too few
+// tiles per wave on smaller launches (DESIGN.md §5.1 has the A/B)
+int pick_variant(uint64_t n_total, uint64_t bytes_total, uint32_t flags) {
+    int variant = t_knobs.variant;
+    const int dflt = (n_total >= (512u << 10) && bytes_total >= (256ull << 20)) ? 16 : 15;
+    if (variant == 0 || (variant == 1 && (flags & kFlagFillL4))) variant = dflt;  // in-place write-back: flat only
+    return variant;
+}
+
 template <bool IPV4>
 int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
            const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n, uint32_t max_len,
            void* stream, uint32_t flags = 0, const RssParams& rss = kNoRss) {
     if (n == 0) return SCCSUM_OK;
-    if (!d_bytes || !d_off || !d_len || (!d_out && !(flags & kFlagFillL4))) return SCCSUM_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(d_bytes) & 15u) || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
-        (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_seed) & 3u) ||
-        (reinterpret_cast<uintptr_t>(d_out) & (IPV4 ? 3u : 1u))) {
-        return SCCSUM_EINVAL;
-    }
-    int variant = t_knobs.variant;
-    // default: the flat kernel, all loads nontemporal — 16 units per lane per
-    // chunk for big batches (>= 512 Ki packets and 256 MiB), else 8 units with
-    // the next chunk in flight: the 16-unit form runs 2 waves per SIMD, too
-    // few tiles per wave on smaller batches (DESIGN.md §5.1 has the A/B)
-    const int dflt = (n >= (512u << 10) && bytes_len >= (256ull << 20)) ? 16 : 15;
-    if (variant == 0 || (variant == 1 && (flags & kFlagFillL4))) variant = dflt;  // in-place write-back: flat only
+    if (!batch_ok<IPV4>(d_bytes, d_off, d_len, d_seed, d_out, flags)) return SCCSUM_EINVAL;
+    const int variant = pick_variant(n, bytes_len, flags);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
     if (variant == 1) {
@@ -1335,8 +1321,63 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
                 b, bytes_len, d_off, d_len, nullptr, n, rss);
         }
     } else {
-        launch_flat_variant<IPV4>(variant, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags, rss);
+        Queues Q{};
+        Q.nq = 1;
+        Q.bytes[0] = b;
+        Q.bytes_len[0] = bytes_len;
+        Q.off[0] = d_off;
+        Q.len[0] = d_len;
+        Q.seed[0] = d_seed;
+        Q.out[0] = d_out;
+        Q.status[0] = d_status;
+        Q.n[0] = n;
+        launch_flat_variant<IPV4>(variant, s, Q, n, bytes_len, flags, rss);
     }
+    return static_cast<int>(hipGetLastError());
+}
+
+// Several independent batches in one flat-kernel launch (sccsum_*_multi).
+template <bool IPV4>
+int launch_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len, void* stream) {
+    if (nbatch > kMaxQueues || (nbatch && !batches)) return SCCSUM_EINVAL;
+    uint64_t n_total = 0, bytes_total = 0;
+    for (uint32_t i = 0; i < nbatch; ++i) {
+        const sccsum_batch& x = batches[i];
+        if (x.n && !batch_ok<IPV4>(x.d_bytes, x.d_off, x.d_len, IPV4 ? nullptr : x.d_seed, x.d_out, 0)) {
+            return SCCSUM_EINVAL;
+        }
+        if (IPV4 && x.d_seed) return SCCSUM_EINVAL;  // frames derive their pseudo-header in-kernel
+        n_total += x.n;
+        bytes_total += x.n ? x.bytes_len : 0;
+    }
+    if (n_total == 0) return SCCSUM_OK;
+    const int variant = pick_variant(n_total, bytes_total, 0);
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    if (variant == 1) {  // the simple kernel takes one batch per launch
+        for (uint32_t i = 0; i < nbatch; ++i) {
+            const sccsum_batch& x = batches[i];
+            if (x.n) {
+                launch_simple<IPV4>(units_class(max_len), s, static_cast<const uint8_t*>(x.d_bytes), x.bytes_len,
+                                    x.d_off, x.d_len, x.d_seed, static_cast<uint16_t*>(x.d_out), x.d_status, x.n, 0);
+            }
+        }
+        return static_cast<int>(hipGetLastError());
+    }
+    Queues Q{};
+    for (uint32_t i = 0; i < nbatch; ++i) {
+        const sccsum_batch& x = batches[i];
+        if (!x.n) continue;
+        const uint32_t q = Q.nq++;
+        Q.bytes[q] = static_cast<const uint8_t*>(x.d_bytes);
+        Q.bytes_len[q] = x.bytes_len;
+        Q.off[q] = x.d_off;
+        Q.len[q] = x.d_len;
+        Q.seed[q] = IPV4 ? nullptr : x.d_seed;
+        Q.out[q] = static_cast<uint16_t*>(x.d_out);
+        Q.status[q] = x.d_status;
+        Q.n[q] = x.n;
+    }
+    launch_flat_variant<IPV4>(variant, s, Q, n_total, bytes_total, 0, kNoRss);
     return static_cast<int>(hipGetLastError());
 }
 
@@ -1423,6 +1464,14 @@ int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len, const uint64_t* 
     return sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len, stream);
 }
 
+int sccsum_spans_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len, void* stream) {
+    return sccsum::launch_multi<false>(batches, nbatch, max_len, stream);
+}
+
+int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len, void* stream) {
+    return sccsum::launch_multi<true>(batches, nbatch, max_len, stream);
+}
+
 static int rss_args_ok(const uint8_t* key, uint32_t key_len, int mode, const uint32_t* d_hash) {
     return key && key_len >= 4 && (mode == SCCSUM_RSS_DISPATCH || mode == SCCSUM_RSS_REASSEMBLED) && d_hash &&
            !(reinterpret_cast<uintptr_t>(d_hash) & 3u);
@@ -1497,9 +1546,17 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
     }
     if (n == 0) return SCCSUM_OK;
     if (mode & SCCSUM_FILL_L4) {
+        // pass 1 generates into d_out2 (required here), pass 2 stores the fields
+        if (!d_out2) return SCCSUM_EINVAL;
         const uint32_t flags = sccsum::kFlagFillL4 | ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u);
-        return sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len, stream,
-                                    flags);
+        const int rc = sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len,
+                                            stream, flags);
+        if (rc != SCCSUM_OK) return rc;
+        const unsigned grid = static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock);
+        sccsum::fill_store_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, static_cast<hipStream_t>(stream)>>>(
+            static_cast<uint8_t*>(d_bytes), bytes_len, d_off, d_len, reinterpret_cast<const uint32_t*>(d_out2), n,
+            mode);
+        return static_cast<int>(hipGetLastError());
     }
     if (!d_bytes || !d_off || !d_len || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
         (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_out2) & 3u)) {
@@ -1539,13 +1596,6 @@ int sccsum_set_tile_packets(int packets) {
 int sccsum_set_tile_bytes(int bytes) {
     if (bytes < 0) return SCCSUM_EINVAL;
     sccsum::t_knobs.tile_bytes = bytes;
-    return SCCSUM_OK;
-}
-
-int sccsum_set_tail_tiles(int divisor, int per_slot) {
-    if (divisor < 1 || divisor > 64 || per_slot < 0 || per_slot > 64) return SCCSUM_EINVAL;
-    sccsum::t_knobs.tail_div = divisor;
-    sccsum::t_knobs.tail_tiles = per_slot;
     return SCCSUM_OK;
 }
 

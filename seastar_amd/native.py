@@ -56,6 +56,8 @@ _PROTOS = {
     "sccsum_pseudo_seed": (_u32, [_u32, _u32, ctypes.c_uint8, ctypes.c_uint16]),
     "sccsum_spans": (ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),
     "sccsum_ipv4_frames": (ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),
+    "sccsum_spans_multi": (ctypes.c_int, [_vp, _u32, _u32, _vp]),
+    "sccsum_ipv4_frames_multi": (ctypes.c_int, [_vp, _u32, _u32, _vp]),
     "sccsum_sync": (ctypes.c_int, [_vp]),
     "sccsum_fragments": (ctypes.c_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "sccsum_fragments_workspace": (_u64, [_u64]),
@@ -69,7 +71,6 @@ _PROTOS = {
     "sccsum_set_tile_packets": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_dynamic_tiles": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_tile_bytes": (ctypes.c_int, [ctypes.c_int]),
-    "sccsum_set_tail_tiles": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "sccsum_read_probe": (ctypes.c_int, [_vp, _u64, _vp, _vp]),
     "sccsum_read_probe_blocks": (ctypes.c_int, []),
     "sccsum_pipeline_create": (ctypes.c_int, [ctypes.c_int, _u64, _u32, ctypes.c_int, ctypes.POINTER(_vp)]),
@@ -94,6 +95,16 @@ GATHER_HOST = 1
 GATHER_STRIDED = 2
 RSS_DISPATCH = 0
 RSS_REASSEMBLED = 1
+
+
+class Batch(ctypes.Structure):
+    """sccsum_batch: one batch of a multi-batch launch."""
+    _fields_ = [("d_bytes", ctypes.c_void_p), ("bytes_len", ctypes.c_uint64), ("d_off", ctypes.c_void_p),
+                ("d_len", ctypes.c_void_p), ("d_seed", ctypes.c_void_p), ("d_out", ctypes.c_void_p),
+                ("d_status", ctypes.c_void_p), ("n", ctypes.c_uint64)]
+
+
+MAX_BATCHES = 16
 
 
 class Fragment(ctypes.Structure):

@@ -51,6 +51,9 @@ int main() {
            SCCSUM_EINVAL);
     EXPECT(sccsum_ipv4_fill(nullptr, 64, nullptr, nullptr, nullptr, nullptr, 3, 0, SCCSUM_FILL_IP, nullptr) ==
            SCCSUM_EINVAL);
+    // FILL_L4 needs d_out2 (the generate pass hands its values to the store pass there)
+    EXPECT(sccsum_ipv4_fill(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr,
+                            nullptr, 3, 0, SCCSUM_FILL_IP | SCCSUM_FILL_L4, nullptr) == SCCSUM_EINVAL);
     // RSS
     const uint8_t key3[3] = {1, 2, 3};
     EXPECT(sccsum_ipv4_rss(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), key3, 3, 0,
@@ -89,7 +92,6 @@ int main() {
     EXPECT(sccsum_set_group_units(3) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_tile_packets(65) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_tile_bytes(-1) == SCCSUM_EINVAL);
-    EXPECT(sccsum_set_tail_tiles(0, 4) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_dynamic_tiles(2) == SCCSUM_EINVAL);
     // host arithmetic and strings
     EXPECT(sccsum_pseudo_seed(1, 2, 17, 8) == 28u);

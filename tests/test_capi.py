@@ -121,3 +121,20 @@ def test_burst_argument_validation_without_device():
     assert lib.sccsum_burst_destroy(None) == native.SCCSUM_OK
     assert lib.sccsum_strerror(native.SCCSUM_EBUSY) == b"every batch slot is in flight"
     assert ctypes.sizeof(native.Fragment) == 16  # char* base; size_t size (packet.hh:43-46)
+
+
+def test_multi_batch_argument_validation_without_device():
+    import ctypes
+
+    lib = native.load()
+    arr = (native.Batch * 17)()
+    assert ctypes.sizeof(native.Batch) == 64
+    assert lib.sccsum_ipv4_frames_multi(None, 0, 0, None) == native.SCCSUM_OK  # nothing to do
+    assert lib.sccsum_spans_multi(ctypes.cast(arr, ctypes.c_void_p), 16, 0, None) == native.SCCSUM_OK  # all empty
+    assert lib.sccsum_spans_multi(ctypes.cast(arr, ctypes.c_void_p), 17, 0, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_spans_multi(None, 2, 0, None) == native.SCCSUM_EINVAL
+    arr[0] = native.Batch(16, 64, 0x1000, 0x2000, 0x3000, 0x4000, None, 3)
+    # frames take no seeds
+    assert lib.sccsum_ipv4_frames_multi(ctypes.cast(arr, ctypes.c_void_p), 1, 0, None) == native.SCCSUM_EINVAL
+    arr[0] = native.Batch(17, 64, 0x1000, 0x2000, None, 0x4000, None, 3)  # misaligned bytes
+    assert lib.sccsum_spans_multi(ctypes.cast(arr, ctypes.c_void_p), 1, 0, None) == native.SCCSUM_EINVAL

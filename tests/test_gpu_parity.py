@@ -21,9 +21,9 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(params=[1, 10, 11, 12, 13, 14, 15, 16],
-                ids=["simple", "flat2", "flat2_pipe", "flat4", "flat4_pipe", "flat8", "flat8_pipe", "flat16"],
-                autouse=True)
+@pytest.fixture(params=[1, 10, 11, 12, 13, 14, 15, 16, 17, 19],
+                ids=["simple", "flat2", "flat2_pipe", "flat4", "flat4_pipe", "flat8", "flat8_pipe", "flat16", "roll8",
+                     "roll16"], autouse=True)
 def kernel_variant(request, dev):
     """Every parity test runs against both kernel families."""
     lib = native.load()
@@ -665,3 +665,52 @@ def test_many_launches_in_flight_streams_and_graphs(dev, kernel_variant):
     torch.cuda.synchronize()
     assert np.array_equal(batch.as_u16(gout).reshape(-1, 2), want)
     assert np.array_equal(gst.cpu().numpy(), want_st)
+
+
+def test_multi_batch_launch(dev, kernel_variant):
+    """sccsum_ipv4_frames_multi / sccsum_spans_multi: 16 independent batches in
+    one launch (empty, 1 packet, 1500 B frames, Zipf frames at odd offsets,
+    malformed frames, packets over 128 KiB, seeded spans) — each batch's
+    outputs exactly what its own launch gives, and the oracle's."""
+    rng = np.random.default_rng(71)
+    items, want = [], []
+    for i in range(16):
+        kind = i % 5
+        if kind == 0:
+            buf, off, lens, _ = synth.udp_ipv4_frames(int(rng.integers(0, 3)) * 700, 1500, seed=100 + i)
+        elif kind == 1:
+            buf, off, lens, _ = synth.mixed_udp_frames(int(rng.integers(1, 900)), seed=200 + i, max_gap=3)
+        elif kind == 2:
+            buf, off, length = _tx_frames(rng, 300)
+            lens = length
+        elif kind == 3:
+            lens = np.array([140_000, 1500, 64], np.uint32)
+            buf, off, lens, _ = synth.mixed_udp_frames(3, seed=300 + i, lengths=lens)
+        else:
+            buf, off, lens, _ = synth.udp_ipv4_frames(1, 200, seed=400 + i)
+        if lens.size == 0:
+            buf, off = np.zeros(16, np.uint8), np.zeros(0, np.uint64)
+        b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+        st = torch.empty(max(b.n, 1), dtype=torch.uint8, device=dev)
+        items.append((b, None, st))
+        want.append(oracle.batch_ipv4(buf, off, lens) if lens.size else (np.zeros((0, 2), np.uint16), np.zeros(0, np.uint8)))
+    outs = batch.ipv4_frames_multi(items)
+    torch.cuda.synchronize()
+    for (b, _, st), o, (w, ws) in zip(items, outs, want):
+        assert np.array_equal(batch.as_u16(o).reshape(-1, 2), w)
+        assert np.array_equal(st[: b.n].cpu().numpy(), ws)
+    # spans with seeds, 16 batches of Zipf lengths
+    sitems, swant = [], []
+    for i in range(16):
+        lens = synth.zipf_lengths(int(rng.integers(0, 400)), seed=500 + i)
+        off, total = synth.pack(lens, seed=600 + i, max_gap=5)
+        buf = rng.integers(0, 256, size=max(int(total), 16), dtype=np.uint8)
+        seeds = rng.integers(0, 65536, size=lens.size).astype(np.uint32)
+        b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+        sd = torch.from_numpy(seeds.view(np.int32)).to(dev) if lens.size else None
+        sitems.append((b, None, None, sd))
+        swant.append(oracle.batch_spans(buf, off, lens, seeds) if lens.size else np.zeros(0, np.uint16))
+    souts = batch.spans_multi(sitems)
+    torch.cuda.synchronize()
+    for o, w in zip(souts, swant):
+        assert np.array_equal(batch.as_u16(o), w)

@@ -83,6 +83,35 @@ __global__ __launch_bounds__(256) void k_st64rw(uint8_t* buf, uint64_t n, uint32
     L[t % 4] = x;
 }
 
+// second pass, one lane per frame: read-modify-write the aligned 64-B line (4 loads, 4 stores)
+__global__ __launch_bounds__(256) void k_st64rw1(uint8_t* buf, uint64_t n, uint32_t v) {
+    const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a = (reinterpret_cast<uint64_t>(buf) + i * kFrame + 10) & ~uint64_t(63);
+    u32x4* L = reinterpret_cast<u32x4*>(a);
+    u32x4 x0 = L[0], x1 = L[1], x2 = L[2], x3 = L[3];
+    x0.z ^= v;
+    x2.x ^= v;
+    L[0] = x0;
+    L[1] = x1;
+    L[2] = x2;
+    L[3] = x3;
+}
+
+// second pass, one lane per frame: read-modify-write the two 16-B units holding the fields
+__global__ __launch_bounds__(256) void k_st16rw1(uint8_t* buf, uint64_t n, uint32_t v) {
+    const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a = reinterpret_cast<uint64_t>(buf) + i * kFrame;
+    u32x4* u0 = reinterpret_cast<u32x4*>((a + 10) & ~15ull);
+    u32x4* u1 = reinterpret_cast<u32x4*>((a + 26) & ~15ull);
+    u32x4 x = *u0, y = *u1;
+    x.x ^= v;
+    y.y ^= v;
+    *u0 = x;
+    *u1 = y;
+}
+
 // MODE 0 = 2-byte field stores, 1 = whole 16-B units re-read first, 2 = whole 64-B line re-read first,
 // 4 = 2-byte stores after a re-read of their units, 5 = whole 16-B units from registers (no re-read);
 // DFL = frame's first line default policy
@@ -182,6 +211,52 @@ __global__ __launch_bounds__(256) void k_rdst(uint8_t* buf, uint64_t n, uint64_t
     if (acc == 0x12345u) sink[0] = acc;
 }
 
+// Reverse streaming: each wave walks its tile's chunks from the END to the
+// START, so a frame's head (where the fields are) is read last; the fields go
+// out right after the chunk holding the head, while its DRAM rows are fresh.
+// MODE 0 = 2-byte stores, 1 = 16-B unit RMW, 2 = no stores (read only, reversed)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_rdrev(uint8_t* buf, uint64_t n, uint64_t* sink) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t(blockIdx.x) * 256 + threadIdx.x) >> 6;
+    const uint64_t nw = uint64_t(gridDim.x) * 4;
+    const uint64_t tiles = n / 64;
+    uint32_t acc = 0;
+    constexpr uint32_t units = 64 * kFrame / 16;  // 6000
+    constexpr uint32_t CH = 64 * 8;               // units per chunk
+    for (uint64_t t = wave; t < tiles; t += nw) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(buf + t * 64 * kFrame);
+        const uint32_t head_unit = uint32_t((uint64_t(lane) * kFrame) / 16);
+        for (int32_t c = int32_t((units + CH - 1) / CH) - 1; c >= 0; --c) {
+            u32x4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t uu = uint32_t(c) * CH + 64 * k + lane;
+                v[k] = uu < units ? __builtin_nontemporal_load(base + uu) : u32x4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
+            if (MODE != 2 && head_unit >= uint32_t(c) * CH && head_unit < uint32_t(c + 1) * CH) {
+                uint8_t* f = buf + (t * 64 + lane) * kFrame;
+                if (MODE == 0) {
+                    *reinterpret_cast<uint16_t*>(f + 10) = uint16_t(acc);
+                    *reinterpret_cast<uint16_t*>(f + 26) = uint16_t(acc);
+                } else {
+                    const uint64_t a = reinterpret_cast<uint64_t>(f);
+                    u32x4* u0 = reinterpret_cast<u32x4*>((a + 10) & ~15ull);
+                    u32x4* u1 = reinterpret_cast<u32x4*>((a + 26) & ~15ull);
+                    u32x4 x = *u0, y = *u1;
+                    x.x ^= acc | 1u;
+                    y.y ^= acc | 1u;
+                    *u0 = x;
+                    *u1 = y;
+                }
+            }
+        }
+    }
+    if (acc == 0x12345u) sink[0] = acc;
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? std::atoi(argv[1]) : 3;
     constexpr int R = 4;
@@ -245,9 +320,23 @@ int main(int argc, char** argv) {
         k_st64rw<<<g_frames * 4, 256>>>(b, kFrames, 0x1234);
     });
     run("st64rw", [&](uint8_t* b) { k_st64rw<<<g_frames * 4, 256>>>(b, kFrames, 0x1234); });
+    run("st64rw1", [&](uint8_t* b) { k_st64rw1<<<g_frames, 256>>>(b, kFrames, 0x1234); });
+    run("st16rw1", [&](uint8_t* b) { k_st16rw1<<<g_frames, 256>>>(b, kFrames, 0x1234); });
+    run("rd;st64rw1", [&](uint8_t* b) {
+        k_read<<<cus * 8, 256>>>(reinterpret_cast<const u32x4*>(b), kBytes / 16, sink);
+        k_st64rw1<<<g_frames, 256>>>(b, kFrames, 0x1234);
+    });
+    run("rd;st16rw1", [&](uint8_t* b) {
+        k_read<<<cus * 8, 256>>>(reinterpret_cast<const u32x4*>(b), kBytes / 16, sink);
+        k_st16rw1<<<g_frames, 256>>>(b, kFrames, 0x1234);
+    });
     run("rd+dfr16", [&](uint8_t* b) { k_rdst<10, false><<<cus * 4, 256>>>(b, kFrames, sink); });
     run("rd+dfr2", [&](uint8_t* b) { k_rdst<12, false><<<cus * 4, 256>>>(b, kFrames, sink); });
     run("rd8w+dfr16", [&](uint8_t* b) { k_rdst<10, false><<<cus * 2, 256>>>(b, kFrames, sink); });
+    run("rev only", [&](uint8_t* b) { k_rdrev<2><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rev+st2", [&](uint8_t* b) { k_rdrev<0><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rev+st16rw", [&](uint8_t* b) { k_rdrev<1><<<cus * 4, 256>>>(b, kFrames, sink); });
+    run("rev8w+st2", [&](uint8_t* b) { k_rdrev<0><<<cus * 2, 256>>>(b, kFrames, sink); });
     run("rd only", [&](uint8_t* b) { k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink); });
     return 0;
 }

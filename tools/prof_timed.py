@@ -96,6 +96,15 @@ def main():
         for r, d in zip(timed, dur):
             w.writerow([r.get(c, "") for c in cols] + [f"{d:.3f}"])
 
+    # further kernels of the same timed step (e.g. the fill's store pass): their
+    # timed dispatches add to the step's kernel time
+    extra = []
+    for ex in roof.get("trace_select_extra", []):
+        rows = trace_dispatches(a.trace, ex["kernel"])[int(ex["skip"]):int(ex["skip"]) + int(ex["count"])]
+        d_ex = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+        if d_ex:
+            extra.append({"kernel_match": ex["kernel"], "timed_dispatches": len(d_ex),
+                          "avg_us_timed": round(statistics.mean(d_ex), 3)})
     alg = float(roof["alg_bytes_per_launch"])
     entry = {
         "kernel_match": kern,
@@ -113,6 +122,11 @@ def main():
         "frac_from_trace": round(alg / statistics.mean(dur) / 1e3 / roof["peak"], 4),
         "trace_csv": os.path.relpath(a.trace_out, os.path.dirname(os.path.abspath(a.out))),
     }
+    if extra:
+        step_us = statistics.mean(dur) + sum(e["avg_us_timed"] for e in extra)
+        entry["extra_kernels"] = extra
+        entry["avg_us_step_kernels"] = round(step_us, 3)
+        entry["frac_from_trace_step"] = round(alg / step_us / 1e3 / roof["peak"], 4)
     res = {"label": a.label, "config": a.config, "bench_line_value": line.get("value"), "kernels": {}}
 
     calib = None
@@ -133,6 +147,19 @@ def main():
             "traffic_over_alg": round((2 * fb + wb) / alg, 4),
             "write_bytes_per_packet": None,
         })
+        for ex, e in zip(roof.get("trace_select_extra", []), extra):
+            sk, ct = int(ex["skip"]), int(ex["count"])
+            fx = [v for _, v in counter_dispatches(a.fetch, ex["kernel"], "FETCH_SIZE")[sk:sk + ct]]
+            wx = [v for _, v in counter_dispatches(a.write, ex["kernel"], "WRITE_SIZE")[sk:sk + ct]]
+            if fx and wx:
+                # a pass of scattered small accesses: FETCH_SIZE x 2 is calibrated for wide
+                # streaming reads only, so the raw value is reported beside it
+                e["fetch_size_raw_bytes"] = statistics.mean(fx) * 1024
+                e["write_size_bytes"] = statistics.mean(wx) * 1024
+        if extra and all("write_size_bytes" in e for e in extra):
+            step_bytes = 2 * fb + wb + sum(2 * e["fetch_size_raw_bytes"] + e["write_size_bytes"] for e in extra)
+            entry["hbm_bytes_per_step"] = step_bytes
+            entry["traffic_over_alg_step"] = round(step_bytes / alg, 4)
         if a.probe_bytes:
             pf = [v for _, v in counter_dispatches(a.fetch, a.probe_kernel, "FETCH_SIZE")]
             if pf:
@@ -145,6 +172,10 @@ def main():
     res["probe_bytes"] = a.probe_bytes
     res["probe_calibration"] = calib
     # bench.py reads kernels["csum_flat_kernel"]["hbm_bytes_per_launch"] for roofline.traffic
+    # (per step when the step has further kernels)
+    if "hbm_bytes_per_step" in entry:
+        entry["hbm_bytes_per_launch_pass1"] = entry["hbm_bytes_per_launch"]
+        entry["hbm_bytes_per_launch"] = entry["hbm_bytes_per_step"]
     res["kernels"]["csum_flat_kernel"] = entry
     json.dump(res, open(a.out, "w"), indent=1)
     print(json.dumps(res, indent=1))

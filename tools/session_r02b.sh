@@ -22,7 +22,7 @@ prof() {  # prof <config> <extra bench args...>: trace + FETCH + WRITE passes, t
         --out $O/${TAG:-r02b}_pmc_$c.json --trace-out $O/${TAG:-r02b}_trace_$c.csv > $O/prof_${c}_summary.log 2>&1
 }
 echo "start $(date)" > $O/steps.log
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 && echo "pytest ok" >> $O/steps.log && \
+[ -n "$SKIP_PYTEST" ] || timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 && echo "pytest ok" >> $O/steps.log && \
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 12 > $O/bench.log 2>&1 && echo "bench ok" >> $O/steps.log && \
 timeout -k 10 300 python bench.py --config fill --steps 20 --no-cpu > $O/bench_fill.log 2>&1 && echo "fill ok" >> $O/steps.log && \
 timeout -k 10 300 python bench.py --config mixed --steps 20 --no-cpu > $O/bench_mixed.log 2>&1 && echo "mixed ok" >> $O/steps.log && \
