@@ -13,7 +13,7 @@ STEPS_PROF="--steps 10 --warmup 2 --no-cpu"
 prof() {  # prof <config> <extra bench args...>: trace + FETCH + WRITE passes, then the cut
     local c=$1; shift
     cd /tmp && \
-    timeout -k 10 300 rocprofv3 --kernel-trace -d $O/prof_$c/trace -o run --output-format csv -- python3 $R/bench.py --config $c $STEPS_PROF "$@" > $O/prof_${c}_trace.log 2>&1 && \
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$c/trace -o run --output-format csv -- python3 $R/bench.py --config $c $STEPS_PROF "$@" > $O/prof_${c}_trace.log 2>&1 && \
     timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/prof_$c/fetch -o run --output-format csv -- python3 $R/bench.py --config $c $STEPS_PROF "$@" > $O/prof_${c}_fetch.log 2>&1 && \
     timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/prof_$c/write -o run --output-format csv -- python3 $R/bench.py --config $c $STEPS_PROF "$@" > $O/prof_${c}_write.log 2>&1 && \
     cd $R && python tools/prof_timed.py --bench-log $O/prof_${c}_trace.log --trace $O/prof_$c/trace \
