@@ -342,7 +342,8 @@ int sccsum_burst_destroy(sccsum_burst* b);
  * (sccsum_host_alloc / hipHostMalloc; hipHostRegister'd memory such as a DPDK
  * mempool, registered once) — then the bytes cross PCIe without a host thread
  * touching them.  Any alignment; destinations must not overlap.  d_desc is a
- * DEVICE array (8-byte aligned). */
+ * DEVICE array (8-byte aligned).  A descriptor with src == NULL is skipped
+ * (its bytes are already in place). */
 typedef struct sccsum_gather_desc {
     const void* src;
     uint32_t dst_off;
@@ -350,6 +351,28 @@ typedef struct sccsum_gather_desc {
 } sccsum_gather_desc;
 
 int sccsum_gather(const sccsum_gather_desc* d_desc, uint64_t n, void* d_dst, void* stream);
+
+/* Packets as fragment lists, summed where the fragments lie (one kernel, each
+ * byte read once — over PCIe for pinned / registered host memory — with no
+ * gather into a batch first): checksummer::sum(const packet&)
+ * (ip_checksum.cc:64-68) for packets whose fragments may be anywhere the
+ * device can read.  Packet p (p < n) has the fragments d_desc[d_first[p] ..
+ * d_first[p+1]) (d_first has n + 1 entries), which must tile its bytes in
+ * order: fragment j holds packet bytes [dst_off_j - d_off[p], + len_j), so
+ * the first starts at dst_off = d_off[p] and the lengths add up to d_len[p].
+ * A fragment with src == NULL lies at d_stage + dst_off (bytes already in a
+ * device batch; d_stage may be NULL when no fragment uses it).  A packet whose
+ * fragments do not tile it gets result 0 and status SCCSUM_ST_RANGE.
+ * Results and status as sccsum_spans / sccsum_ipv4_frames (frames: IPv4
+ * header + L4, the header may be split across fragments).  d_desc, d_first,
+ * d_off, d_len, d_seed, d_out, d_status: device arrays (aligned to their
+ * element size, d_desc to 8).  max_len: the longest packet (sizes the loop). */
+int sccsum_spans_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const uint64_t* d_off,
+                      const uint32_t* d_len, const uint32_t* d_seed, const void* d_stage, uint16_t* d_out,
+                      uint8_t* d_status, uint64_t n, uint32_t max_len, void* stream);
+int sccsum_ipv4_frames_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const uint64_t* d_off,
+                            const uint32_t* d_len, const void* d_stage, uint16_t* d_out2, uint8_t* d_status,
+                            uint64_t n, uint32_t max_len, void* stream);
 
 /* Pinned (page-locked) host memory for packet pools. */
 int sccsum_host_alloc(void** p, uint64_t bytes);

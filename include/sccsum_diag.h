@@ -26,7 +26,7 @@ extern "C" {
  * 17-19 = flat kernel with rolling rows: U = 8 / 12 / 16 rows of 64 units
  *     in flight, each pair of rows scanned as it lands and its registers
  *     reloaded with the next chunk's rows at once (A/B: slower than 16 on
- *     1500 B frames, profiles/r02g_ab_roll.log).
+ *     1500 B frames, profiles/r02_ab_roll.log).
  * SCCSUM_EINVAL for anything else. */
 int sccsum_set_kernel_variant(int variant);
 
@@ -55,6 +55,14 @@ int sccsum_set_dynamic_tiles(int on);
 int sccsum_read_probe(const void* d_src, uint64_t bytes, uint64_t* d_sink, void* stream);
 int sccsum_read_probe_blocks(void);
 
+/* Burst queues driven from this thread: how a batch holding zero-copy packets
+ * (sccsum_burst_submit_mapped) runs.  2 (default) = one launch of the
+ * fragment-list kernel that reads the pinned metadata, descriptors and
+ * fragments where they lie and writes the results into the pinned result
+ * block (no copies); 1 = metadata H2D, fragment-list kernel, results D2H;
+ * 0 = metadata H2D, sccsum_gather into the batch, sum the batch, results D2H
+ * (the two-pass form).  SCCSUM_EINVAL for anything else. */
+int sccsum_set_burst_fused(int on);
 
 #ifdef __cplusplus
 }

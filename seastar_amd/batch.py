@@ -214,6 +214,56 @@ def fragments(data: torch.Tensor, bytes_len: int, frag_off: torch.Tensor, frag_l
     return out[:n]
 
 
+DESC_DTYPE = np.dtype([("src", "<u8"), ("dst_off", "<u4"), ("len", "<u4")])  # sccsum_gather_desc
+
+
+def make_desc(src, dst_off, length) -> np.ndarray:
+    """sccsum_gather_desc records: src = absolute device-readable addresses
+    (0 = in the stage buffer at dst_off), dst_off = the fragment's position in
+    the packet layout (packet offset + offset inside the packet), length."""
+    d = np.zeros(len(length), dtype=DESC_DTYPE)
+    d["src"] = src
+    d["dst_off"] = dst_off
+    d["len"] = length
+    return d
+
+
+def _desc_call(name, desc, first, off, length, max_len, width, seeds, stage, out, status, stream):
+    lib = native.load()
+    n = int(off.numel())
+    dev = off.device
+    assert int(first.numel()) == n + 1 and first.dtype == torch.int32 and desc.dtype == torch.uint8
+    if out is None:
+        out = torch.empty(max(width * n, width), dtype=torch.int16, device=dev)
+    args = [ctypes_ptr(desc), ctypes_ptr(first), ctypes_ptr(off), ctypes_ptr(length)]
+    if width == 1:
+        args.append(_ptr(seeds))
+    args += [None if stage is None else ctypes_ptr(stage), ctypes_ptr(out), _ptr(status), n, max_len, _stream(stream)]
+    native.check(getattr(lib, name)(*args), name)
+    return out
+
+
+def spans_desc(desc: torch.Tensor, first: torch.Tensor, off: torch.Tensor, length: torch.Tensor, max_len: int,
+               seeds: torch.Tensor | None = None, stage: torch.Tensor | None = None, out: torch.Tensor | None = None,
+               status: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """sccsum_spans_desc: packets as fragment lists summed where the fragments
+    lie (desc = make_desc records as a uint8 device tensor, first = int32
+    [n + 1]); one int16 checksum per packet."""
+    n = int(off.numel())
+    return _desc_call("sccsum_spans_desc", desc, first, off, length, max_len, 1, seeds, stage, out, status,
+                      stream)[:n]
+
+
+def ipv4_frames_desc(desc: torch.Tensor, first: torch.Tensor, off: torch.Tensor, length: torch.Tensor, max_len: int,
+                     stage: torch.Tensor | None = None, out2: torch.Tensor | None = None,
+                     status: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """sccsum_ipv4_frames_desc: frames as fragment lists; [n, 2] int16."""
+    n = int(off.numel())
+    out2 = _desc_call("sccsum_ipv4_frames_desc", desc, first, off, length, max_len, 2, None, stage, out2, status,
+                      stream)
+    return out2[: 2 * n].view(n, 2) if n else out2[:0].view(0, 2)
+
+
 def read_probe(buf: torch.Tensor, nbytes: int, sink: torch.Tensor | None = None, stream=None) -> torch.Tensor:
     """Stream-read nbytes of buf with the kernels' load shape (HBM ceiling probe)."""
     lib = native.load()

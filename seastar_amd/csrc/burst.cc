@@ -17,9 +17,12 @@
 //            SCCSUM_EBUSY when every slot is in flight (poll, then retry)
 //   submit_mapped: zero-copy — the fragments lie in memory the device reads
 //            (pinned / registered host memory, e.g. a DPDK mempool): only a
-//            {src, dst, len} descriptor is recorded; at launch a gather kernel
-//            (sccsum_gather) pulls the bytes over PCIe into the batch, so no
-//            host thread touches packet bytes
+//            {src, dst, len} descriptor is recorded; at launch the
+//            fragment-list kernel (sccsum_*_desc) reads the bytes over PCIe
+//            straight into the sum, so no host thread touches packet bytes and
+//            they cross PCIe once with no gathered copy in HBM (a copied
+//            packet of the same batch is one descriptor into the staged
+//            bytes)
 //   poll:    launch the open slot when full (bytes / packets) or older than
 //            max_delay_ns — on the slot's own stream: ONE H2D of the staged
 //            bytes with the metadata packed behind them, the kernel, ONE D2H
@@ -38,6 +41,7 @@
 #include <vector>
 
 #include "sccsum.h"
+#include "sccsum_diag.h"
 
 struct sccsum_burst {
     enum class state { free, open, inflight, delivering };
@@ -50,15 +54,17 @@ struct sccsum_burst {
         uint64_t* h_off = nullptr;  // metadata as submitted
         uint32_t* h_len = nullptr;
         uint32_t* h_seed = nullptr;
-        sccsum_gather_desc* h_desc = nullptr;  // zero-copy fragments (submit_mapped)
+        uint32_t* h_first = nullptr;           // packet p's descriptors: h_desc[h_first[p] .. h_first[p+1])
+        sccsum_gather_desc* h_desc = nullptr;  // every packet's fragments (src NULL: staged by copy)
         uint8_t* h_res = nullptr;  // results then status, one D2H
         uint8_t* d_stage = nullptr;
         uint8_t* d_res = nullptr;
         hipEvent_t done = nullptr;
         uint64_t used = 0;  // staged bytes
         uint32_t npk = 0;
-        uint32_t ndesc = 0;   // mapped fragments the device gathers
+        uint32_t ndesc = 0;   // descriptors recorded
         bool copied = false;  // some packet was memcpy'd into h_stage
+        bool mapped = false;  // some packet is zero-copy (the batch runs the fragment-list kernel)
         uint32_t max_len = 0;
         uint64_t first_ticket = 0;
         std::chrono::steady_clock::time_point opened{};
@@ -94,6 +100,7 @@ void free_slot(sccsum_burst::Slot& s) {
     (void)hipHostFree(s.h_off);
     (void)hipHostFree(s.h_len);
     (void)hipHostFree(s.h_seed);
+    (void)hipHostFree(s.h_first);
     (void)hipHostFree(s.h_desc);
     (void)hipHostFree(s.h_res);
     (void)hipFree(s.d_stage);
@@ -104,14 +111,21 @@ void free_slot(sccsum_burst::Slot& s) {
 
 int width(const sccsum_burst* b) { return b->mode == SCCSUM_PIPE_IPV4 ? 2 : 1; }
 
-// gather descriptors per slot (a packet of more fragments launches its slot early)
+// fragment descriptors per slot (a packet of more fragments launches its slot early)
 uint64_t desc_cap(const sccsum_burst* b) { return 4ull * b->batch_packets; }
 
 // staging bytes per slot: the data room plus room for the packed metadata
-// and gather descriptors
+// (offsets, lengths, seeds, descriptor starts) and descriptors
 uint64_t stage_bytes(const sccsum_burst* b) {
-    return b->batch_bytes + 16ull * b->batch_packets + sizeof(sccsum_gather_desc) * desc_cap(b) + 32;
+    return b->batch_bytes + 20ull * b->batch_packets + sizeof(sccsum_gather_desc) * desc_cap(b) + 48;
 }
+
+// Diagnostic (sccsum_diag.h), how a batch holding zero-copy packets runs:
+// 2 = the fragment-list kernel reads the metadata and descriptors where the
+// host wrote them and writes the results straight into the pinned result
+// block (one launch, no copies); 1 = metadata H2D, fragment-list kernel,
+// results D2H; 0 = metadata H2D, gather into the batch, sum, results D2H.
+thread_local int t_fused = 2;
 
 // One H2D (packets + metadata packed behind them), the kernel, one D2H
 // (results + status), an event: 4 stream operations per batch.  On failure
@@ -120,41 +134,88 @@ uint64_t stage_bytes(const sccsum_burst* b) {
 // so a later poll / drain retries the launch.
 int launch_slot_ops(sccsum_burst* b, sccsum_burst::Slot& s);
 
+// A zero-copy one-launch batch (t_fused 2) is a single kernel with no copies
+// to overlap, so every such batch goes to ONE stream: the kernels run in
+// submit order, the oldest batch — the one delivery waits for — finishes
+// first, and the host refills its slot while the GPU runs the next ones
+// (on separate streams they share PCIe and finish together, leaving the GPU
+// idle while the host refills).  Batches with copies keep their slot's stream
+// so one batch's copies overlap another's kernel.
+bool one_launch(const sccsum_burst::Slot& s) { return s.mapped && t_fused == 2; }
+
+hipStream_t stream_of(const sccsum_burst* b, const sccsum_burst::Slot& s) {
+    return one_launch(s) ? b->slots[0].stream : s.stream;
+}
+
 int launch_slot(sccsum_burst* b, sccsum_burst::Slot& s) {
+    const hipStream_t st = stream_of(b, s);
     const int rc = launch_slot_ops(b, s);
-    if (rc != SCCSUM_OK) (void)hipStreamSynchronize(s.stream);
+    if (rc != SCCSUM_OK) (void)hipStreamSynchronize(st);
     return rc;
 }
 
 int launch_slot_ops(sccsum_burst* b, sccsum_burst::Slot& s) {
     SCCSUM_TRY(hipSetDevice(b->device));
-    const hipStream_t st = s.stream;
+    const hipStream_t st = stream_of(b, s);
     const uint64_t n = s.npk;
-    const uint64_t a_off = (s.used + 15) & ~uint64_t(15), a_len = a_off + 8 * n, a_seed = a_len + 4 * n;
     const bool spans = b->mode != SCCSUM_PIPE_IPV4;
-    const uint64_t a_desc = ((spans ? a_seed + 4 * n : a_seed) + 7) & ~uint64_t(7);
-    const uint64_t total = a_desc + sizeof(sccsum_gather_desc) * s.ndesc;
+    if (one_launch(s)) {
+        // zero-copy batch: the kernel reads the pinned metadata, descriptors
+        // and (for copied packets) staged bytes over PCIe and writes the
+        // results into the pinned result block the callback reads
+        s.h_first[n] = s.ndesc;
+        auto* h_out = reinterpret_cast<uint16_t*>(s.h_res);
+        uint8_t* h_status = s.h_res + 2 * width(b) * n;
+        const int rk = spans ? sccsum_spans_desc(s.h_desc, s.h_first, s.h_off, s.h_len, s.h_seed, s.h_stage, h_out,
+                                                 h_status, n, s.max_len, st)
+                             : sccsum_ipv4_frames_desc(s.h_desc, s.h_first, s.h_off, s.h_len, s.h_stage, h_out,
+                                                       h_status, n, s.max_len, st);
+        if (rk != SCCSUM_OK) return rk;
+        SCCSUM_TRY(hipEventRecord(s.done, st));
+        s.st = sccsum_burst::state::inflight;
+        ++b->inflight;
+        b->next_launch = (b->next_launch + 1) % b->slots.size();
+        if (b->open != SIZE_MAX && &b->slots[b->open] == &s) b->open = SIZE_MAX;
+        return SCCSUM_OK;
+    }
+    const uint64_t a_off = (s.used + 15) & ~uint64_t(15), a_len = a_off + 8 * n, a_seed = a_len + 4 * n;
+    const uint64_t a_first = spans ? a_seed + 4 * n : a_seed;
+    const bool fused = s.mapped && t_fused;
+    const uint64_t a_desc = ((fused ? a_first + 4 * (n + 1) : a_first) + 7) & ~uint64_t(7);
+    const uint64_t total = a_desc + (s.mapped ? sizeof(sccsum_gather_desc) * s.ndesc : 0);
     std::memcpy(s.h_stage + a_off, s.h_off, 8 * n);
     std::memcpy(s.h_stage + a_len, s.h_len, 4 * n);
     if (spans) std::memcpy(s.h_stage + a_seed, s.h_seed, 4 * n);
-    if (s.ndesc) std::memcpy(s.h_stage + a_desc, s.h_desc, sizeof(sccsum_gather_desc) * s.ndesc);
-    // only mapped packets: the packet bytes come over PCIe through the gather,
+    if (fused) {
+        s.h_first[n] = s.ndesc;
+        std::memcpy(s.h_stage + a_first, s.h_first, 4 * (n + 1));
+    }
+    if (s.mapped) std::memcpy(s.h_stage + a_desc, s.h_desc, sizeof(sccsum_gather_desc) * s.ndesc);
+    // only mapped packets: their bytes come over PCIe as the kernel reads them,
     // the H2D carries the metadata alone
     const uint64_t from = s.copied ? 0 : a_off;
     SCCSUM_TRY(hipMemcpyAsync(s.d_stage + from, s.h_stage + from, total - from, hipMemcpyHostToDevice, st));
-    if (s.ndesc) {
-        const int rg = sccsum_gather(reinterpret_cast<const sccsum_gather_desc*>(s.d_stage + a_desc), s.ndesc,
-                                     s.d_stage, st);
-        if (rg != SCCSUM_OK) return rg;
-    }
     const auto* d_off = reinterpret_cast<const uint64_t*>(s.d_stage + a_off);
     const auto* d_len = reinterpret_cast<const uint32_t*>(s.d_stage + a_len);
+    const auto* d_seed = reinterpret_cast<const uint32_t*>(s.d_stage + a_seed);
+    const auto* d_desc = reinterpret_cast<const sccsum_gather_desc*>(s.d_stage + a_desc);
     auto* d_out = reinterpret_cast<uint16_t*>(s.d_res);
     uint8_t* d_status = s.d_res + 2 * width(b) * n;
-    const int rk = spans ? sccsum_spans(s.d_stage, s.used, d_off, d_len,
-                                        reinterpret_cast<const uint32_t*>(s.d_stage + a_seed), d_out, d_status, n,
-                                        s.max_len, st)
-                         : sccsum_ipv4_frames(s.d_stage, s.used, d_off, d_len, d_out, d_status, n, s.max_len, st);
+    int rk = SCCSUM_OK;
+    if (fused) {
+        const auto* d_first = reinterpret_cast<const uint32_t*>(s.d_stage + a_first);
+        rk = spans ? sccsum_spans_desc(d_desc, d_first, d_off, d_len, d_seed, s.d_stage, d_out, d_status, n,
+                                       s.max_len, st)
+                   : sccsum_ipv4_frames_desc(d_desc, d_first, d_off, d_len, s.d_stage, d_out, d_status, n, s.max_len,
+                                             st);
+    } else {
+        if (s.mapped) {  // gather the zero-copy fragments into the batch, then sum it (diagnostic form)
+            const int rg = sccsum_gather(d_desc, s.ndesc, s.d_stage, st);
+            if (rg != SCCSUM_OK) return rg;
+        }
+        rk = spans ? sccsum_spans(s.d_stage, s.used, d_off, d_len, d_seed, d_out, d_status, n, s.max_len, st)
+                   : sccsum_ipv4_frames(s.d_stage, s.used, d_off, d_len, d_out, d_status, n, s.max_len, st);
+    }
     if (rk != SCCSUM_OK) return rk;
     SCCSUM_TRY(hipMemcpyAsync(s.h_res, s.d_res, (2 * width(b) + 1) * n, hipMemcpyDeviceToHost, st));
     SCCSUM_TRY(hipEventRecord(s.done, st));
@@ -192,6 +253,7 @@ int deliver(sccsum_burst* b, bool wait, bool* did) {
         s.npk = 0;
         s.ndesc = 0;
         s.copied = false;
+        s.mapped = false;
         s.max_len = 0;
         s.st = sccsum_burst::state::free;
         *did = true;
@@ -231,6 +293,7 @@ int sccsum_burst_create(int device, int mode, uint64_t batch_bytes, uint32_t bat
         if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_off, np * 8, hipHostMallocDefault));
         if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_len, np * 4, hipHostMallocDefault));
         if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_seed, np * 4, hipHostMallocDefault));
+        if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_first, (np + 1) * 4, hipHostMallocDefault));
         if (rc == SCCSUM_OK) {
             rc = hip_rc(hipHostMalloc(&s.h_desc, desc_cap(b) * sizeof(sccsum_gather_desc), hipHostMallocDefault));
         }
@@ -265,7 +328,8 @@ static int submit(sccsum_burst* b, const sccsum_fragment* frags, uint32_t nfrag,
         nd += frags[j].size != 0;
     }
     if (L > b->batch_bytes || L > UINT32_MAX) return SCCSUM_EINVAL;  // never fits a batch
-    if (mapped && nd > desc_cap(b)) return SCCSUM_EINVAL;
+    if (!mapped) nd = L != 0;  // a copied packet: one descriptor into the staged bytes
+    if (nd > desc_cap(b)) return SCCSUM_EINVAL;
     for (int attempt = 0; attempt < 2; ++attempt) {
         if (b->open == SIZE_MAX) {
             auto& s = b->slots[b->next_launch];
@@ -277,11 +341,12 @@ static int submit(sccsum_burst* b, const sccsum_fragment* frags, uint32_t nfrag,
         }
         auto& s = b->slots[b->open];
         const uint64_t at = (s.used + 15) & ~uint64_t(15);  // 16-byte aligned starts: full-rate loads
-        if (s.npk == b->batch_packets || at + L > b->batch_bytes || (mapped && s.ndesc + nd > desc_cap(b))) {
+        if (s.npk == b->batch_packets || at + L > b->batch_bytes || s.ndesc + nd > desc_cap(b)) {
             const int rc = launch_slot(b, s);  // full: send it, open the next slot
             if (rc != SCCSUM_OK) return rc;
             continue;
         }
+        s.h_first[s.npk] = s.ndesc;
         uint64_t pos = at;
         for (uint32_t j = 0; j < nfrag; ++j) {
             if (frags[j].size) {
@@ -294,7 +359,9 @@ static int submit(sccsum_burst* b, const sccsum_fragment* frags, uint32_t nfrag,
             }
             pos += frags[j].size;
         }
+        if (!mapped && L) s.h_desc[s.ndesc++] = {nullptr, static_cast<uint32_t>(at), static_cast<uint32_t>(L)};
         s.copied |= !mapped && L;
+        s.mapped |= mapped && L;
         s.h_off[s.npk] = at;
         s.h_len[s.npk] = static_cast<uint32_t>(L);
         s.h_seed[s.npk] = seed;
@@ -353,6 +420,12 @@ int sccsum_burst_drain(sccsum_burst* b) {
     }
     bool did = false;
     return deliver(b, true, &did);
+}
+
+int sccsum_set_burst_fused(int on) {
+    if (on < 0 || on > 2) return SCCSUM_EINVAL;
+    t_fused = on;
+    return SCCSUM_OK;
 }
 
 int sccsum_burst_destroy(sccsum_burst* b) {

@@ -110,6 +110,114 @@ __device__ __forceinline__ uint32_t xcd_block_id() {
 
 // ---------------------------------------------------------------- kernels
 
+// IPv4 frame header from its first 20 bytes as little-endian dwords h0..h4
+// (ip.cc:121-127 verify / ip.cc:266-278 generate): the header checksum, the L4
+// range [l4_off, l4_off + l4_len) of a frame of L bytes (the IP total length,
+// clipped to the frame) and the pseudo-header (ip.hh:70-75) in the
+// little-endian domain — the address words are dwords 3 and 4, then (0, proto)
+// and the big-endian L4 length byte-swapped.
+struct FrameHeader {
+    uint32_t ipc, l4_off, l4_len, pseudo;
+    uint8_t st;
+};
+
+__device__ __forceinline__ FrameHeader frame_header(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3, uint32_t h4,
+                                                    uint32_t L) {
+    FrameHeader F{};
+    F.ipc = ~fold16(static_cast<uint64_t>(h0) + h1 + h2 + h3 + h4) & 0xffffu;
+    const uint32_t ihl = h0 & 0xfu;
+    const uint32_t ip_len = swap16(h0 >> 16);
+    const uint32_t proto = (h2 >> 8) & 0xffu;
+    F.l4_off = 4u * ihl;
+    const uint32_t l4_end = ip_len < L ? ip_len : L;
+    if (L < ip_len) F.st |= SCCSUM_ST_MALFORMED;
+    if (F.l4_off > l4_end) {
+        F.st |= SCCSUM_ST_MALFORMED;
+    } else {
+        F.l4_len = l4_end - F.l4_off;
+    }
+    F.pseudo = fold16(static_cast<uint64_t>(h3 & 0xffffu) + (h3 >> 16) + (h4 & 0xffffu) + (h4 >> 16) + (proto << 8) +
+                      swap16(F.l4_len & 0xffffu));
+    return F;
+}
+
+// One contiguous packet of L bytes at ptr, summed by one wave: U 16-byte
+// units per lane in flight; frame mode reads the IPv4 header with the first
+// units (one round trip) and sums the L4 range only.  S is the folded sum of
+// the summed range at its packet parity (byte-swapped back when ptr is odd),
+// before the pseudo-header / seed.
+struct PacketSum {
+    uint32_t S, ipc, pseudo;
+    uint8_t st;
+};
+
+template <int U, bool IPV4>
+__device__ __forceinline__ PacketSum span_packet(const uint8_t* ptr, uint32_t L, int lane) {
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(ptr);
+    const int head = static_cast<int>(addr & 15u);
+    const uint8_t* a0 = ptr - head;
+    const uint32_t nunits = L ? (static_cast<uint32_t>(head) + L + 15u) >> 4 : 0u;
+
+    // Frame mode: the 20-byte IPv4 header as 5 dwords re-aligned to the
+    // packet start (lanes 0..5 load the covering dwords; lane 5 only when
+    // the packet is not 4-byte aligned, so every dword read holds a
+    // header byte and stays inside the 16-byte unit bound).
+    uint32_t hv = 0;
+    const int s = static_cast<int>(addr & 3u);
+    if (IPV4) {
+        if (lane < 5 || (lane == 5 && s != 0)) {
+            hv = *reinterpret_cast<const uint32_t*>(ptr - s + 4 * lane);
+        }
+    }
+
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t c = static_cast<uint32_t>(u * kWave + lane);
+        v[u] = c < nunits ? load_unit(a0 + 16u * c) : u32x4{0, 0, 0, 0};
+    }
+
+    PacketSum R{};
+    int rs = head;  // summed range, relative to a0
+    int re = head + static_cast<int>(L);
+    if (IPV4) {
+        const uint32_t nxt = static_cast<uint32_t>(
+            __builtin_amdgcn_update_dpp(0, static_cast<int>(hv), 0x101, 0xF, 0xF, false));  // row_shl:1
+        const uint32_t al = __builtin_amdgcn_alignbyte(nxt, hv, static_cast<uint32_t>(s));
+        const FrameHeader F = frame_header(
+            __builtin_amdgcn_readlane(al, 0), __builtin_amdgcn_readlane(al, 1), __builtin_amdgcn_readlane(al, 2),
+            __builtin_amdgcn_readlane(al, 3), __builtin_amdgcn_readlane(al, 4), L);
+        R.ipc = F.ipc;
+        R.st = F.st;
+        R.pseudo = F.pseudo;
+        rs = head + static_cast<int>(F.l4_off);
+        re = rs + static_cast<int>(F.l4_len);
+    }
+
+    uint64_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c16 = 16 * (u * kWave + lane);
+        acc += unit_sum(v[u], rs - c16, re - c16);
+    }
+    for (uint32_t g = U * kWave; g < nunits; g += U * kWave) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = g + static_cast<uint32_t>(u * kWave + lane);
+            v[u] = c < nunits ? load_unit(a0 + 16u * c) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c16 = 16 * static_cast<int>(g + u * kWave + lane);
+            acc += unit_sum(v[u], rs - c16, re - c16);
+        }
+    }
+
+    R.S = fold16(wave_sum(fold16(acc)));
+    if (addr & 1u) R.S = swap16(R.S);  // span starts at an odd address (4*ihl is even)
+    return R;
+}
+
 // U = 16-byte units in flight per lane per group (packet bytes covered by one
 // group = U * 1 KiB).  IPV4 = frame mode (IPv4 header + L4 with pseudo-header).
 template <int U, bool IPV4>
@@ -139,88 +247,12 @@ __global__ __launch_bounds__(kBlock) void csum_kernel(
             }
             continue;
         }
-        const uint8_t* ptr = bytes + o;
-        const uintptr_t addr = reinterpret_cast<uintptr_t>(ptr);
-        const int head = static_cast<int>(addr & 15u);
-        const uint8_t* a0 = ptr - head;
-        const uint32_t nunits = L ? (static_cast<uint32_t>(head) + L + 15u) >> 4 : 0u;
-
-        // Frame mode: the 20-byte IPv4 header as 5 dwords re-aligned to the
-        // packet start (lanes 0..5 load the covering dwords; lane 5 only when
-        // the packet is not 4-byte aligned, so every dword read holds a
-        // header byte and stays inside the 16-byte unit bound).
-        uint32_t hv = 0;
-        const int s = static_cast<int>(addr & 3u);
+        const PacketSum R = span_packet<U, IPV4>(bytes + o, L, lane);
+        uint32_t S = R.S;
+        const uint32_t ipc = R.ipc;
+        const uint8_t st = R.st;
         if (IPV4) {
-            if (lane < 5 || (lane == 5 && s != 0)) {
-                hv = *reinterpret_cast<const uint32_t*>(ptr - s + 4 * lane);
-            }
-        }
-
-        u32x4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t c = static_cast<uint32_t>(u * kWave + lane);
-            v[u] = c < nunits ? load_unit(a0 + 16u * c) : u32x4{0, 0, 0, 0};
-        }
-
-        int rs = head;                        // summed range, relative to a0
-        int re = head + static_cast<int>(L);
-        uint32_t ipc = 0, pseudo = 0;
-        uint8_t st = 0;
-        if (IPV4) {
-            const uint32_t nxt = static_cast<uint32_t>(
-                __builtin_amdgcn_update_dpp(0, static_cast<int>(hv), 0x101, 0xF, 0xF, false));  // row_shl:1
-            const uint32_t al = __builtin_amdgcn_alignbyte(nxt, hv, static_cast<uint32_t>(s));
-            const uint32_t h0 = __builtin_amdgcn_readlane(al, 0);
-            const uint32_t h1 = __builtin_amdgcn_readlane(al, 1);
-            const uint32_t h2 = __builtin_amdgcn_readlane(al, 2);
-            const uint32_t h3 = __builtin_amdgcn_readlane(al, 3);
-            const uint32_t h4 = __builtin_amdgcn_readlane(al, 4);
-            ipc = ~fold16(static_cast<uint64_t>(h0) + h1 + h2 + h3 + h4) & 0xffffu;
-            const uint32_t ihl = h0 & 0xfu;
-            const uint32_t ip_len = swap16(h0 >> 16);
-            const uint32_t proto = (h2 >> 8) & 0xffu;
-            const uint32_t l4_off = 4u * ihl;
-            const uint32_t l4_end = ip_len < L ? ip_len : L;
-            uint32_t l4_len = 0;
-            if (L < ip_len) st |= SCCSUM_ST_MALFORMED;
-            if (l4_off > l4_end) {
-                st |= SCCSUM_ST_MALFORMED;
-            } else {
-                l4_len = l4_end - l4_off;
-            }
-            rs = head + static_cast<int>(l4_off);
-            re = rs + static_cast<int>(l4_len);
-            // pseudo-header in the little-endian domain: the address words are
-            // header dwords 3 and 4; (0, proto) and the big-endian length swap.
-            pseudo = fold16(static_cast<uint64_t>(h3 & 0xffffu) + (h3 >> 16) + (h4 & 0xffffu) + (h4 >> 16) +
-                            (proto << 8) + swap16(l4_len & 0xffffu));
-        }
-
-        uint64_t acc = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int c16 = 16 * (u * kWave + lane);
-            acc += unit_sum(v[u], rs - c16, re - c16);
-        }
-        for (uint32_t g = U * kWave; g < nunits; g += U * kWave) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t c = g + static_cast<uint32_t>(u * kWave + lane);
-                v[u] = c < nunits ? load_unit(a0 + 16u * c) : u32x4{0, 0, 0, 0};
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int c16 = 16 * static_cast<int>(g + u * kWave + lane);
-                acc += unit_sum(v[u], rs - c16, re - c16);
-            }
-        }
-
-        uint32_t S = fold16(wave_sum(fold16(acc)));
-        if (addr & 1u) S = swap16(S);  // span starts at an odd address (4*ihl is even)
-        if (IPV4) {
-            S = fold16(static_cast<uint64_t>(S) + pseudo);
+            S = fold16(static_cast<uint64_t>(S) + R.pseudo);
         } else if (seed && !raw) {
             S = fold16(static_cast<uint64_t>(S) + swap16(fold16(seed[p])));
         }
@@ -1396,6 +1428,7 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const sccsum_gather_desc
     const uint64_t nw = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
     for (uint64_t w = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6; w < n; w += nw) {
         const sccsum_gather_desc d = desc[w];
+        if (!d.src) continue;  // already in the batch (a copied packet of a mixed burst)
         const uint8_t* src = static_cast<const uint8_t*>(d.src);
         uint8_t* o = dst + d.dst_off;
         const uintptr_t a = reinterpret_cast<uintptr_t>(o), e = a + d.len;
@@ -1410,6 +1443,217 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const sccsum_gather_desc
             }
         }
     }
+}
+
+// ---- fragment-list kernel: packets given as descriptor lists over
+// device-readable memory (HBM, or pinned / registered host memory read over
+// PCIe), summed where they lie — the bytes are read once, straight into the
+// sum, with no gather into a contiguous batch first (checksummer::sum(const
+// packet&), ip_checksum.cc:64-68, over fragments anywhere).  Packet p has
+// fragments desc[first[p] .. first[p+1]); fragment j holds packet bytes
+// [dst_off_j - off[p], + len_j) — they must tile [0, len[p]) in order — and
+// lies at src_j, or at stage + dst_off_j when src_j is NULL (bytes already in
+// the batch).  One wave per packet at a time (grid-stride; a wave loads the
+// metadata of its next 64 packets one per lane first), U 16-byte units per
+// lane in flight; a one-fragment packet takes the contiguous-span path.  A fragment's bytes are summed at their address parity and the
+// fragment's folded sum byte-swapped when its address and its packet offset
+// differ in parity (the odd carry of the reference's fragment loop).
+template <int U, bool IPV4>
+__global__ __launch_bounds__(kBlock) void csum_desc_kernel(
+    const sccsum_gather_desc* __restrict__ desc, const uint32_t* __restrict__ first,
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len, const uint32_t* __restrict__ seed,
+    const uint8_t* __restrict__ stage, uint16_t* __restrict__ out, uint8_t* __restrict__ status, uint64_t n,
+    uint32_t flags) {
+    const bool raw = !IPV4 && (flags & kFlagRaw);
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+    auto frag_addr = [&](const sccsum_gather_desc& d) {
+        return d.src ? reinterpret_cast<uintptr_t>(d.src) : reinterpret_cast<uintptr_t>(stage + d.dst_off);
+    };
+
+    auto rl32 = [](uint32_t v, uint32_t k) {
+        return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(k)));
+    };
+    auto rl64 = [&](uint64_t v, uint32_t k) {
+        return static_cast<uint64_t>(rl32(static_cast<uint32_t>(v), k)) |
+               static_cast<uint64_t>(rl32(static_cast<uint32_t>(v >> 32), k)) << 32;
+    };
+    // A wave's packets are p0, p0 + stride, ...: their metadata and first
+    // descriptors are loaded 64 at a time, one packet per lane (two round trips
+    // for up to 64 packets — over PCIe when the arrays are pinned host memory),
+    // then each packet costs one round trip for its bytes.
+    const uint64_t p0 = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
+    for (uint64_t base = p0; base < n; base += kWave * stride) {
+        const uint64_t q = base + lane * stride;
+        uint64_t m_off = 0, m_src = 0;
+        uint32_t m_len = 0, m_f0 = 0, m_f1 = 0, m_dst = 0, m_dlen = 0;
+        if (q < n) {
+            m_off = off[q];
+            m_len = len[q];
+            m_f0 = first[q];
+            m_f1 = first[q + 1];
+        }
+        if (q < n && m_f1 > m_f0) {
+            const sccsum_gather_desc d = desc[m_f0];
+            m_src = reinterpret_cast<uint64_t>(d.src);
+            m_dst = d.dst_off;
+            m_dlen = d.len;
+        }
+        const uint64_t left = (n - base + stride - 1) / stride;
+        const uint32_t cnt = left < kWave ? static_cast<uint32_t>(left) : kWave;
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const uint64_t p = base + k * stride;
+            const uint64_t o = rl64(m_off, k);
+            const uint32_t L = rl32(m_len, k);
+            const uint32_t f0 = rl32(m_f0, k), f1 = rl32(m_f1, k);
+            sccsum_gather_desc d0{};
+            d0.src = reinterpret_cast<const void*>(rl64(m_src, k));
+            d0.dst_off = rl32(m_dst, k);
+            d0.len = rl32(m_dlen, k);
+            // the fragments must tile the packet: [0, L) in order, no gaps
+            bool bad = f1 < f0;
+            if (f1 - f0 == 1) {
+                bad = d0.dst_off != o || d0.len != L || (!d0.src && !stage);
+            } else if (!bad) {
+                uint64_t at = 0;
+                for (uint32_t j = f0; j < f1 && !bad; ++j) {
+                    const sccsum_gather_desc d = desc[j];
+                    bad = static_cast<uint64_t>(d.dst_off) != o + at || (!d.src && !stage);
+                    at += d.len;
+                }
+                bad = bad || at != L;
+            }
+            if (bad || (IPV4 && L < 20)) {
+                if (lane == 0) {
+                    if (IPV4) {
+                        reinterpret_cast<uint32_t*>(out)[p] = 0;
+                    } else {
+                        out[p] = 0;
+                    }
+                    if (status) status[p] = bad ? SCCSUM_ST_RANGE : SCCSUM_ST_MALFORMED;
+                }
+                continue;
+            }
+
+            uint32_t S = 0, ipc = 0, pseudo = 0;
+            uint8_t st = 0;
+            if (f1 - f0 <= 1) {
+                // one fragment (or an empty packet): the contiguous-span path, header
+                // and first units in one round trip
+                const uint8_t* ptr = L ? reinterpret_cast<const uint8_t*>(frag_addr(d0)) : stage;
+                const PacketSum R = span_packet<U, IPV4>(ptr, L, static_cast<int>(lane));
+                S = R.S;
+                ipc = R.ipc;
+                pseudo = R.pseudo;
+                st = R.st;
+            } else {
+                uint32_t rs = 0, re = L;
+                if (IPV4) {
+                    // header byte `lane` (lanes 0..19) from whichever fragment holds it
+                    uint32_t hb = 0;
+                    if (lane < 20u) {
+                        uint32_t at = 0;
+                        for (uint32_t j = f0; j < f1; ++j) {
+                            const sccsum_gather_desc d = desc[j];
+                            if (lane < at + d.len) {
+                                hb = reinterpret_cast<const uint8_t*>(frag_addr(d))[lane - at];
+                                break;
+                            }
+                            at += d.len;
+                        }
+                    }
+                    uint32_t h[5];
+    #pragma unroll
+                    for (int k = 0; k < 5; ++k) {
+                        h[k] = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(hb), 4 * k)) |
+                               static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(hb), 4 * k + 1)) << 8 |
+                               static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(hb), 4 * k + 2)) << 16 |
+                               static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(hb), 4 * k + 3)) << 24;
+                    }
+                    const FrameHeader F = frame_header(h[0], h[1], h[2], h[3], h[4], L);
+                    ipc = F.ipc;
+                    st = F.st;
+                    pseudo = F.pseudo;
+                    rs = F.l4_off;
+                    re = F.l4_off + F.l4_len;
+                }
+                uint64_t acc = 0;  // per lane: folded fragment partials, each at its packet parity
+                uint32_t at = 0;   // packet offset of fragment j
+                for (uint32_t j = f0; j < f1; ++j) {
+                    const sccsum_gather_desc d = desc[j];
+                    const uint32_t lo = rs > at ? rs : at;
+                    const uint32_t hi = re < at + d.len ? re : at + d.len;
+                    if (lo < hi) {
+                        const uintptr_t A = frag_addr(d);
+                        const uint32_t head = static_cast<uint32_t>(A & 15u);
+                        const uint8_t* a0 = reinterpret_cast<const uint8_t*>(A - head);
+                        // the summed bytes, relative to the aligned base a0
+                        const int ulo = static_cast<int>(head + lo - at), uhi = static_cast<int>(head + hi - at);
+                        const uint32_t c0 = static_cast<uint32_t>(ulo) >> 4;
+                        const uint32_t c1 = (static_cast<uint32_t>(uhi) + 15u) >> 4;
+                        uint64_t part = 0;
+                        for (uint32_t g = c0; g < c1; g += U * kWave) {
+                            u32x4 v[U];
+    #pragma unroll
+                            for (int u = 0; u < U; ++u) {
+                                const uint32_t c = g + static_cast<uint32_t>(u * kWave) + lane;
+                                v[u] = c < c1 ? load_unit(a0 + 16u * c) : u32x4{0, 0, 0, 0};
+                            }
+    #pragma unroll
+                            for (int u = 0; u < U; ++u) {
+                                const int c16 = 16 * static_cast<int>(g + u * kWave + lane);
+                                part += unit_sum(v[u], ulo - c16, uhi - c16);
+                            }
+                        }
+                        uint32_t f = fold16(part);
+                        if ((A ^ at) & 1u) f = swap16(f);
+                        acc += f;
+                    }
+                    at += d.len;
+                }
+                S = fold16(wave_sum(fold16(acc)));
+            }
+
+            if (IPV4) {
+                S = fold16(static_cast<uint64_t>(S) + pseudo);
+            } else if (seed && !raw) {
+                S = fold16(static_cast<uint64_t>(S) + swap16(fold16(seed[p])));
+            }
+            const uint32_t r = raw ? S : ~S & 0xffffu;
+            if (lane == 0) {
+                if (IPV4) {
+                    reinterpret_cast<uint32_t*>(out)[p] = ipc | (r << 16);
+                    if (status) status[p] = st | (ipc == 0 ? SCCSUM_ST_OK : 0u) | (r == 0 ? SCCSUM_ST_L4_OK : 0u);
+                } else {
+                    out[p] = static_cast<uint16_t>(r);
+                    if (status) status[p] = (!raw && r == 0) ? SCCSUM_ST_OK : 0u;
+                }
+            }
+        }
+    }
+}
+
+template <bool IPV4>
+int launch_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const uint64_t* d_off,
+                const uint32_t* d_len, const uint32_t* d_seed, const void* d_stage, uint16_t* d_out, uint8_t* d_status,
+                uint64_t n, uint32_t max_len, void* stream) {
+    if (n == 0) return SCCSUM_OK;
+    if (!d_desc || !d_first || !d_off || !d_len || !d_out || (reinterpret_cast<uintptr_t>(d_desc) & 7u) ||
+        (reinterpret_cast<uintptr_t>(d_first) & 3u) || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
+        (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_seed) & 3u) ||
+        (reinterpret_cast<uintptr_t>(d_out) & (IPV4 ? 3u : 1u))) {
+        return SCCSUM_EINVAL;
+    }
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const auto* st = static_cast<const uint8_t*>(d_stage);
+    const dim3 g(grid_for(n)), t(kBlock);
+    switch (units_class(max_len)) {
+        case 1: csum_desc_kernel<1, IPV4><<<g, t, 0, s>>>(d_desc, d_first, d_off, d_len, d_seed, st, d_out, d_status, n, 0); break;
+        case 2: csum_desc_kernel<2, IPV4><<<g, t, 0, s>>>(d_desc, d_first, d_off, d_len, d_seed, st, d_out, d_status, n, 0); break;
+        default: csum_desc_kernel<4, IPV4><<<g, t, 0, s>>>(d_desc, d_first, d_off, d_len, d_seed, st, d_out, d_status, n, 0); break;
+    }
+    return static_cast<int>(hipGetLastError());
 }
 
 }  // namespace
@@ -1510,6 +1754,20 @@ int sccsum_gather(const sccsum_gather_desc* d_desc, uint64_t n, void* d_dst, voi
     sccsum::gather_kernel<<<dim3(static_cast<unsigned>(blocks)), dim3(sccsum::kBlock), 0,
                             static_cast<hipStream_t>(stream)>>>(d_desc, n, static_cast<uint8_t*>(d_dst));
     return static_cast<int>(hipGetLastError());
+}
+
+int sccsum_spans_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const uint64_t* d_off,
+                      const uint32_t* d_len, const uint32_t* d_seed, const void* d_stage, uint16_t* d_out,
+                      uint8_t* d_status, uint64_t n, uint32_t max_len, void* stream) {
+    return sccsum::launch_desc<false>(d_desc, d_first, d_off, d_len, d_seed, d_stage, d_out, d_status, n, max_len,
+                                      stream);
+}
+
+int sccsum_ipv4_frames_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const uint64_t* d_off,
+                            const uint32_t* d_len, const void* d_stage, uint16_t* d_out2, uint8_t* d_status,
+                            uint64_t n, uint32_t max_len, void* stream) {
+    return sccsum::launch_desc<true>(d_desc, d_first, d_off, d_len, nullptr, d_stage, d_out2, d_status, n, max_len,
+                                     stream);
 }
 
 uint64_t sccsum_fragments_workspace(uint64_t nfrag) { return ((2 * nfrag + 15) & ~uint64_t(15)) + nfrag + 16; }

@@ -82,6 +82,9 @@ _PROTOS = {
     "sccsum_burst_submit": (ctypes.c_int, [_vp, _vp, _u32, _u32, ctypes.POINTER(_u64)]),
     "sccsum_burst_submit_mapped": (ctypes.c_int, [_vp, _vp, _u32, _u32, ctypes.POINTER(_u64)]),
     "sccsum_gather": (ctypes.c_int, [_vp, _u64, _vp, _vp]),
+    "sccsum_spans_desc": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),
+    "sccsum_ipv4_frames_desc": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),
+    "sccsum_set_burst_fused": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_burst_poll": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "sccsum_burst_drain": (ctypes.c_int, [_vp]),
     "sccsum_burst_destroy": (ctypes.c_int, [_vp]),

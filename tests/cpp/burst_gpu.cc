@@ -6,10 +6,17 @@
 // an odd offset (the `odd` carry of checksummer::sum(const packet&),
 // ip_checksum.cc:64-68).  Every result is checked against the per-packet API;
 // the hook's throughput is printed.  Usage: burst_gpu [frames] [depth]
-// [max_delay_ns] [copy|mapped]: mapped = the pool is pinned (as a DPDK mempool
-// registered with the device) and frames go in by zero-copy submit_mapped.
+// [max_delay_ns] [copy|copy_pageable|mapped] [poll_every] [fused] [pool_slots]:
+// copy_pageable = copied from an ordinary malloc'd pool; mapped = the pool is pinned (as a
+// DPDK mempool registered with the device) and frames go in by zero-copy
+// submit_mapped; poll_every = frames handed over between reactor polls
+// (default 32, one rx burst); fused = how zero-copy batches run
+// (sccsum_set_burst_fused: 2 one launch on pinned metadata, the default; 1
+// with metadata / result copies; 0 gather, then sum).  The time spent inside poll() is
+// reported apart.
 #include <seastar/net/ip_checksum.hh>
 #include <seastar/net/ip_checksum_batch.hh>
+#include <sccsum_diag.h>
 
 #include <arpa/inet.h>
 
@@ -27,11 +34,22 @@ int main(int argc, char** argv) {
     const int depth = argc > 2 ? std::atoi(argv[2]) : 4;
     const uint64_t delay_ns = argc > 3 ? std::strtoull(argv[3], nullptr, 0) : 100000;
     constexpr uint32_t kSlot = 2304, kData = 256;
-    const uint32_t pool_n = static_cast<uint32_t>(n < 65536 ? n : 65536);  // slots, reused round robin
+    uint64_t pool_cap = argc > 7 ? std::strtoull(argv[7], nullptr, 0) : 65536;  // slots, reused round robin
+    pool_cap = pool_cap ? pool_cap : 1;
+    const uint32_t pool_n = static_cast<uint32_t>(n < pool_cap ? n : pool_cap);
     std::mt19937 rng(11);
     const bool mapped = argc > 4 && std::strcmp(argv[4], "mapped") == 0;
+    const bool pageable = argc > 4 && std::strcmp(argv[4], "copy_pageable") == 0;
+    const uint64_t poll_every = argc > 5 ? std::strtoull(argv[5], nullptr, 0) : 32;
+    const int fused = argc > 6 ? std::atoi(argv[6]) : 2;
+    if (sccsum_set_burst_fused(fused) != SCCSUM_OK) {
+        std::printf("FAILED: fused must be 0, 1 or 2\n");
+        return 2;
+    }
     uint8_t* pool = nullptr;
-    if (sccsum_host_alloc(reinterpret_cast<void**>(&pool), uint64_t(pool_n) * kSlot) != SCCSUM_OK) {
+    if (pageable) {
+        pool = static_cast<uint8_t*>(std::aligned_alloc(4096, uint64_t(pool_n) * kSlot));
+    } else if (sccsum_host_alloc(reinterpret_cast<void**>(&pool), uint64_t(pool_n) * kSlot) != SCCSUM_OK) {
         std::printf("FAILED: sccsum_host_alloc\n");
         return 2;
     }
@@ -74,11 +92,17 @@ int main(int argc, char** argv) {
         delivered += count;
     };
     int bad = 0;
-    uint64_t busy = 0, bytes = 0;
-    double secs = 0;
+    uint64_t busy = 0, bytes = 0, polls = 0;
+    double secs = 0, poll_secs = 0;
     try {
         burst_queue<decltype(done)> q(0, SCCSUM_PIPE_IPV4, 16u << 20, 16384, delay_ns, depth, done);
         const auto t0 = std::chrono::steady_clock::now();
+        auto timed_poll = [&] {
+            const auto a = std::chrono::steady_clock::now();
+            q.poll();
+            poll_secs += std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+            ++polls;
+        };
         for (uint64_t i = 0; i < n; ++i) {
             const uint32_t k = static_cast<uint32_t>(i % pool_n);
             const uint8_t* f = pool + size_t(k) * kSlot + kData;
@@ -92,11 +116,11 @@ int main(int argc, char** argv) {
             uint64_t t = 0;
             while (!(mapped ? q.submit_mapped(fr, nf, 0, &t) : q.submit(fr, nf, 0, &t))) {
                 ++busy;
-                q.poll();
+                timed_poll();
             }
             if (t != i && bad++ < 5) std::printf("ticket %llu for packet %llu\n", (unsigned long long)t, (unsigned long long)i);
             bytes += len[k];
-            if ((i & 31) == 31) q.poll();  // a burst of 32 handed over: the reactor runs its pollers
+            if ((i + 1) % poll_every == 0) timed_poll();  // a burst handed over: the reactor runs its pollers
         }
         q.drain();
         secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -116,10 +140,14 @@ int main(int argc, char** argv) {
         }
     }
     std::printf("burst_gpu: %llu frames, %.1f MB, %llu batches, depth %d, delay %llu ns, %s, %.3f s: %.2f Mpkt/s, %.2f GiB/s of packet "
-                "bytes, %llu busy polls\n",
+                "bytes, %llu busy polls, %llu polls %.3f s in poll, %s, pool %u slots\n",
                 (unsigned long long)n, bytes / 1e6, (unsigned long long)batches, depth, (unsigned long long)delay_ns, mapped ? "mapped" : "copy", secs, n / secs / 1e6,
-                bytes / secs / (1u << 30), (unsigned long long)busy);
-    sccsum_host_free(pool);
+                bytes / secs / (1u << 30), (unsigned long long)busy, (unsigned long long)polls, poll_secs, mapped ? (fused == 2 ? "zero-copy launch" : fused ? "fused+copies" : "gather+sum") : pageable ? "staged from pageable" : "staged from pinned", pool_n);
+    if (pageable) {
+        std::free(pool);
+    } else {
+        sccsum_host_free(pool);
+    }
     if (bad) {
         std::printf("FAILED: %d mismatches\n", bad);
         return 1;

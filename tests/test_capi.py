@@ -138,3 +138,21 @@ def test_multi_batch_argument_validation_without_device():
     assert lib.sccsum_ipv4_frames_multi(ctypes.cast(arr, ctypes.c_void_p), 1, 0, None) == native.SCCSUM_EINVAL
     arr[0] = native.Batch(17, 64, 0x1000, 0x2000, None, 0x4000, None, 3)  # misaligned bytes
     assert lib.sccsum_spans_multi(ctypes.cast(arr, ctypes.c_void_p), 1, 0, None) == native.SCCSUM_EINVAL
+
+
+def test_desc_argument_validation_without_device():
+    """sccsum_*_desc refuse null / misaligned arrays before any device call."""
+    lib = native.load()
+    p = 0x10000
+    assert lib.sccsum_ipv4_frames_desc(None, None, None, None, None, None, None, 0, 0, None) == native.SCCSUM_OK
+    assert lib.sccsum_ipv4_frames_desc(None, p, p, p, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_frames_desc(p, None, p, p, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_spans_desc(p + 4, p, p, p, None, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_spans_desc(p, p + 2, p, p, None, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_spans_desc(p, p, p + 4, p, None, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_spans_desc(p, p, p, p + 1, None, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_spans_desc(p, p, p, p, p + 2, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_spans_desc(p, p, p, p, None, None, p + 1, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_frames_desc(p, p, p, p, None, p + 2, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_set_burst_fused(3) == native.SCCSUM_EINVAL
+    assert lib.sccsum_set_burst_fused(2) == native.SCCSUM_OK

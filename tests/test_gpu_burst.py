@@ -81,6 +81,16 @@ def test_burst_frames_and_backpressure(dev):
     q1.close()
 
 
+@pytest.fixture(params=[2, 1, 0], ids=["zero_copy", "fused", "gather"])
+def fused(request):
+    """Zero-copy batches: one fragment-list launch on pinned metadata (default),
+    the same kernel between metadata / result copies, or gathered first."""
+    lib = native.load()
+    assert lib.sccsum_set_burst_fused(request.param) == native.SCCSUM_OK
+    yield request.param
+    lib.sccsum_set_burst_fused(2)
+
+
 def _pinned_copy(buf):
     from seastar_amd import pipeline
 
@@ -89,9 +99,9 @@ def _pinned_copy(buf):
     return pool
 
 
-def test_burst_mapped_zero_copy(dev):
-    """sccsum_burst_submit_mapped: fragments in pinned host memory, gathered
-    over PCIe by the device; odd fragment cuts, empty packets, seeds."""
+def test_burst_mapped_zero_copy(dev, fused):
+    """sccsum_burst_submit_mapped: fragments in pinned host memory, read over
+    PCIe by the device; odd fragment cuts, empty packets, seeds."""
     rng = np.random.default_rng(55)
     lens = np.concatenate([rng.integers(0, 2100, 2500), [0, 1, 9000, 65535]]).astype(np.uint32)
     off, total = synth.pack(lens, seed=56, max_gap=5)
@@ -114,9 +124,10 @@ def test_burst_mapped_zero_copy(dev):
     q.close()
 
 
-def test_burst_mixed_copy_and_mapped(dev):
+def test_burst_mixed_copy_and_mapped(dev, fused):
     """Copied and zero-copy packets alternate inside the same batches (the
-    H2D then carries the staged bytes and the gather fills the rest)."""
+    H2D then carries the staged bytes; the fragment-list kernel reads those
+    from the batch and the rest where they lie)."""
     host, off, lens, _ = synth.mixed_udp_frames(1200, seed=57, max_gap=3)
     want, want_st = oracle.batch_ipv4(host, off, lens)
     buf = _pinned_copy(host)
@@ -239,3 +250,30 @@ def test_callback_reentrancy(dev):
     assert all(code == native.SCCSUM_EINVAL for code in inner)
     q.close()
     assert ctypes.sizeof(ctypes.c_void_p) == 8
+
+
+def test_burst_mapped_recycled_buffers(dev, fused):
+    """Zero-copy submits from a small pinned pool whose slots the host rewrites
+    after every drain (recycled mbufs): no batch may see an earlier batch's
+    bytes."""
+    from seastar_amd import pipeline
+
+    rng = np.random.default_rng(81)
+    nslot, slot = 64, 2304
+    pool = pipeline.pinned_empty(nslot * slot)
+    q = BurstQueue(native.PIPE_SPANS, batch_bytes=256 << 10, batch_packets=32, max_delay_ns=0, depth=2)
+    for rnd in range(10):
+        lens = rng.integers(0, 2049, nslot).astype(np.uint32)
+        pool[:] = rng.integers(0, 256, pool.size, dtype=np.uint8)
+        tickets = []
+        for i in range(nslot):
+            pkt = pool[i * slot + 128:i * slot + 128 + int(lens[i])]
+            while (t := q.submit(_split(rng, pkt), 0, mapped=True)) is None:
+                q.poll()
+            tickets.append(t)
+        q.drain()
+        off = (np.arange(nslot, dtype=np.uint64) * slot + 128)
+        want = oracle.batch_spans(np.array(pool), off, lens, np.zeros(nslot, np.uint32))
+        got = np.array([int(q.results[t]) for t in tickets], np.uint16)
+        assert np.array_equal(got, want), rnd
+    q.close()

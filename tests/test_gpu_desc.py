@@ -1,0 +1,189 @@
+"""Fragment-list kernel (sccsum_spans_desc / sccsum_ipv4_frames_desc) against
+the oracle: packets given as fragment descriptors anywhere the device can read
+— pinned host memory over PCIe, device memory, the stage buffer — summed where
+they lie (checksummer::sum(const packet&), ip_checksum.cc:64-68, with the
+fragments of packet_test.cc-style chains: odd cuts, empty pieces, headers split
+across fragments)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from seastar_amd import batch, native, pipeline, synth
+from test_gpu_parity import _tx_frames
+
+pytestmark = pytest.mark.gpu
+
+
+def _scatter(rng, buf, off, lens, pool_base, pool_len, stage_frac=0.0, header_cuts=True):
+    """Cut every packet into 1-5 fragments (odd cuts, cuts inside the first 20
+    bytes, empty pieces dropped as the burst queue drops them) and place each
+    at a random position of a pool (shuffled, any alignment).  Returns the
+    descriptor records, first[], the packets' layout offsets and the pool image
+    and the stage image (fragments with src = 0 live there at dst_off)."""
+    n = lens.size
+    lay_off = np.zeros(n, np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(rng.integers(0, 4))
+        lay_off[i] = pos
+        pos += int(lens[i])
+    stage = np.zeros(pos + 64, np.uint8)
+    pieces = []  # (packet, inner offset, length)
+    first = np.zeros(n + 1, np.int32)
+    for i in range(n):
+        L = int(lens[i])
+        k = int(rng.integers(0, 5))
+        cuts = set(int(c) for c in rng.integers(0, L + 1, size=k))
+        if header_cuts and L > 3 and rng.random() < 0.2:
+            cuts.add(int(rng.integers(1, min(L, 20))))
+        edges = [0, *sorted(cuts), L]
+        first[i] = len(pieces)
+        for a, b in zip(edges[:-1], edges[1:]):
+            if b > a:
+                pieces.append((i, a, b - a))
+    first[n] = len(pieces)
+    nd = len(pieces)
+    order = rng.permutation(nd)
+    pool = rng.integers(0, 256, size=pool_len, dtype=np.uint8)
+    src = np.zeros(nd, np.uint64)
+    at = int(rng.integers(0, 16))
+    for j in order:
+        i, a, ln = pieces[j]
+        o = int(off[i]) + a
+        if rng.random() < stage_frac:
+            d = int(lay_off[i]) + a
+            stage[d:d + ln] = buf[o:o + ln]
+            continue  # src stays 0: in the stage
+        assert at + ln <= pool_len
+        pool[at:at + ln] = buf[o:o + ln]
+        src[j] = pool_base + at
+        at += ln + int(rng.integers(0, 40))
+    dst = np.array([int(lay_off[i]) + a for i, a, _ in pieces], np.uint64)
+    ln = np.array([p[2] for p in pieces], np.uint32)
+    return batch.make_desc(src, dst, ln), first, lay_off, pool, stage
+
+
+def _dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    return (t if dtype is None else t.view(dtype)).to("cuda:0")
+
+
+@pytest.mark.parametrize("where", ["pinned", "device", "stage_mix"])
+def test_frames_desc_against_oracle(dev, where):
+    rng = np.random.default_rng(71)
+    buf, off, lens = _tx_frames(rng, 3000)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
+    pool_len = int(lens.sum()) + 40 * 16000 + 64
+    if where == "pinned":
+        host = pipeline.pinned_empty(pool_len)
+        base = host.ctypes.data
+    else:
+        dpool = torch.empty(pool_len, dtype=torch.uint8, device=dev)
+        base = dpool.data_ptr()
+    desc, first, lay, pool, stage = _scatter(rng, buf, off, lens, base, pool_len,
+                                             stage_frac=0.4 if where == "stage_mix" else 0.0)
+    if where == "pinned":
+        host[:] = pool
+    else:
+        dpool.copy_(torch.from_numpy(pool))
+    status = torch.zeros(lens.size, dtype=torch.uint8, device=dev)
+    got = batch.ipv4_frames_desc(_dev(desc.view(np.uint8)), _dev(first), _dev(lay.view(np.int64)),
+                                 _dev(lens.view(np.int32)), int(lens.max()), stage=_dev(stage), status=status)
+    torch.cuda.synchronize()
+    assert np.array_equal(batch.as_u16(got), want)
+    assert np.array_equal(status.cpu().numpy(), want_st)
+
+
+def test_spans_desc_seeds_lengths_and_big_packets(dev):
+    rng = np.random.default_rng(72)
+    lens = np.concatenate([rng.integers(0, 2100, 4000), [0, 1, 2, 15, 16, 17, 9000, 65535, 70000]]).astype(np.uint32)
+    off, total = synth.pack(lens, seed=73, max_gap=3)
+    buf = rng.integers(0, 256, size=max(int(total), 1), dtype=np.uint8)
+    seeds = rng.integers(0, 1 << 32, lens.size, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch_spans(buf, off, lens, seeds)
+    pool_len = int(lens.sum()) + 40 * 20000 + 64
+    host = pipeline.pinned_empty(pool_len)
+    desc, first, lay, pool, stage = _scatter(rng, buf, off, lens, host.ctypes.data, pool_len, stage_frac=0.2,
+                                             header_cuts=False)
+    host[:] = pool
+    got = batch.spans_desc(_dev(desc.view(np.uint8)), _dev(first), _dev(lay.view(np.int64)),
+                           _dev(lens.view(np.int32)), int(lens.max()), seeds=_dev(seeds.view(np.int32)),
+                           stage=_dev(stage))
+    torch.cuda.synchronize()
+    assert np.array_equal(batch.as_u16(got), want)
+
+
+def test_desc_fragments_that_do_not_tile_are_refused_per_packet(dev):
+    """A gap, an overlap, a wrong first offset, a short total, a stage fragment
+    with no stage: result 0 + SCCSUM_ST_RANGE for that packet only."""
+    rng = np.random.default_rng(74)
+    buf, off, lens, _ = synth.mixed_udp_frames(64, seed=75)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
+    d_buf = _dev(buf)
+    base = d_buf.data_ptr()
+    # one fragment per packet, straight from the device copy (layout = the buffer's own offsets)
+    desc = batch.make_desc(base + off, off, lens)
+    first = np.arange(lens.size + 1, dtype=np.int32)
+    bad = {3: ("dst_off", 1), 7: ("len", -1), 11: ("len", 1), 15: ("src0", 0)}
+    for i, (field, delta) in bad.items():
+        if field == "src0":
+            desc["src"][i] = 0
+        else:
+            desc[field][i] = int(desc[field][i]) + delta
+    status = torch.zeros(lens.size, dtype=torch.uint8, device=dev)
+    got = batch.ipv4_frames_desc(_dev(desc.view(np.uint8)), _dev(first), _dev(off.astype(np.uint64).view(np.int64)),
+                                 _dev(lens.view(np.int32)), int(lens.max()), stage=None, status=status)
+    torch.cuda.synchronize()
+    g = batch.as_u16(got)
+    st = status.cpu().numpy()
+    for i in range(lens.size):
+        if i in bad:
+            assert tuple(g[i]) == (0, 0) and st[i] == native.ST_RANGE, i
+        else:
+            assert tuple(g[i]) == tuple(want[i]) and st[i] == want_st[i], i
+
+
+def test_desc_argument_checks(dev):
+    import ctypes
+
+    lib = native.load()
+    t = torch.zeros(64, dtype=torch.int64, device=dev)
+    p = t.data_ptr()
+    assert lib.sccsum_ipv4_frames_desc(None, None, None, None, None, None, None, 0, 0, None) == native.SCCSUM_OK
+    assert lib.sccsum_ipv4_frames_desc(None, p, p, p, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_spans_desc(p + 4, p, p, p, None, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_spans_desc(p, p, p + 4, p, None, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_spans_desc(p, p, p, p, None, None, p + 1, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert ctypes.sizeof(ctypes.c_void_p) == 8
+
+
+def test_desc_rereads_rewritten_host_memory(dev):
+    """The same pinned slots rewritten by the host between launches (an mbuf
+    pool recycles its buffers): every launch must see the new bytes, not lines
+    an earlier launch left in the GPU's caches."""
+    rng = np.random.default_rng(76)
+    n, slot = 256, 2304
+    host = pipeline.pinned_empty(n * slot)
+    src_off = np.arange(n, dtype=np.uint64) * slot + 256
+    lens = rng.integers(28, 1501, n).astype(np.uint32)
+    lay, _ = synth.pack(lens)
+    desc = batch.make_desc(host.ctypes.data + src_off, lay, lens)
+    d_desc, d_first = _dev(desc.view(np.uint8)), _dev(np.arange(n + 1, dtype=np.int32))
+    d_off, d_len = _dev(lay.astype(np.uint64).view(np.int64)), _dev(lens.view(np.int32))
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    for rnd in range(12):
+        buf, off, _, _ = synth.mixed_udp_frames(n, seed=100 + rnd)
+        frames = np.zeros(int(lay[-1]) + 1600, np.uint8)
+        for i in range(n):
+            L = int(lens[i])
+            pkt = buf[int(off[i]):int(off[i]) + L]
+            if pkt.size < L:
+                pkt = np.concatenate([pkt, rng.integers(0, 256, L - pkt.size, dtype=np.uint8)])
+            host[int(src_off[i]):int(src_off[i]) + L] = pkt
+            frames[int(lay[i]):int(lay[i]) + L] = pkt
+        want, want_st = oracle.batch_ipv4(frames, lay, lens)
+        got = batch.ipv4_frames_desc(d_desc, d_first, d_off, d_len, 1500, status=status)
+        torch.cuda.synchronize()
+        assert np.array_equal(batch.as_u16(got), want), rnd
+        assert np.array_equal(status.cpu().numpy(), want_st), rnd

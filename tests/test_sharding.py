@@ -1,7 +1,9 @@
 """Multi-rank sharding on CPU: world_size 2 over gloo.
-Each rank takes its byte-balanced shard, checksums it (the oracle stands in
-for the per-rank GPU engine here), results are gathered by index and must
-equal the unsharded batch; no data-path collective is involved."""
+Each rank takes its byte-balanced shard, checksums it, results are gathered
+by index and must equal the unsharded batch; no data-path collective is
+involved.  On CPU the oracle stands in for the per-rank engine; the gpu test
+runs libsccsum in every rank (two rank processes on the box's one GPU, the
+same code path the driver's N-GPU run takes with cuda:rank)."""
 import os
 import socket
 
@@ -38,12 +40,26 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _engine_gpu(sbuf, soff, slen):
+    import torch
+    from seastar_amd import batch
+
+    b = batch.PacketBatch.from_host(sbuf, soff, slen, device="cuda:0")
+    status = torch.zeros(max(b.n, 1), dtype=torch.uint8, device=b.device)
+    out = batch.ipv4_frames(b, status=status)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint16), status[:b.n].cpu().numpy()
+
+
+def _worker(rank, world, port, q, engine="oracle", n=3000):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    buf, off, lens, _ = synth.mixed_udp_frames(3000, seed=5, max_gap=3)
+    buf, off, lens, _ = synth.mixed_udp_frames(n, seed=5, max_gap=3)
     sbuf, soff, slen, (lo, hi) = shard.shard(buf, off, lens, rank, world)
-    out, st = oracle.batch_ipv4(sbuf, soff, slen)
+    if engine == "gpu":
+        out, st = _engine_gpu(sbuf, soff, slen)
+    else:
+        out, st = oracle.batch_ipv4(sbuf, soff, slen)
     parts = [None] * world
     dist.all_gather_object(parts, (lo, hi, out, st))
     if rank == 0:
@@ -54,15 +70,24 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_shards_match_unsharded():
-    world = 2
+def _run(world, engine, n):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, engine, n)) for r in range(world)]
     for p in procs:
         p.start()
-    ok = q.get(timeout=120)
+    ok = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
     assert ok
+    assert all(p.exitcode == 0 for p in procs)
+
+
+def test_two_rank_gloo_shards_match_unsharded():
+    _run(2, "oracle", 3000)
+
+
+@pytest.mark.gpu
+def test_two_rank_gpu_engine_shards_match_oracle():
+    _run(2, "gpu", 20000)
