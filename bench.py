@@ -72,6 +72,9 @@ def parse():
                     help="udp1500 = the metric's config (cfg 2, default); mixed = cfg 3; tcp64k = cfg 4 "
                          "(per-GPU shard); e2e = cfg 5 (pinned host mbufs, PCIe-inclusive); fill = cfg 2 tx "
                          "generate with in-place write-back (sccsum_ipv4_fill); sweep = rate against batch size")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="udp1500 / mixed / fill: step k launches on stream k %% S (A/B: with 2, consecutive steps' "
+                         "launches run concurrently)")
     ap.add_argument("--launch", default="multi", choices=["multi", "single"],
                     help="udp1500: one sccsum_ipv4_frames_multi launch per step over the tx and rx batches (multi, "
                          "default) or one sccsum_ipv4_frames launch per batch (single)")
@@ -258,12 +261,30 @@ class Launches:
 LAUNCHES = Launches()
 
 
-def timed(step, steps, warmup, world, stream):
+def make_streams(args, dev):
+    """The step's launch streams: step k goes to streams[k % S].  Default 1 =
+    the current stream, one launch at a time, so a launch's duration is the
+    step's.  With 2 (A/B only), consecutive steps' launches run concurrently
+    over their whole length — +2-3 % on the read-only passes, -8 % on the
+    in-place fill (profiles/r02_ab_bench_streams.log) — and a kernel's trace
+    duration is no longer its share of the step."""
+    ns = args.streams
+    if ns <= 1:
+        return [torch.cuda.current_stream(dev)]
+    return [torch.cuda.Stream(device=dev) for _ in range(ns)]
+
+
+def timed(step, steps, warmup, world, streams):
     """Warm up, then time `steps` calls bracketed by barrier + sync; returns
     (max-over-ranks wall seconds, seconds per step from ONE pair of HIP events
-    around the timed launches on their stream).  An event between every two
-    launches leaves the GPU idle ~5 us at each (a timestamp packet), which
-    per-launch events would add to the wall time."""
+    around the timed launches: the start event on streams[0], which every other
+    stream waits on, the end event on streams[0] after it has waited on every
+    other stream).  An event between every two launches leaves the GPU idle
+    ~5 us at each (a timestamp packet), which per-launch events would add to
+    the wall time."""
+    streams = streams if isinstance(streams, (list, tuple)) else [streams]
+    s0 = streams[0]
+    torch.cuda.synchronize()  # inputs built on the default stream are complete before any step stream reads them
     for k in range(warmup):
         step(k)
     torch.cuda.synchronize()
@@ -271,10 +292,16 @@ def timed(step, steps, warmup, world, stream):
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    e0.record(stream)
+    e0.record(s0)
+    for s in streams[1:]:
+        s.wait_event(e0)
     for k in range(warmup, warmup + steps):
         step(k)
-    e1.record(stream)
+    for s in streams[1:]:
+        ev = torch.cuda.Event()
+        ev.record(s)
+        s0.wait_event(ev)
+    e1.record(s0)
     torch.cuda.synchronize()
     t1 = time.perf_counter()  # this rank's end, before the closing barrier's own latency
     barrier(world)
@@ -326,8 +353,14 @@ def run_udp1500(args, world, rank, dev):
     R = max(1, args.rotate)
     kern = flat_kernel(True, False, n, n * FRAME)
     txs, rxs, sts = [], [], []
-    out_tx = torch.empty(2 * n, dtype=torch.int16, device=dev)
-    out_rx = torch.empty(2 * n, dtype=torch.int16, device=dev)
+    streams = make_streams(args, dev)
+    if R % len(streams):  # a batch (and its status buffer) must always come back to the same stream
+        streams = streams[:1]
+    ns = len(streams)
+    # one result buffer per stream: steps on different streams may overlap
+    outs = [(torch.empty(2 * n, dtype=torch.int16, device=dev), torch.empty(2 * n, dtype=torch.int16, device=dev))
+            for _ in range(ns)]
+    out_tx = outs[0][0]
     g = torch.Generator(device=dev)
     g.manual_seed(SEED + rank)
     bad = torch.randperm(n, device=dev, generator=g)[: n // 100]
@@ -340,7 +373,6 @@ def run_udp1500(args, world, rank, dev):
         txs.append(tx)
         rxs.append(rx)
         sts.append(torch.empty(n, dtype=torch.uint8, device=dev))
-    stream = torch.cuda.current_stream()
     multi = args.launch == "multi"
     per_step = 1 if multi else 2  # launches per step
     if multi:  # the tx and rx batches of a step form ONE launch of 2 * n frames
@@ -348,13 +380,16 @@ def run_udp1500(args, world, rank, dev):
 
     def step(k):
         r = k % R
+        s = streams[k % ns]
+        o_tx, o_rx = outs[k % ns]
         if multi:
-            batch.ipv4_frames_multi([(txs[r], out_tx, None), (rxs[r], out_rx, sts[r])], stream=stream)
+            batch.ipv4_frames_multi([(txs[r], o_tx, None), (rxs[r], o_rx, sts[r])], stream=s)
         else:
-            batch.ipv4_frames(txs[r], out2=out_tx, stream=stream)
-            batch.ipv4_frames(rxs[r], out2=out_rx, status=sts[r], stream=stream)
+            batch.ipv4_frames(txs[r], out2=o_tx, stream=s)
+            batch.ipv4_frames(rxs[r], out2=o_rx, status=sts[r], stream=s)
 
     warm = max(args.warmup, R)
+    torch.cuda.synchronize()  # the batches were built on the default stream
     for k in range(warm):
         step(k)
     LAUNCHES.add(kern, per_step * warm)
@@ -364,9 +399,10 @@ def run_udp1500(args, world, rank, dev):
         n_fail = int(((st_rx & 2) == 0).sum())
         assert n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
     sel = LAUNCHES.select(kern, per_step * args.steps)
-    wall, step_s = timed(step, args.steps, 0, world, stream)
+    wall, step_s = timed(step, args.steps, 0, world, streams)
     LAUNCHES.add(kern, per_step * args.steps)
     avg_launch_s = step_s / per_step
+    stream = streams[0]
 
     value = world * 2 * n * FRAME * args.steps / wall / 2**30
     # per launch: every frame byte + 12 B metadata + 4 B of results (+ 1 B status per rx frame)
@@ -383,6 +419,7 @@ def run_udp1500(args, world, rank, dev):
               "launch": ("one sccsum_ipv4_frames_multi launch per step over the tx and rx batches" if multi
                          else "one sccsum_ipv4_frames launch per batch (2 per step)"),
               "rotation": f"{R} distinct tx/rx batch pairs launched in turn ({2 * R * n * FRAME / 1e9:.1f} GB per GPU)",
+              "streams": f"{ns} (step k on stream k % {ns})",
               "global_batch": n * world, "parallelism": f"{world} independent shards, no collective"},
              roofline(alg, avg_launch_s, "udp1500", kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi
                                                                    else " (sccsum_ipv4_frames)"), sel, args,
@@ -430,14 +467,16 @@ def run_mixed(args, world, rank, dev):
     lens = synth.zipf_lengths(n, seed=SEED + rank)
     R = max(1, args.rotate)  # distinct batches launched in turn (no cached-line replay)
     bs = [devsynth.mixed_frames(lens, seed=SEED + 31 * rank + 7 * r, device=dev) for r in range(R)]
-    out = torch.empty(2 * n, dtype=torch.int16, device=dev)
-    stream = torch.cuda.current_stream()
+    streams = make_streams(args, dev)
+    ns = len(streams)
+    outs = [torch.empty(2 * n, dtype=torch.int16, device=dev) for _ in range(ns)]
+    stream = streams[0]
     warm = max(args.warmup, R)
     kern = flat_kernel(True, False, n, bs[0].bytes_len)
     LAUNCHES.add(kern, warm)
     sel = LAUNCHES.select(kern, args.steps)
-    wall, launch_s = timed(lambda k: batch.ipv4_frames(bs[k % R], out2=out, stream=stream), args.steps, warm, world,
-                           stream)
+    wall, launch_s = timed(lambda k: batch.ipv4_frames(bs[k % R], out2=outs[k % ns], stream=streams[k % ns]),
+                           args.steps, warm, world, streams)
     total = int(lens.sum())
     alg = total + n * (META_BYTES + 4)
     ceiling = read_ceiling(bs[0].data, bs[0].bytes_len, stream)
@@ -446,7 +485,8 @@ def run_mixed(args, world, rank, dev):
              world * total * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": "cfg3: Zipf(s=1.2) IPv4/UDP frames 64..9000 B, packed back to back (odd offsets)",
               "packets_per_gpu": n, "bytes_per_gpu": total, "mean_len": round(total / n, 1),
-              "rotation": f"{R} distinct batches launched in turn", "parallelism": f"{world} independent shards"},
+              "rotation": f"{R} distinct batches launched in turn", "streams": f"{ns} (step k on stream k % {ns})",
+              "parallelism": f"{world} independent shards"},
              roofline(alg, launch_s, "mixed", kern + " (sccsum_ipv4_frames)", sel, args,
                       {"measured_read_ceiling_GBps": round(ceiling, 1)}))
 
@@ -468,18 +508,22 @@ def run_fill(args, world, rank, dev):
         assert args.no_check or int((st != 3).sum()) == 0, "filled frames do not verify"
     kern = flat_kernel(True, True, n, n * FRAME)
     LAUNCHES.add(kern, R)
-    stream = torch.cuda.current_stream()
+    streams = make_streams(args, dev)
+    if R % len(streams):  # a batch filled in place must always come back to the same stream
+        streams = streams[:1]
+    ns = len(streams)
     warm = max(args.warmup, R)
     LAUNCHES.add(kern, warm)
     sel = LAUNCHES.select(kern, args.steps)
-    wall, launch_s = timed(lambda k: batch.ipv4_fill(bs[k % R], mode, stream=stream), args.steps, warm, world, stream)
+    wall, launch_s = timed(lambda k: batch.ipv4_fill(bs[k % R], mode, stream=streams[k % ns]), args.steps, warm, world,
+                           streams)
     alg = n * (FRAME + META_BYTES + 4)  # read every byte + metadata, write the two 2-byte fields
     if rank == 0:
         emit("GiB/s device-resident Internet checksum, 1500B-packet batches, in-place generate (cfg 2 tx)",
              world * n * FRAME * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": "cfg2 tx: 1500 B IPv4/UDP frames, IP + UDP checksums generated and stored in place",
               "packets_per_gpu": n, "rotation": f"{R} distinct batches launched in turn",
-              "parallelism": f"{world} independent shards"},
+              "streams": f"{ns} (step k on stream k % {ns})", "parallelism": f"{world} independent shards"},
              roofline(alg, launch_s, "fill", kern + " + fill_store_kernel (sccsum_ipv4_fill: generate pass, "
                                                     "then the field-store pass)", sel, args,
                       {"trace_select_extra": [{"kernel": "fill_store_kernel", "skip": sel["skip"],
