@@ -72,6 +72,9 @@ def parse():
                     help="udp1500 = the metric's config (cfg 2, default); mixed = cfg 3; tcp64k = cfg 4 "
                          "(per-GPU shard); e2e = cfg 5 (pinned host mbufs, PCIe-inclusive); fill = cfg 2 tx "
                          "generate with in-place write-back (sccsum_ipv4_fill); sweep = rate against batch size")
+    ap.add_argument("--seg-len", type=int, default=65536, help="tcp64k: segment bytes (65536, or 65535: odd offsets)")
+    ap.add_argument("--align", type=int, default=1, help="mixed: frame start alignment (1 = packed, SURVEY §8(d) (i); "
+                                                         "64 = layout (ii))")
     ap.add_argument("--streams", type=int, default=1,
                     help="udp1500 / mixed / fill: step k launches on stream k %% S (A/B: with 2, consecutive steps' "
                          "launches run concurrently)")
@@ -430,7 +433,7 @@ def run_tcp64k(args, world, rank, dev):
     """cfg 4: 64 KiB TCP segments with pseudo-header seeds (len 65536 wraps to
     0, tcp.hh:878), this rank's independent shard of the 16 M-segment job."""
     n = args.packets if args.packets != (1 << 20) else 2 * 1024 * 1024  # 16 M / 8 GPUs per rank
-    seg = 65536
+    seg = args.seg_len  # 65536 (pseudo-header len wraps to 0), or the 65535 B variant of SURVEY §8(d)
     b, seeds = devsynth.tcp_segments(n, seg, seed=SEED + 104729 * rank, device=dev)
     out = torch.empty(n, dtype=torch.int16, device=dev)
     st = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -452,7 +455,7 @@ def run_tcp64k(args, world, rank, dev):
     if rank == 0:
         emit("GiB/s device-resident Internet checksum, 64 KiB TCP segments (cfg 4)",
              world * n * seg * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
-             {"workload": "cfg4: 65536 B TCP segments + pseudo-header seed per segment, verify pass",
+             {"workload": f"cfg4: {seg} B TCP segments + pseudo-header seed per segment, verify pass",
               "segments_per_gpu": n, "segment_bytes": seg, "parallelism": f"{world} independent shards"},
              roofline(alg, launch_s, "tcp64k", kern + " (sccsum_spans)", sel, args,
                       {"measured_read_ceiling_GBps": round(ceiling, 1), "read_ceiling_bytes": cbytes}))
@@ -466,7 +469,8 @@ def run_mixed(args, world, rank, dev):
     n = args.packets if args.packets != (1 << 20) else 3_400_000
     lens = synth.zipf_lengths(n, seed=SEED + rank)
     R = max(1, args.rotate)  # distinct batches launched in turn (no cached-line replay)
-    bs = [devsynth.mixed_frames(lens, seed=SEED + 31 * rank + 7 * r, device=dev) for r in range(R)]
+    align = max(1, args.align)
+    bs = [devsynth.mixed_frames(lens, seed=SEED + 31 * rank + 7 * r, device=dev, align=align) for r in range(R)]
     streams = make_streams(args, dev)
     ns = len(streams)
     outs = [torch.empty(2 * n, dtype=torch.int16, device=dev) for _ in range(ns)]
@@ -483,7 +487,8 @@ def run_mixed(args, world, rank, dev):
     if rank == 0:
         emit("GiB/s device-resident Internet checksum, mixed-MTU Zipf batches (cfg 3)",
              world * total * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
-             {"workload": "cfg3: Zipf(s=1.2) IPv4/UDP frames 64..9000 B, packed back to back (odd offsets)",
+             {"workload": ("cfg3: Zipf(s=1.2) IPv4/UDP frames 64..9000 B, packed back to back (odd offsets)" if align == 1
+                           else f"cfg3 (ii): Zipf(s=1.2) IPv4/UDP frames 64..9000 B, each at a {align} B boundary"),
               "packets_per_gpu": n, "bytes_per_gpu": total, "mean_len": round(total / n, 1),
               "rotation": f"{R} distinct batches launched in turn", "streams": f"{ns} (step k on stream k % {ns})",
               "parallelism": f"{world} independent shards"},

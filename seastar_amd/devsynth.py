@@ -111,15 +111,17 @@ def store_tcp_checksums(b: PacketBatch, out: torch.Tensor) -> None:
     f[:, 16:18] = out.contiguous().view(torch.uint8).view(b.n, 2)
 
 
-def mixed_frames(lengths, seed: int, device) -> PacketBatch:
-    """IPv4/UDP frames of the given lengths packed back to back (odd offsets
-    included), built in HBM: random payload, headers per ip.cc:249-269."""
+def mixed_frames(lengths, seed: int, device, align: int = 1) -> PacketBatch:
+    """IPv4/UDP frames of the given lengths packed back to back (align 1: odd
+    offsets included) or each starting on an `align`-byte boundary, built in
+    HBM: random payload (and gap bytes), headers per ip.cc:249-269."""
     import numpy as np
 
     lengths = np.asarray(lengths, dtype=np.int64)
     n = lengths.size
-    off = np.concatenate([[0], np.cumsum(lengths)[:-1]])
-    total = int(lengths.sum())
+    pitch = (lengths + align - 1) // align * align
+    off = np.concatenate([[0], np.cumsum(pitch)[:-1]])
+    total = int(off[-1] + lengths[-1]) if n else 0
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     data = torch.randint(0, 256, (_round16(total),), dtype=torch.uint8, device=device, generator=g)
