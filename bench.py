@@ -626,7 +626,9 @@ def run_e2e(args, world, rank, dev):
     data at +256); chunks H2D on a copy stream, kernel on a compute stream,
     results D2H, 3 chunks in flight.  A = slots copied as they lie; B =
     packets gathered into pinned staging first; C = one 2D DMA per chunk of
-    each slot's packet bytes (B and C: only packet bytes cross PCIe)."""
+    each slot's packet bytes; D = no copies: the fragment-list kernel reads
+    each packet in place over PCIe and writes results to pinned staging (B, C
+    and D: only packet bytes cross PCIe)."""
     from seastar_amd import pipeline
 
     n = args.packets
@@ -643,7 +645,8 @@ def run_e2e(args, world, rank, dev):
     res = {}
     for name, gather, chunk_bytes in (("A_slots_as_is", native.GATHER_NONE, 65536 * pipeline.MBUF_SLOT),
                                       ("B_gathered", native.GATHER_HOST, 65536 * FRAME),
-                                      ("C_strided_dma", native.GATHER_STRIDED, 65536 * ((FRAME + 15) & ~15))):
+                                      ("C_strided_dma", native.GATHER_STRIDED, 65536 * ((FRAME + 15) & ~15)),
+                                      ("D_zero_copy", native.GATHER_ZERO_COPY, 65536 * FRAME)):
         pl = pipeline.HostPipeline(dev.index or 0, chunk_bytes=chunk_bytes, chunk_packets=65536, depth=3)
         got = pl.run(native.PIPE_IPV4, pool, off, length, gather=gather, max_len=FRAME)
         assert np.array_equal(got, want), f"e2e {name} mismatch vs device-resident results"
@@ -662,7 +665,8 @@ def run_e2e(args, world, rank, dev):
         emit("GiB/s Internet checksum incl. PCIe: pinned mbuf-shaped host buffers -> HBM -> host (cfg 5)",
              world * best["GiBps_packet_bytes"], "GiB/s", args, world, best["ms_per_batch"] / 1e3 * args.steps, "u8",
              {"workload": "cfg5: 1,048,576 x 1500 B IPv4/UDP frames in 2304-B mbuf slots (pinned), "
-                          "H2D + kernel + D2H of 4 B/frame, 3-deep pipeline, 64Ki-frame chunks",
+                          "H2D + kernel + D2H of 4 B/frame (or the kernel reading the slots in place), 3-deep "
+                          "pipeline, 64Ki-frame chunks; value = the best variant",
               "parallelism": f"{world} independent shards"}, extra={"variants": res})
 
 

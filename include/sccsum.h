@@ -244,6 +244,7 @@ typedef struct sccsum_pipeline sccsum_pipeline;
 #define SCCSUM_GATHER_NONE    0 /* copy each chunk's covering byte range as it lies */
 #define SCCSUM_GATHER_HOST    1 /* pack packets into pinned staging on the host first */
 #define SCCSUM_GATHER_STRIDED 2 /* packets at one pitch (mbuf slots): one 2D DMA of each slot's packet bytes */
+#define SCCSUM_GATHER_ZERO_COPY 3 /* no copies: the kernel reads each packet in place (host_bytes pinned / registered) */
 
 /* Allocate device buffers and pinned staging for `depth` chunks on `device`. */
 int sccsum_pipeline_create(int device, uint64_t chunk_bytes, uint32_t chunk_packets, int depth,
@@ -258,7 +259,11 @@ int sccsum_pipeline_create(int device, uint64_t chunk_bytes, uint32_t chunk_pack
  * slots of an mbuf pool, dpdk.cc:139-156) and none is longer than P, one 2D
  * DMA (hipMemcpy2DAsync) copies the first W bytes of each slot, W = the
  * chunk's longest packet — only packet bytes cross PCIe, with no host copy;
- * other chunks are copied as they lie.  mode = SCCSUM_PIPE_SPANS (host_seed optional, host_out[n]) or
+ * other chunks are copied as they lie; gather = 3: nothing is copied — one
+ * fragment-list launch per chunk reads every packet in place over PCIe
+ * (packet bytes only) and writes its results to pinned staging; host_bytes
+ * must be pinned or registered (SCCSUM_EINVAL otherwise, checked with
+ * hipPointerGetAttributes on both ends).  mode = SCCSUM_PIPE_SPANS (host_seed optional, host_out[n]) or
  * SCCSUM_PIPE_IPV4 (host_out[2n]); host_status optional.  Returns when all
  * results are in host_out.  host_len is the size of the host_bytes area. */
 int sccsum_pipeline_run(sccsum_pipeline* p, int mode, int gather, const void* host_bytes, uint64_t host_len,

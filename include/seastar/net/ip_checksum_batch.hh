@@ -13,7 +13,8 @@
 //   ip.cc:121-127 (IPv4 verify) + tcp.hh:876-883 (TCP verify) ipv4_frames(batch, ...)
 //   ip.cc:271-277 (IPv4 generate) + udp/tcp generate          ipv4_frames(batch, ...) on zeroed fields
 //   the same, stored into the frames (wire-ready tx)          ipv4_fill(batch, SCCSUM_FILL_IP | SCCSUM_FILL_L4, ...)
-//   checksummer::sum(const packet&)  ip_checksum.cc:64-68     (C-ABI sccsum_fragments)
+//   checksummer::sum(const packet&)  ip_checksum.cc:64-68     spans_desc / ipv4_frames_desc (fragments
+//                                                             anywhere the device reads); C-ABI sccsum_fragments
 //   toeplitz_hash(rss_key(), forward_hash)  net.cc:330-341    ipv4_rss(batch, key, ...) / ipv4_frames_rss(...)
 //   per packet as qp::poll_tx / DPDK rx hand them over         burst_queue (host packets, async completion)
 //       net.cc:81-105, dpdk.cc:2190-2204
@@ -127,6 +128,25 @@ public:
         ipv4_rss(b, key.data(), key.size(), mode, d_hash, d_status, stream);
     }
 #endif
+
+    // Packets as fragment lists summed where the fragments lie (HBM, pinned /
+    // registered host memory over PCIe, or d_stage for src == nullptr):
+    // checksummer::sum(const packet&) (ip_checksum.cc:64-68) without a gather.
+    // Packet i is d_desc[d_first[i] .. d_first[i+1]), tiling its bytes from
+    // dst_off = d_off[i]; d_len / max_len as in device_packet_batch.
+    void spans_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const uint64_t* d_off,
+                    const uint32_t* d_len, uint64_t n, uint32_t max_len, const void* d_stage, const uint32_t* d_seeds,
+                    uint16_t* d_out, uint8_t* d_status, void* stream) const {
+        check(sccsum_spans_desc(d_desc, d_first, d_off, d_len, d_seeds, d_stage, d_out, d_status, n, max_len, stream),
+              "sccsum_spans_desc");
+    }
+
+    void ipv4_frames_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const uint64_t* d_off,
+                          const uint32_t* d_len, uint64_t n, uint32_t max_len, const void* d_stage, uint16_t* d_out2,
+                          uint8_t* d_status, void* stream) const {
+        check(sccsum_ipv4_frames_desc(d_desc, d_first, d_off, d_len, d_stage, d_out2, d_status, n, max_len, stream),
+              "sccsum_ipv4_frames_desc");
+    }
 
     void sync(void* stream) const { check(sccsum_sync(stream), "sccsum_sync"); }
 };

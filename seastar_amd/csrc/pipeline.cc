@@ -10,6 +10,10 @@
 //                   DMA of each slot's packet bytes) + offsets/lengths/seeds
 //   compute stream: wait(copied[c]) -> sccsum kernel -> D2H results -> record(done[c])
 // so the H2D of chunk c+1 overlaps the kernel of chunk c and the D2H of c-1.
+// Zero copy (gather 3): no copies at all — one fragment-list launch per chunk
+// reads each packet where it lies in the pinned pool (over PCIe, packet bytes
+// only) and the chunk's metadata from pinned staging, and writes the results
+// into pinned staging (sccsum_*_desc).
 // Results land in pinned staging and are copied to the caller's arrays when
 // the stage is recycled or at the end.
 #include <hip/hip_runtime.h>
@@ -36,6 +40,8 @@ struct sccsum_pipeline {
         uint32_t* h_seed = nullptr;
         uint16_t* h_out = nullptr;   // pinned results
         uint8_t* h_status = nullptr;
+        sccsum_gather_desc* h_desc = nullptr;  // zero copy: one descriptor per packet
+        uint32_t* h_first = nullptr;
         hipEvent_t copied = nullptr, done = nullptr;
         // pending result copy-out (caller arrays)
         uint16_t* dst_out = nullptr;
@@ -83,6 +89,8 @@ void free_stage(sccsum_pipeline::Stage& s) {
     (void)hipHostFree(s.h_seed);
     (void)hipHostFree(s.h_out);
     (void)hipHostFree(s.h_status);
+    (void)hipHostFree(s.h_desc);
+    (void)hipHostFree(s.h_first);
     if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.done) (void)hipEventDestroy(s.done);
 }
@@ -120,6 +128,8 @@ int sccsum_pipeline_create(int device, uint64_t chunk_bytes, uint32_t chunk_pack
         if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_seed, np * 4, hipHostMallocDefault));
         if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_out, np * 4, hipHostMallocDefault));
         if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_status, np, hipHostMallocDefault));
+        if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_desc, np * sizeof(sccsum_gather_desc), hipHostMallocDefault));
+        if (rc == SCCSUM_OK) rc = hip_rc(hipHostMalloc(&s.h_first, (np + 1) * 4, hipHostMallocDefault));
         if (rc == SCCSUM_OK) rc = hip_rc(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
         if (rc == SCCSUM_OK) rc = hip_rc(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
     }
@@ -147,14 +157,35 @@ int sccsum_pipeline_destroy(sccsum_pipeline* p) {
 
 namespace {
 
+// The device may read [p, p + len) in place: both ends lie in pinned or
+// registered host memory (or device memory).  Pageable memory would fault the
+// GPU, so a zero-copy run refuses it up front.
+bool device_readable(const void* p, uint64_t len) {
+    if (len == 0) return true;
+    const auto* b = static_cast<const uint8_t*>(p);
+    for (const uint8_t* q : {b, b + len - 1}) {
+        hipPointerAttribute_t a{};
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();  // clear the sticky "not registered" error
+            return false;
+        }
+        if (a.type != hipMemoryTypeHost && a.type != hipMemoryTypeDevice && a.type != hipMemoryTypeManaged) {
+            return false;
+        }
+    }
+    return true;
+}
+
 int run_chunks(sccsum_pipeline* p, int mode, int gather, const void* host_bytes, uint64_t host_len,
                const uint64_t* host_off, const uint32_t* host_lens, const uint32_t* host_seed, uint64_t n,
                uint32_t max_len, uint16_t* host_out, uint8_t* host_status) {
     if (!p || (mode != SCCSUM_PIPE_SPANS && mode != SCCSUM_PIPE_IPV4) || !host_off || !host_lens || !host_out ||
-        (n && !host_bytes) || gather < 0 || gather > SCCSUM_GATHER_STRIDED) {
+        (n && !host_bytes) || gather < 0 || gather > SCCSUM_GATHER_ZERO_COPY) {
         return SCCSUM_EINVAL;
     }
     SCCSUM_TRY(hipSetDevice(p->device));
+    const bool zc = gather == SCCSUM_GATHER_ZERO_COPY;
+    if (zc && n && !device_readable(host_bytes, host_len)) return SCCSUM_EINVAL;
     const auto* src = static_cast<const uint8_t*>(host_bytes);
     const int width = mode == SCCSUM_PIPE_IPV4 ? 2 : 1;
     uint64_t i = 0;
@@ -187,8 +218,10 @@ int run_chunks(sccsum_pipeline* p, int mode, int gather, const void* host_bytes,
                 if (j == i && L > P) rows = false;  // not slot-shaped after all: copy as it lies
                 W = nW;
             }
-            if (gather == 1) {
-                if (j > i && packed + L > p->chunk_bytes) break;
+            if (gather == 1 || zc) {
+                // zero copy: descriptor positions are 32-bit
+                const uint64_t cap = zc ? std::min<uint64_t>(p->chunk_bytes, UINT32_MAX) : p->chunk_bytes;
+                if (j > i && packed + L > cap) break;
                 packed += L;
             } else if (!rows) {
                 const uint64_t nlo = std::min(lo, o), nhi = std::max(hi, o + L);
@@ -208,8 +241,41 @@ int run_chunks(sccsum_pipeline* p, int mode, int gather, const void* host_bytes,
             }
         }
         const uint64_t Wd = (W + 15) & ~uint64_t(15);
-        if (gather == 1 ? packed > p->chunk_bytes : (rows ? npk * Wd > p->chunk_bytes : hi - lo > p->chunk_bytes)) {
+        if ((gather == 1 || zc) ? packed > p->chunk_bytes
+                                : (rows ? npk * Wd > p->chunk_bytes : hi - lo > p->chunk_bytes)) {
             return SCCSUM_EINVAL;  // one oversized packet
+        }
+        if (zc) {
+            // one descriptor per (non-empty) packet, read in place; the layout
+            // offsets are the packets' positions packed back to back
+            uint64_t pos = 0;
+            uint32_t nd = 0;
+            for (uint64_t k = 0; k < npk; ++k) {
+                const uint32_t L = host_lens[i + k];
+                s.h_first[k] = nd;
+                s.h_off[k] = pos;
+                if (L) s.h_desc[nd++] = {src + host_off[i + k], static_cast<uint32_t>(pos), L};
+                pos += L;
+            }
+            s.h_first[npk] = nd;
+            std::memcpy(s.h_len, host_lens + i, npk * 4);
+            if (host_seed) std::memcpy(s.h_seed, host_seed + i, npk * 4);
+            const int rk = mode == SCCSUM_PIPE_IPV4
+                               ? sccsum_ipv4_frames_desc(s.h_desc, s.h_first, s.h_off, s.h_len, nullptr, s.h_out,
+                                                         host_status ? s.h_status : nullptr, npk, max_len, p->compute)
+                               : sccsum_spans_desc(s.h_desc, s.h_first, s.h_off, s.h_len,
+                                                   host_seed ? s.h_seed : nullptr, nullptr, s.h_out,
+                                                   host_status ? s.h_status : nullptr, npk, max_len, p->compute);
+            if (rk != SCCSUM_OK) return rk;
+            SCCSUM_TRY(hipEventRecord(s.done, p->compute));
+            s.dst_out = host_out + i * width;
+            s.dst_status = host_status ? host_status + i : nullptr;
+            s.npk = npk;
+            s.width = width;
+            s.busy = true;
+            i = j;
+            ++chunk;
+            continue;
         }
         uint64_t nbytes;
         if (gather == 1) {

@@ -96,6 +96,7 @@ PIPE_IPV4 = 1
 GATHER_NONE = 0
 GATHER_HOST = 1
 GATHER_STRIDED = 2
+GATHER_ZERO_COPY = 3
 RSS_DISPATCH = 0
 RSS_REASSEMBLED = 1
 

@@ -106,7 +106,11 @@ class HostPipeline:
     def run(self, mode: int, buf: np.ndarray, off: np.ndarray, length: np.ndarray, seeds: np.ndarray | None = None,
             status: bool = False, gather: int = 0, max_len: int = 0):
         """gather: 0 = copy chunks as they lie, 1 = pack on the host first,
-        2 = one 2D DMA of each slot's packet bytes (native.GATHER_*)."""
+        2 = one 2D DMA of each slot's packet bytes, 3 = no copies: the kernel
+        reads the packets in place (buf must be pinned: pinned_empty)
+        (native.GATHER_*)."""
+        if gather == native.GATHER_ZERO_COPY and buf.size and not is_pinned(buf):
+            raise ValueError("zero-copy pipeline runs need a pinned buffer (pinned_empty)")
         off = np.ascontiguousarray(off, dtype=np.uint64)
         length = np.ascontiguousarray(length, dtype=np.uint32)
         n = off.size

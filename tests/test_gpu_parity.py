@@ -261,7 +261,7 @@ def test_zipf_large_frames(dev):
     assert np.array_equal(got, want) and np.array_equal(st, want_st)
 
 
-@pytest.mark.parametrize("gather", [0, 1, 2], ids=["as_is", "host_gather", "strided_dma"])
+@pytest.mark.parametrize("gather", [0, 1, 2, 3], ids=["as_is", "host_gather", "strided_dma", "zero_copy"])
 def test_host_pipeline_mbuf_pool(dev, gather, kernel_variant):
     """cfg 5 path: frames in an mbuf-shaped pinned pool, chunked through the
     GPU with async copies; small chunks force many stage recycles."""
@@ -281,6 +281,33 @@ def test_host_pipeline_mbuf_pool(dev, gather, kernel_variant):
     got2 = pl.run(native.PIPE_SPANS, pool, poff, plen, seeds=seeds, gather=gather)
     assert np.array_equal(got2, oracle.batch_spans(pool, poff, plen, seeds))
     pl.close()
+
+
+def test_host_pipeline_zero_copy_refuses_pageable_memory(dev):
+    """gather = 3 reads the caller's buffer in place: pageable memory is
+    refused (ValueError in Python, SCCSUM_EINVAL from the C-ABI) instead of
+    faulting the GPU."""
+    import ctypes
+
+    from seastar_amd import pipeline
+
+    buf, off, lens, _ = synth.mixed_udp_frames(50, seed=41)
+    pl = pipeline.HostPipeline(0, chunk_bytes=1 << 20, chunk_packets=64, depth=2)
+    with pytest.raises(ValueError):
+        pl.run(native.PIPE_IPV4, buf, off, lens, gather=native.GATHER_ZERO_COPY)
+    off64 = np.ascontiguousarray(off, np.uint64)
+    l32 = np.ascontiguousarray(lens, np.uint32)
+    out = np.empty(2 * lens.size, np.uint16)
+    rc = native.load().sccsum_pipeline_run(pl._h, native.PIPE_IPV4, native.GATHER_ZERO_COPY, buf.ctypes.data, buf.size,
+                                           off64.ctypes.data, l32.ctypes.data, None, lens.size, 1500,
+                                           out.ctypes.data, None)
+    assert rc == native.SCCSUM_EINVAL
+    pinned = pipeline.pinned_empty(buf.size)
+    pinned[:] = buf
+    got = pl.run(native.PIPE_IPV4, pinned, off, lens, gather=native.GATHER_ZERO_COPY, max_len=1500)
+    assert np.array_equal(got, oracle.batch_ipv4(buf, off, lens)[0])
+    pl.close()
+    assert ctypes.sizeof(ctypes.c_void_p) == 8
 
 
 def test_host_pipeline_strided_irregular(dev):
