@@ -986,9 +986,20 @@ __global__ __launch_bounds__(kBlock) void fill_store_kernel(uint8_t* __restrict_
     if (o > bytes_len || L > bytes_len - o || L < 20u) return;
     uint8_t* p = bytes + o;
     const uint32_t w = words[i];
-    const uint32_t ihl = p[0] & 0xfu;
-    const uint32_t ip_len = (static_cast<uint32_t>(p[2]) << 8) | p[3];
-    const uint32_t proto = p[9];
+    // header bytes 0..9 from the four dwords at the dword-aligned address at or
+    // below p (one 16-byte request instead of four byte loads)
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t sh = static_cast<uint32_t>(a & 3u);
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(a - sh);
+    const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
+    auto hbyte = [&](uint32_t k) {
+        const uint32_t b = sh + k;
+        const uint32_t dw = b < 4u ? d0 : (b < 8u ? d1 : (b < 12u ? d2 : d3));
+        return (dw >> (8u * (b & 3u))) & 0xffu;
+    };
+    const uint32_t ihl = hbyte(0) & 0xfu;
+    const uint32_t ip_len = (hbyte(2) << 8) | hbyte(3);
+    const uint32_t proto = hbyte(9);
     const uint32_t l4_off = 4u * ihl;
     const uint32_t l4_end = ip_len < L ? ip_len : L;
     const bool malformed = L < ip_len || l4_off > l4_end;

@@ -12,7 +12,9 @@
 //   rd+st16   ... and rewrites the 16-B units holding them from the loaded bytes
 //   rd+st64   ... rewrites the aligned 64-B line holding frame+10 (bytes as read)
 //   rd+st2d   as rd+st2, but the tile's first line of each frame is loaded default-policy
-// usage: store_probe [reps]
+//   rd+side   the read pass stashes each frame's head line in a dense side array
+//   side2line a second pass writes the stashed lines back whole (no partial-line RMW)
+// usage: store_probe [reps] [set: 1 = the side-buffer set only]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -257,6 +259,54 @@ __global__ __launch_bounds__(256) void k_rdrev(uint8_t* buf, uint64_t n, uint64_
     if (acc == 0x12345u) sink[0] = acc;
 }
 
+// Side-buffer variants: the read pass stashes each frame's head line (the
+// aligned 64 B holding frame+10) in a dense side array — coalesced full-line
+// writes, 4 KB per wave per tile — and a second pass writes those lines back
+// whole (full-line writes, no partial-line read-modify-write in HBM).
+// RELOAD: the stash is the line's real content (4 loads after the tile);
+// otherwise a register value (pure write cost).
+template <bool RELOAD>
+__global__ __launch_bounds__(256) void k_rdside(uint8_t* buf, uint64_t n, u32x4* side, uint64_t* sink) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t(blockIdx.x) * 256 + threadIdx.x) >> 6;
+    const uint64_t nw = uint64_t(gridDim.x) * 4;
+    const uint64_t tiles = n / 64;
+    uint32_t acc = 0;
+    for (uint64_t t = wave; t < tiles; t += nw) {
+        const u32x4* base = reinterpret_cast<const u32x4*>(buf + t * 64 * kFrame);
+        constexpr uint32_t units = 64 * kFrame / 16;
+        for (uint32_t u = lane; u < units; u += 64 * 8) {
+            u32x4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t uu = u + 64 * k;
+                v[k] = uu < units ? __builtin_nontemporal_load(base + uu) : u32x4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
+        }
+        const uint64_t f = reinterpret_cast<uint64_t>(buf) + (t * 64 + lane) * kFrame;
+        const u32x4* L = reinterpret_cast<const u32x4*>((f + 10) & ~63ull);
+        u32x4* out = side + (t * 64 + lane) * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            u32x4 x = RELOAD ? L[k] : u32x4{acc, acc, acc, acc};
+            x.x ^= acc | 1u;
+            __builtin_nontemporal_store(x, out + k);
+        }
+    }
+    if (acc == 0x12345u) sink[0] = acc;
+}
+
+// Second pass: 4 lanes per frame copy its stashed 64 B back over the head line.
+__global__ __launch_bounds__(256) void k_side2line(uint8_t* buf, uint64_t n, const u32x4* side) {
+    const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    const uint64_t i = t / 4;
+    if (i >= n) return;
+    u32x4* L = reinterpret_cast<u32x4*>((reinterpret_cast<uint64_t>(buf) + i * kFrame + 10) & ~63ull);
+    L[t % 4] = __builtin_nontemporal_load(side + i * 4 + t % 4);
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? std::atoi(argv[1]) : 3;
     constexpr int R = 4;
@@ -291,6 +341,25 @@ int main(int argc, char** argv) {
         std::printf("%-10s %9.1f us/launch  %7.0f GB/s of frame bytes\n", name, us, kBytes / us / 1e3);
         std::fflush(stdout);
     };
+    u32x4* side;
+    CK(hipMalloc(&side, kFrames * 64));
+    if (argc > 2 && std::atoi(argv[2]) == 1) {  // side-buffer set only
+        run("rd only", [&](uint8_t* b) { k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+        run("rd;st2", [&](uint8_t* b) {
+            k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st2<<<g_frames, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rd+sideR", [&](uint8_t* b) { k_rdside<false><<<cus * 4, 256>>>(b, kFrames, side, sink); });
+        run("rd+side", [&](uint8_t* b) { k_rdside<true><<<cus * 4, 256>>>(b, kFrames, side, sink); });
+        run("side2line", [&](uint8_t* b) { k_side2line<<<g_frames * 4, 256>>>(b, kFrames, side); });
+        run("rd+side;2line", [&](uint8_t* b) {
+            k_rdside<true><<<cus * 4, 256>>>(b, kFrames, side, sink);
+            k_side2line<<<g_frames * 4, 256>>>(b, kFrames, side);
+        });
+        run("st64", [&](uint8_t* b) { k_stline<64><<<g_frames * 4, 256>>>(b, kFrames, 0x1234); });
+        run("st2", [&](uint8_t* b) { k_st2<<<g_frames, 256>>>(b, kFrames, 0x1234); });
+        return 0;
+    }
     run("read", [&](uint8_t* b) { k_read<<<cus * 8, 256>>>(reinterpret_cast<const u32x4*>(b), kBytes / 16, sink); });
     run("st2", [&](uint8_t* b) { k_st2<<<g_frames, 256>>>(b, kFrames, 0x1234); });
     run("st16", [&](uint8_t* b) { k_st16<<<g_frames, 256>>>(b, kFrames, 0x1234); });
