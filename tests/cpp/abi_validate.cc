@@ -43,6 +43,18 @@ int main() {
     EXPECT(sccsum_fragments_workspace(1000) >= 3000);
     EXPECT(sccsum_gather(static_cast<const sccsum_gather_desc*>(odd), 1, d16, nullptr) == SCCSUM_EINVAL);
     EXPECT(sccsum_read_probe(nullptr, 16, nullptr, nullptr) == SCCSUM_EINVAL);
+    // fragment lists: nothing to do, then null / misaligned arrays
+    EXPECT(sccsum_ipv4_frames_desc(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr) ==
+           SCCSUM_OK);
+    EXPECT(sccsum_ipv4_frames_desc(nullptr, static_cast<const uint32_t*>(d16), static_cast<const uint64_t*>(d16),
+                                   static_cast<const uint32_t*>(d16), nullptr, static_cast<uint16_t*>(d16), nullptr, 2,
+                                   64, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_spans_desc(static_cast<const sccsum_gather_desc*>(odd), static_cast<const uint32_t*>(d16),
+                             static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr, nullptr,
+                             static_cast<uint16_t*>(d16), nullptr, 2, 64, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_spans_desc(static_cast<const sccsum_gather_desc*>(d16), static_cast<const uint32_t*>(d16),
+                             static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr, nullptr,
+                             nullptr, nullptr, 2, 64, nullptr) == SCCSUM_EINVAL);
     // fill modes
     EXPECT(sccsum_ipv4_fill(nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, nullptr) == SCCSUM_EINVAL);
     EXPECT(sccsum_ipv4_fill(nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, 0,
@@ -93,6 +105,10 @@ int main() {
     EXPECT(sccsum_set_tile_packets(65) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_tile_bytes(-1) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_dynamic_tiles(2) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_burst_fused(3) == SCCSUM_EINVAL && sccsum_set_burst_fused(-1) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_burst_fused(2) == SCCSUM_OK);
+    EXPECT(sccsum_pipeline_run(nullptr, SCCSUM_PIPE_IPV4, SCCSUM_GATHER_ZERO_COPY, nullptr, 0, nullptr, nullptr,
+                               nullptr, 0, 0, nullptr, nullptr) == SCCSUM_EINVAL);
     // host arithmetic and strings
     EXPECT(sccsum_pseudo_seed(1, 2, 17, 8) == 28u);
     EXPECT(sccsum_pseudo_seed(0xffffffffu, 0xffffffffu, 255, 0xffff) <= 0xffffu);
