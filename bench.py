@@ -72,6 +72,7 @@ def parse():
                     help="udp1500 = the metric's config (cfg 2, default); mixed = cfg 3; tcp64k = cfg 4 "
                          "(per-GPU shard); e2e = cfg 5 (pinned host mbufs, PCIe-inclusive); fill = cfg 2 tx "
                          "generate with in-place write-back (sccsum_ipv4_fill); sweep = rate against batch size")
+    ap.add_argument("--tile-bytes", type=int, default=None, help="A/B: flat-kernel tile target (sccsum_diag.h)")
     ap.add_argument("--seg-len", type=int, default=65536, help="tcp64k: segment bytes (65536, or 65535: odd offsets)")
     ap.add_argument("--align", type=int, default=1, help="mixed: frame start alignment (1 = packed, SURVEY §8(d) (i); "
                                                          "64 = layout (ii))")
@@ -695,6 +696,8 @@ def main():
         run_dry(args, world, rank)
     else:
         dev = torch.device("cuda", local)
+        if args.tile_bytes is not None:  # A/B only (sccsum_diag.h)
+            native.check(native.load().sccsum_set_tile_bytes(args.tile_bytes), "sccsum_set_tile_bytes")
         {"udp1500": run_udp1500, "tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e, "fill": run_fill,
          "sweep": run_sweep}[args.config](args, world, rank, dev)
     if world > 1:

@@ -41,7 +41,7 @@ int sccsum_set_group_units(int units);
 /* Flat kernel: cap a tile (packets a wave plans at once) at 1..64 (default 64). */
 int sccsum_set_tile_packets(int packets);
 
-/* Flat kernel: target bytes per tile (default 0 = only the packet cap). */
+/* Flat kernel: target bytes per tile (default 49152; 0 = only the 64-packet cap). */
 int sccsum_set_tile_bytes(int bytes);
 
 /* Flat kernel: tiles dequeued from per-stream counters (1, the default) or

@@ -1103,6 +1103,15 @@ int cu_count() {
     return c;
 }
 
+// Default tile target: about 48 KiB of packets per tile (32 x 1500 B frames,
+// one 64 KiB segment; short packets stay at the 64-packet cap).  Measured
+// against the plain 64-packet cap on every bench config (profiles/
+// r02_ab_bench_tiles.log: cfg 2 +1.3-1.9 %, fill +1.7 %, cfg 4 +2.6 %, cfg 3
+// unchanged): a launch's drain shrinks with the tile.  The packet count is
+// what matters, and 32 is a sweet spot for 1500 B frames — 24-30 and 34-43
+// packets per tile run slower than 64 (profiles/r02_ab_tiles2.log).
+constexpr int kTileBytes = 49152;
+
 // Diagnostic knobs (include/sccsum_diag.h): per host thread, so one shard's
 // A/B settings never leak into another thread's launches.
 struct Knobs {
@@ -1111,7 +1120,7 @@ struct Knobs {
     int group_units = 0;             // simple kernel: U override (0 = by max_len)
     int tile_packets = kWave;        // flat kernel: max packets per tile
     int dynamic = 1;                 // flat kernel: dequeue tiles (1) or static round robin (0)
-    int tile_bytes = 0;              // flat kernel: target bytes per tile (0 = packets cap only)
+    int tile_bytes = kTileBytes;     // flat kernel: target bytes per tile (0 = packets cap only)
 };
 thread_local Knobs t_knobs;
 

@@ -741,3 +741,35 @@ def test_multi_batch_launch(dev, kernel_variant):
     torch.cuda.synchronize()
     for o, w in zip(souts, swant):
         assert np.array_equal(batch.as_u16(o), w)
+
+
+@pytest.mark.parametrize("tile_bytes,tile_packets", [(0, 64), (0, 1), (0, 7), (1500, 64), (49152, 64), (49152, 13),
+                                                     (1 << 20, 64)])
+def test_tile_shapes_match_oracle(dev, kernel_variant, tile_bytes, tile_packets):
+    """The flat kernel's tile sizing (bytes target, packet cap) changes only
+    the schedule: 1500 B frames, Zipf frames and 64 KiB spans match the
+    oracle under every shape (the default is 49152 B / 64)."""
+    if kernel_variant not in (15, 16):
+        pytest.skip("tile shapes exercised on the default flat forms")
+    lib = native.load()
+    native.check(lib.sccsum_set_tile_bytes(tile_bytes), "tile_bytes")
+    native.check(lib.sccsum_set_tile_packets(tile_packets), "tile_packets")
+    try:
+        buf, off, lens, _ = synth.udp_ipv4_frames(3000, 1500, seed=91)
+        got, st = _frames(dev, buf, off, lens)
+        want, want_st = oracle.batch_ipv4(buf, off, lens)
+        assert np.array_equal(got, want) and np.array_equal(st, want_st)
+        buf, off, lens, _ = synth.mixed_udp_frames(4000, seed=92, max_gap=3)
+        got, st = _frames(dev, buf, off, lens)
+        want, want_st = oracle.batch_ipv4(buf, off, lens)
+        assert np.array_equal(got, want) and np.array_equal(st, want_st)
+        rng = np.random.default_rng(93)
+        lens = np.full(24, 65536, np.uint32)
+        lens[::5] = 65535
+        off, total = synth.pack(lens, seed=94, max_gap=2)
+        buf = rng.integers(0, 256, size=int(total), dtype=np.uint8)
+        seeds = rng.integers(0, 65536, lens.size).astype(np.uint32)
+        assert np.array_equal(_spans(dev, buf, off, lens, seeds), oracle.batch_spans(buf, off, lens, seeds))
+    finally:
+        native.check(lib.sccsum_set_tile_bytes(49152), "tile_bytes")
+        native.check(lib.sccsum_set_tile_packets(64), "tile_packets")

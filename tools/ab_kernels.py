@@ -88,7 +88,7 @@ def main():
             native.check(lib.sccsum_set_group_units(int(parts[2] or 0)), "group_units")
             native.check(lib.sccsum_set_tile_packets(int(parts[3] or 64)), "tile_packets")
             native.check(lib.sccsum_set_dynamic_tiles(int(parts[4] or 1)), "dynamic")
-            native.check(lib.sccsum_set_tile_bytes(int(parts[5] or 0)), "tile_bytes")
+            native.check(lib.sccsum_set_tile_bytes(int(parts[5] or 49152)), "tile_bytes")
 
         def run(bb):
             if mode == "frames":
@@ -133,6 +133,7 @@ def main():
     native.check(lib.sccsum_set_group_units(0), "group_units")
     native.check(lib.sccsum_set_tile_packets(64), "tile_packets")
     native.check(lib.sccsum_set_dynamic_tiles(1), "dynamic")
+    native.check(lib.sccsum_set_tile_bytes(49152), "tile_bytes")
 
 
 if __name__ == "__main__":
