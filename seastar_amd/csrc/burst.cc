@@ -127,8 +127,10 @@ uint64_t stage_bytes(const sccsum_burst* b) {
 // results D2H; 0 = metadata H2D, gather into the batch, sum, results D2H.
 thread_local int t_fused = 2;
 
-// One H2D (packets + metadata packed behind them), the kernel, one D2H
-// (results + status), an event: 4 stream operations per batch.  On failure
+// A batch of copied packets: one H2D (packets + metadata packed behind them),
+// the kernel, one D2H (results + status), an event — 4 stream operations.  A
+// batch holding zero-copy packets: the fragment-list launch and an event (see
+// one_launch), or, in the A/B forms, the same 4 operations.  On failure
 // the slot is left exactly as before the call (still open, its packets
 // staged) once whatever part of the batch reached the stream has finished,
 // so a later poll / drain retries the launch.
