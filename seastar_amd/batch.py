@@ -130,6 +130,46 @@ def ipv4_frames_multi(items, stream=None) -> list:
     return [o[: 2 * it[0].n].view(it[0].n, 2) for o, it in zip(outs, items)]
 
 
+def prepare_ipv4_frames_multi(items):
+    """A prebuilt sccsum_ipv4_frames_multi launch over fixed batches and
+    outputs: returns launch(stream) that only crosses the C-ABI (no argument
+    marshalling per call), for callers that relaunch the same batch set."""
+    lib = native.load()
+    if not items or len(items) > native.MAX_BATCHES:
+        raise ValueError(f"1..{native.MAX_BATCHES} batches per launch")
+    arr = (native.Batch * len(items))()
+    for i, (b, out, status) in enumerate(items):
+        assert out is not None and out.numel() >= 2 * b.n
+        arr[i] = native.Batch(ctypes_ptr(b.data), b.bytes_len, ctypes_ptr(b.off), ctypes_ptr(b.length), None,
+                              ctypes_ptr(out), _ptr(status), b.n)
+    ml = max(it[0].max_len for it in items)
+    fn, ptr, nb = lib.sccsum_ipv4_frames_multi, ctypes.cast(arr, ctypes.c_void_p), len(items)
+
+    def launch(stream):
+        code = fn(ptr, nb, ml, stream.cuda_stream)
+        if code:
+            native.check(code, "sccsum_ipv4_frames_multi")
+
+    launch.keep = (arr, items)  # the descriptors and tensors outlive the closure's callers
+    return launch
+
+
+def prepare_call(name: str, *args):
+    """A prebuilt C-ABI call: tensors become device addresses once; the
+    returned launch(stream) appends the stream handle and calls `name`."""
+    lib = native.load()
+    fn = getattr(lib, name)
+    conv = tuple(ctypes_ptr(a) if isinstance(a, torch.Tensor) else a for a in args)
+
+    def launch(stream):
+        code = fn(*conv, stream.cuda_stream)
+        if code:
+            native.check(code, name)
+
+    launch.keep = args
+    return launch
+
+
 def spans_multi(items, stream=None) -> list:
     """sccsum_spans_multi: items = [(PacketBatch, out | None, status | None[, seeds int32]), ...]."""
     ml = max((it[0].max_len for it in items), default=0)
