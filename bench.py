@@ -53,7 +53,7 @@ def flat_kernel(ipv4: bool, fill: bool, n: int, nbytes: int) -> str:
     the next chunk in flight), as rocprofv3 names it."""
     big = n >= (512 << 10) and nbytes >= (256 << 20)
     u, pipe = (16, "false") if big else (8, "true")
-    return f"csum_flat_kernel<{u}, {str(ipv4).lower()}, {str(fill).lower()}, {pipe}, false>"
+    return f"csum_flat_kernel<{u}, {str(ipv4).lower()}, {str(fill).lower()}, {pipe}>"
 
 
 def parse():

@@ -20,13 +20,10 @@ extern "C" {
  * 1 = one packet per wave, per-lane byte masks (an independent second
  *     implementation kept for cross-checking; in-place fill uses the flat
  *     kernel whatever the variant).
- * 10-16 = flat kernel forms: each tile's byte extent streamed densely, unit
- *     sums prefix-scanned across the wave; U = 2 (10, 11), 4 (12, 13),
- *     8 (14, 15), 16 (16) units per lane per chunk, odd = next chunk in flight.
- * 17-19 = flat kernel with rolling rows: U = 8 / 12 / 16 rows of 64 units
- *     in flight, each pair of rows scanned as it lands and its registers
- *     reloaded with the next chunk's rows at once (A/B: slower than 16 on
- *     1500 B frames, profiles/r02_ab_roll.log).
+ * 14-16 = flat kernel forms: each tile's byte extent streamed densely, unit
+ *     sums prefix-scanned across the wave; U = 8 (14, 15: the next chunk in
+ *     flight) or 16 (16) units per lane per chunk.  (The U = 2 / 4 forms and
+ *     the rolling-row forms lost their A/Bs and were removed in round 2.)
  * SCCSUM_EINVAL for anything else. */
 int sccsum_set_kernel_variant(int variant);
 

@@ -529,13 +529,12 @@ struct Queues {
 // and the packets the fast path cannot take are redone exactly, one wave each.
 // Layouts that do not run forward (shuffled offsets) degrade to one run per
 // packet.
-template <int U, bool IPV4, bool FILL, bool PIPE, bool ROLL = false>
+template <int U, bool IPV4, bool FILL, bool PIPE>
 __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint32_t B, uint32_t* __restrict__ heads,
                                                           uint32_t flags, const RssParams rss) {
     static_assert(!FILL || IPV4, "in-place generate is a frames mode");
-    static_assert(!ROLL || (!PIPE && U % 2 == 0), "rolling rows: pairs of rows, no chunk double buffer");
     constexpr uint32_t C = kWave * U;  // units per chunk
-    constexpr uint32_t kLdsUnits = ROLL ? 2 * kWave : C;  // ROLL parks one pair of rows at a time
+    constexpr uint32_t kLdsUnits = C;
     constexpr int kHead = FILL ? 4 : (IPV4 ? 3 : 1);
     const bool raw = !IPV4 && (flags & kFlagRaw);
     const bool fill_ip = FILL && (flags & kFlagFillIp);
@@ -729,49 +728,7 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
                 }
                 __builtin_amdgcn_wave_barrier();  // this chunk's LDS reads precede the next chunk's writes
             };
-            if (ROLL) {
-                // Rolling rows: U rows of 64 units stay in flight; each pair
-                // of rows is summed, scanned and parked in LDS as soon as it
-                // lands, and its registers take the same rows of the next
-                // chunk at once, so the wave never drains its loads between
-                // chunks (rows past the extent read as zeros, no memory access).
-                u32x4 v[U];
-                load(r, 0, v);
-                for (uint32_t g = 0; g < ext; g += C) {
-#pragma unroll
-                    for (int u = 0; u < U; u += 2) {
-                        const uint32_t row = g + kWave * static_cast<uint32_t>(u);
-                        uint32_t x[2] = {sad4(v[u], 0u), sad4(v[u + 1], 0u)};
-                        wave_scan_n<2>(x);
-                        pbuf[lane] = carry + x[0];
-                        ubuf[lane] = v[u];
-                        carry += __builtin_amdgcn_readlane(x[0], 63);
-                        pbuf[kWave + lane] = carry + x[1];
-                        ubuf[kWave + lane] = v[u + 1];
-                        carry += __builtin_amdgcn_readlane(x[1], 63);
-                        v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(16u * (row + C) + vo), 0, kNT);
-                        v[u + 1] = __builtin_amdgcn_raw_buffer_load_b128(
-                            r, static_cast<int>(16u * (row + C + kWave) + vo), 0, kNT);
-                        __builtin_amdgcn_wave_barrier();
-                        const int a = rf - static_cast<int>(row);
-                        if (static_cast<uint32_t>(a) < 2 * kWave) {
-                            const u32x4 w = ubuf[a];
-                            pst = pbuf[a] - sad4(w, 0u);
-                            hs[0] = w;
-                        }
-#pragma unroll
-                        for (int j = 1; j < kHead; ++j) {
-                            if (static_cast<uint32_t>(a + j) < 2 * kWave) hs[j] = ubuf[a + j];
-                        }
-                        const int b = rl - static_cast<int>(row);
-                        if (static_cast<uint32_t>(b) < 2 * kWave) {
-                            pend = pbuf[b];
-                            hl = ubuf[b];
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                }
-            } else if (PIPE) {
+            if (PIPE) {
                 u32x4 va[U], vb[U];
                 load(r, 0, va);
                 for (uint32_t g = 0; g < ext; g += 2 * C) {
@@ -1115,7 +1072,7 @@ constexpr int kTileBytes = 49152;
 // Diagnostic knobs (include/sccsum_diag.h): per host thread, so one shard's
 // A/B settings never leak into another thread's launches.
 struct Knobs {
-    int variant = 0;                 // 0 = default; 1 = simple kernel; 10-16 = flat-kernel forms
+    int variant = 0;                 // 0 = default; 1 = simple kernel; 14-16 = flat-kernel forms
     int blocks_per_cu = kBlocksPerCU;  // grid cap in workgroups per CU
     int group_units = 0;             // simple kernel: U override (0 = by max_len)
     int tile_packets = kWave;        // flat kernel: max packets per tile
@@ -1295,9 +1252,10 @@ void launch_simple(int uc, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     }
 }
 
-// Flat-kernel forms: 10 / 11 = U 2, 12 / 13 = U 4, 14 / 15 = U 8 (odd: the
-// next chunk in flight), 16 = U 16, 17 / 18 / 19 = rolling rows U 8 / 12 / 16.
-// Frames may fill in place; spans never do.
+// Flat-kernel forms: 14 / 15 = U 8 (15: the next chunk in flight), 16 = U 16.
+// (U 2 / 4 forms and rolling rows lost their A/Bs in rounds 1-2 and were
+// removed: profiles/r01_ab_variants.log, r02_ab_roll.log.)  Frames may fill
+// in place; spans never do.
 template <bool IPV4>
 void launch_flat_variant(int variant, hipStream_t s, Queues& Q, uint64_t n_total, uint64_t bytes_total,
                          uint32_t flags, const RssParams& rss) {
@@ -1305,15 +1263,8 @@ void launch_flat_variant(int variant, hipStream_t s, Queues& Q, uint64_t n_total
     constexpr bool F = IPV4;
     const bool fill = IPV4 && (flags & kFlagFillL4);
     switch (variant) {
-        case 10: fill ? go(csum_flat_kernel<2, IPV4, F, false>) : go(csum_flat_kernel<2, IPV4, false, false>); break;
-        case 11: fill ? go(csum_flat_kernel<2, IPV4, F, true>) : go(csum_flat_kernel<2, IPV4, false, true>); break;
-        case 12: fill ? go(csum_flat_kernel<4, IPV4, F, false>) : go(csum_flat_kernel<4, IPV4, false, false>); break;
-        case 13: fill ? go(csum_flat_kernel<4, IPV4, F, true>) : go(csum_flat_kernel<4, IPV4, false, true>); break;
         case 14: fill ? go(csum_flat_kernel<8, IPV4, F, false>) : go(csum_flat_kernel<8, IPV4, false, false>); break;
         case 15: fill ? go(csum_flat_kernel<8, IPV4, F, true>) : go(csum_flat_kernel<8, IPV4, false, true>); break;
-        case 17: fill ? go(csum_flat_kernel<8, IPV4, F, false, true>) : go(csum_flat_kernel<8, IPV4, false, false, true>); break;
-        case 18: fill ? go(csum_flat_kernel<12, IPV4, F, false, true>) : go(csum_flat_kernel<12, IPV4, false, false, true>); break;
-        case 19: fill ? go(csum_flat_kernel<16, IPV4, F, false, true>) : go(csum_flat_kernel<16, IPV4, false, false, true>); break;
         default: fill ? go(csum_flat_kernel<16, IPV4, F, false>) : go(csum_flat_kernel<16, IPV4, false, false>); break;
     }
 }
@@ -1848,7 +1799,7 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
 }
 
 int sccsum_set_kernel_variant(int variant) {
-    if (!(variant == 0 || variant == 1 || (variant >= 10 && variant <= 19))) return SCCSUM_EINVAL;
+    if (!(variant == 0 || variant == 1 || (variant >= 14 && variant <= 16))) return SCCSUM_EINVAL;
     sccsum::t_knobs.variant = variant;
     return SCCSUM_OK;
 }

@@ -99,6 +99,7 @@ int main() {
     // diagnostics: thread-local knobs validate their ranges
     EXPECT(sccsum_set_kernel_variant(5) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_kernel_variant(20) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_kernel_variant(10) == SCCSUM_EINVAL && sccsum_set_kernel_variant(17) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_kernel_variant(16) == SCCSUM_OK && sccsum_set_kernel_variant(0) == SCCSUM_OK);
     EXPECT(sccsum_set_blocks_per_cu(0) == SCCSUM_EINVAL && sccsum_set_blocks_per_cu(33) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_group_units(3) == SCCSUM_EINVAL);

@@ -21,9 +21,7 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(params=[1, 10, 11, 12, 13, 14, 15, 16, 17, 19],
-                ids=["simple", "flat2", "flat2_pipe", "flat4", "flat4_pipe", "flat8", "flat8_pipe", "flat16", "roll8",
-                     "roll16"], autouse=True)
+@pytest.fixture(params=[1, 14, 15, 16], ids=["simple", "flat8", "flat8_pipe", "flat16"], autouse=True)
 def kernel_variant(request, dev):
     """Every parity test runs against both kernel families."""
     lib = native.load()
@@ -563,7 +561,7 @@ def test_rss_standalone_and_fused(dev, mode, kernel_variant):
     sccsum_ipv4_rss and the fused sccsum_ipv4_frames_rss vs the oracle, on
     fragments, options, ICMP/other protocols, padded / truncated / short frames
     at odd offsets; the fused pass leaves the checksums and status unchanged."""
-    if kernel_variant not in (1, 10, 15, 16):
+    if kernel_variant not in (1, 14, 15, 16):
         pytest.skip("RSS exercised with the simple and flat families")
     rss = json.load(open(os.path.join(GOLDEN, "rss.json")))
     buf, off, lens = synth.rss_frames(5000, seed=21)
