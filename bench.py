@@ -105,9 +105,24 @@ def launch_ranks(args) -> int:
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         env.setdefault("GLOO_SOCKET_IFNAME", "lo")  # one node: the control plane stays on loopback
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    # wait for all; if a rank fails, the others would wait at the next barrier
+    # until gloo's timeout: stop them (these exact children) and report it
     rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or (128 - code if code < 0 else code)  # a signal -s reads as 128 + s
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.05)
     for p in procs:
-        rc = max(rc, p.wait())
+        p.wait()
     return rc
 
 
@@ -691,6 +706,8 @@ def run_dry(args, world, rank):
     """--dry-run: the multi-rank control plane without a device."""
     import torch.distributed as dist
 
+    if os.environ.get("SCCSUM_DRY_RUN_FAIL_RANK") == str(rank):  # test hook: a rank that dies
+        sys.exit(3)
     t0 = time.perf_counter()
     barrier(world)
     wall = max_over_ranks(time.perf_counter() - t0, world)

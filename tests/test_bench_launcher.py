@@ -31,6 +31,21 @@ def test_launcher_starts_n_ranks_without_device(n):
     assert len({r["pid"] for r in d["ranks"]}) == n  # one process per rank
 
 
+def test_launcher_reports_a_failed_rank_and_stops_the_others():
+    """A rank that dies is reported (its exit code) and the ranks waiting for
+    it at the barrier are stopped, not left for gloo's timeout."""
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["SCCSUM_DRY_RUN_FAIL_RANK"] = "1"
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "3", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=REPO)
+    assert r.returncode == 3, r.stdout + r.stderr
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert time.monotonic() - t0 < 90
+
+
 @pytest.mark.gpu
 def test_launcher_two_ranks_on_the_gpu():
     """Two rank processes on the box's one GPU (a rehearsal of the driver's
