@@ -110,3 +110,10 @@ def test_burst_cpp_program_on_gpu(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK" in r.stdout
     print(r.stdout)
+    # zero-copy submits (pinned pool), each batch form: one fragment-list launch (2), with copies (1), gather (0)
+    for form in ("2", "1", "0"):
+        r = subprocess.run([exe, "200000", "3", "100000", "mapped", "32", form, "4096"], capture_output=True,
+                           text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "OK" in r.stdout
+        print(r.stdout)
