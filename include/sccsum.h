@@ -367,7 +367,9 @@ int sccsum_gather(const sccsum_gather_desc* d_desc, uint64_t n, void* d_dst, voi
  * the first starts at dst_off = d_off[p] and the lengths add up to d_len[p].
  * A fragment with src == NULL lies at d_stage + dst_off (bytes already in a
  * device batch; d_stage may be NULL when no fragment uses it).  A packet whose
- * fragments do not tile it gets result 0 and status SCCSUM_ST_RANGE.
+ * fragments do not tile it gets result 0 and status SCCSUM_ST_RANGE; the
+ * d_first entries themselves must index inside d_desc (not checked: the
+ * descriptor count is not an argument).
  * Results and status as sccsum_spans / sccsum_ipv4_frames (frames: IPv4
  * header + L4, the header may be split across fragments).  d_desc, d_first,
  * d_off, d_len, d_seed, d_out, d_status: device arrays (aligned to their
