@@ -771,3 +771,36 @@ def test_tile_shapes_match_oracle(dev, kernel_variant, tile_bytes, tile_packets)
     finally:
         native.check(lib.sccsum_set_tile_bytes(49152), "tile_bytes")
         native.check(lib.sccsum_set_tile_packets(64), "tile_packets")
+
+
+@pytest.mark.parametrize("seed", [101, 202, 303])
+def test_random_layouts_shuffled_overlapping(dev, kernel_variant, seed):
+    """Offsets in any order: shuffled, overlapping spans (packets sharing
+    bytes), duplicates, zero lengths, spans over 128 KiB (the exact redo) and
+    runs broken at random — spans with seeds and frames, against the oracle."""
+    rng = np.random.default_rng(seed)
+    total = 3 << 20
+    buf = rng.integers(0, 256, size=total, dtype=np.uint8)
+    n = 3000
+    kinds = rng.random(n)
+    lens = np.where(kinds < 0.05, 0, np.where(kinds < 0.07, rng.integers(131073, 300000, n),
+                                               rng.integers(1, 9001, n))).astype(np.uint32)
+    off = np.array([int(rng.integers(0, total - int(L) + 1)) for L in lens], np.uint64)
+    off[10:20] = off[0]  # duplicates of one packet
+    lens[10:20] = lens[0]
+    order = rng.permutation(n)
+    off, lens = off[order], lens[order]
+    seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    assert np.array_equal(_spans(dev, buf, off, lens, seeds), oracle.batch_spans(buf, off, lens, seeds))
+    # frames: the same layout with IPv4 headers written at each start (later writes win, as on the host)
+    fb = buf.copy()
+    for i in range(n):
+        L = int(lens[i])
+        if L >= 20:
+            o = int(off[i])
+            fb[o] = 0x45
+            fb[o + 2], fb[o + 3] = (L >> 8) & 0xFF, L & 0xFF
+            fb[o + 9] = 17 if i % 2 else 6
+    got, st = _frames(dev, fb, off, lens)
+    want, want_st = oracle.batch_ipv4(fb, off, lens)
+    assert np.array_equal(got, want) and np.array_equal(st, want_st)
