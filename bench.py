@@ -686,11 +686,12 @@ def run_e2e(args, world, rank, dev):
         assert np.array_equal(got, want), f"e2e {name} mismatch vs device-resident results"
         times = []
         for _ in range(max(1, args.steps // 4)):
+            barrier(world)  # every rank's batch crosses its own PCIe link at the same time
             t0 = time.perf_counter()
             pl.run(native.PIPE_IPV4, pool, off, length, gather=gather, max_len=FRAME)
-            times.append(time.perf_counter() - t0)
+            times.append(max_over_ranks(time.perf_counter() - t0, world))
         pl.close()
-        t = float(np.median(times))
+        t = float(np.median(times))  # median over runs of the slowest rank's time
         pcie = n * (pipeline.MBUF_SLOT if gather == native.GATHER_NONE else FRAME) + n * (12 + 4)
         res[name] = {"GiBps_packet_bytes": round(n * FRAME / t / 2**30, 2), "ms_per_batch": round(t * 1e3, 2),
                      "pcie_GBps_h2d_plus_d2h": round(pcie / t / 1e9, 2)}
