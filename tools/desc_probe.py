@@ -3,7 +3,7 @@ the fragment-list kernel (sccsum_ipv4_frames_desc) and the gather kernel
 (sccsum_gather) reading packets from a pinned host pool, against one
 contiguous hipMemcpyAsync DMA of the same byte count.  Layouts: packets back
 to back ("packed"), or one per 2304-byte mbuf slot at +256 ("slots",
-dpdk.cc:139-156), or slots of a small pool reused round robin; fixed 1500 B
+dpdk.cc:139-156), or slots of a small pool reused round robin, or the slots copied to HBM; fixed 1500 B
 or random 28..1500 B frames.  Pinned memory is cached by the GPU's L2s, so
 every timed run follows a 256 MiB device read that evicts them.
 
@@ -31,12 +31,12 @@ def main():
     for lens_kind in ("1500", "rand"):
         lens = np.full(n, 1500, np.uint32) if lens_kind == "1500" else rng.integers(28, 1501, n).astype(np.uint32)
         frames = synth.udp_ipv4_frames(min(n, 4096), 1500, seed=9)[0].reshape(-1, 1500)
-        for layout in ("packed", "slots", "slots_small_pool"):
-            if layout == "packed":
+        for layout in ("packed", "slots", "slots_small_pool", "slots_in_hbm"):
+            if layout in ("packed",):
                 src_off = np.zeros(n, np.uint64)
                 src_off[1:] = np.cumsum(((lens.astype(np.uint64) + 15) // 16) * 16)[:-1]
                 pool_len = int(src_off[-1]) + 1600
-            elif layout == "slots":
+            elif layout in ("slots", "slots_in_hbm"):
                 src_off = np.arange(n, dtype=np.uint64) * 2304 + 256
                 pool_len = n * 2304 + 64
             else:  # 2048 slots reused round robin (a 4.7 MB pool)
@@ -46,6 +46,9 @@ def main():
             for i in range(n):  # valid headers everywhere: the frames kernel reads each whole L4 range
                 pool[int(src_off[i]):int(src_off[i]) + int(lens[i])] = frames[i % frames.shape[0], :lens[i]]
             base = pool.ctypes.data
+            if layout == "slots_in_hbm":  # the same slots in device memory: the kernels' HBM rate
+                dpool = torch.from_numpy(np.asarray(pool)).to(dev)
+                base = dpool.data_ptr()
             lay = np.zeros(n, np.uint64)
             lay[1:] = np.cumsum(((lens.astype(np.uint64) + 15) // 16) * 16)[:-1]
             desc = batch.make_desc(base + src_off, lay, lens)
