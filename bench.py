@@ -80,8 +80,12 @@ def parse():
                     help="udp1500 / mixed / fill: step k launches on stream k %% S (A/B: with 2, consecutive steps' "
                          "launches run concurrently)")
     ap.add_argument("--launch", default="multi", choices=["multi", "single"],
-                    help="udp1500: one sccsum_ipv4_frames_multi launch per step over the tx and rx batches (multi, "
-                         "default) or one sccsum_ipv4_frames launch per batch (single)")
+                    help="udp1500 / mixed: one sccsum_ipv4_frames_multi launch per step over the tx and rx batches "
+                         "(multi, default) or one sccsum_ipv4_frames launch per batch (single; mixed: the rx "
+                         "batch only)")
+    ap.add_argument("--rx-out2", action="store_true",
+                    help="udp1500 / mixed: the verify (rx) half also writes both checksums per frame (default: status "
+                         "bits only, what the reference's verify keeps: ip.cc:121-127, tcp.hh:876-883)")
     ap.add_argument("--dry-run", action="store_true",
                     help="multi-rank plumbing only: launch, rendezvous, barrier, max-over-ranks, one line; "
                          "no device call (the CPU test of the launcher)")
@@ -404,7 +408,8 @@ def run_udp1500(args, world, rank, dev):
         for r in range(R):
             for i in range(ns):
                 o_tx, o_rx = outs[i]
-                pre[(r, i)] = batch.prepare_ipv4_frames_multi([(txs[r], o_tx, None), (rxs[r], o_rx, sts[r])])
+                pre[(r, i)] = batch.prepare_ipv4_frames_multi([(txs[r], o_tx, None),
+                                                               (rxs[r], o_rx if args.rx_out2 else None, sts[r])])
 
     def step(k):
         r = k % R
@@ -433,8 +438,10 @@ def run_udp1500(args, world, rank, dev):
     stream = streams[0]
 
     value = world * 2 * n * FRAME * args.steps / wall / 2**30
-    # per launch: every frame byte + 12 B metadata + 4 B of results (+ 1 B status per rx frame)
-    alg = 2 * n * (FRAME + META_BYTES + 4) + n if multi else n * (FRAME + META_BYTES + 4) + n // 2
+    # per launch: every frame byte + 12 B metadata + the results written: tx 4 B (IP, UDP checksums), rx 1 B
+    # of status bits (+ 4 B with --rx-out2; --launch single always writes both)
+    rx_out = 4 if (args.rx_out2 or not multi) else 0
+    alg = (n * (FRAME + META_BYTES + 4) + n * (FRAME + META_BYTES + 1 + rx_out)) // per_step
     ceiling = read_ceiling(txs[0].data, txs[0].bytes_len, stream)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -488,39 +495,78 @@ def run_tcp64k(args, world, rank, dev):
 
 def run_mixed(args, world, rank, dev):
     """cfg 3: Zipf(1.2) frame lengths 64..9000 B, contiguous packing (odd
-    offsets), ~1.5 GB per GPU, IPv4 + UDP checksums per frame."""
+    offsets), ~1.5 GB per batch, IPv4 + UDP checksums per frame.  Like cfg 2,
+    a step is both directions of the traffic: generate over a tx batch
+    (checksum fields zero) and verify over an rx batch (its own Zipf draw,
+    checksums stored in place by sccsum_ipv4_fill) — one
+    sccsum_ipv4_frames_multi launch (--launch multi, default), or one
+    sccsum_ipv4_frames launch over the rx batch alone (--launch single)."""
     from seastar_amd import synth
 
     n = args.packets if args.packets != (1 << 20) else 3_400_000
+    multi = args.launch == "multi"
     lens = synth.zipf_lengths(n, seed=SEED + rank)
+    lens_rx = synth.zipf_lengths(n, seed=SEED + 7717 + rank) if multi else lens
     R = max(1, args.rotate)  # distinct batches launched in turn (no cached-line replay)
     align = max(1, args.align)
-    bs = [devsynth.mixed_frames(lens, seed=SEED + 31 * rank + 7 * r, device=dev, align=align) for r in range(R)]
+    rxs = [devsynth.mixed_frames(lens_rx, seed=SEED + 31 * rank + 7 * r, device=dev, align=align) for r in range(R)]
+    txs = ([devsynth.mixed_frames(lens, seed=SEED + 131 * rank + 17 * r + 5, device=dev, align=align)
+            for r in range(R)] if multi else [])
     streams = make_streams(args, dev)
+    if R % len(streams):  # a batch (and its status buffer) must always come back to the same stream
+        streams = streams[:1]
     ns = len(streams)
-    outs = [torch.empty(2 * n, dtype=torch.int16, device=dev) for _ in range(ns)]
     stream = streams[0]
+    outs = [(torch.empty(2 * n, dtype=torch.int16, device=dev), torch.empty(2 * n, dtype=torch.int16, device=dev))
+            for _ in range(ns)]
+    sts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(R)]
+    for rx, st in zip(rxs, sts):  # rx: checksums stored, so every frame verifies
+        batch.ipv4_fill(rx, native.FILL_IP | native.FILL_L4)
+        if multi:
+            batch.ipv4_frames(rx, out2=outs[0][1], status=st)
+            LAUNCHES.add(flat_kernel(True, False, n, rx.bytes_len))
+    LAUNCHES.add(flat_kernel(True, True, n, rxs[0].bytes_len), R)
+    torch.cuda.synchronize()
+    if multi:
+        for st in sts:
+            assert int((st != 3).sum()) == 0, "mixed rx frames do not verify"
+    total = int(lens.sum()) + (int(lens_rx.sum()) if multi else 0)
+    nbytes = total  # packet bytes checksummed per step
+    if multi:
+        kern = flat_kernel(True, False, 2 * n, rxs[0].bytes_len + txs[0].bytes_len)
+        pre = {(r, i): batch.prepare_ipv4_frames_multi([(txs[r], outs[i][0], None),
+                                                        (rxs[r], outs[i][1] if args.rx_out2 else None, sts[r])])
+               for r in range(R) for i in range(ns)}
+    else:
+        kern = flat_kernel(True, False, n, rxs[0].bytes_len)
+        # prebuilt launches: a step only crosses the C-ABI
+        pre = {(r, i): batch.prepare_call("sccsum_ipv4_frames", rxs[r].data, rxs[r].bytes_len, rxs[r].off,
+                                          rxs[r].length, outs[i][1], None, rxs[r].n, rxs[r].max_len)
+               for r in range(R) for i in range(ns)}
     warm = max(args.warmup, R)
-    kern = flat_kernel(True, False, n, bs[0].bytes_len)
     LAUNCHES.add(kern, warm)
     sel = LAUNCHES.select(kern, args.steps)
-    # prebuilt launches: a step only crosses the C-ABI
-    pre = {(r, i): batch.prepare_call("sccsum_ipv4_frames", bs[r].data, bs[r].bytes_len, bs[r].off, bs[r].length,
-                                      outs[i], None, bs[r].n, bs[r].max_len)
-           for r in range(R) for i in range(ns)}
     wall, launch_s = timed(lambda k: pre[(k % R, k % ns)](streams[k % ns]), args.steps, warm, world, streams)
-    total = int(lens.sum())
-    alg = total + n * (META_BYTES + 4)
-    ceiling = read_ceiling(bs[0].data, bs[0].bytes_len, stream)
+    # per launch: every frame byte + 12 B metadata + the results: 4 B per frame, except a multi step's rx
+    # half, which writes 1 B of status bits (+ 4 B with --rx-out2)
+    alg = (total + n * (META_BYTES + 4) + n * (META_BYTES + 1 + (4 if args.rx_out2 else 0)) if multi
+           else total + n * (META_BYTES + 4))
+    ceiling = read_ceiling(rxs[0].data, rxs[0].bytes_len, stream)
     if rank == 0:
         emit("GiB/s device-resident Internet checksum, mixed-MTU Zipf batches (cfg 3)",
-             world * total * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
+             world * nbytes * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": ("cfg3: Zipf(s=1.2) IPv4/UDP frames 64..9000 B, packed back to back (odd offsets)" if align == 1
-                           else f"cfg3 (ii): Zipf(s=1.2) IPv4/UDP frames 64..9000 B, each at a {align} B boundary"),
-              "packets_per_gpu": n, "bytes_per_gpu": total, "mean_len": round(total / n, 1),
-              "rotation": f"{R} distinct batches launched in turn", "streams": f"{ns} (step k on stream k % {ns})",
-              "parallelism": f"{world} independent shards"},
-             roofline(alg, launch_s, "mixed", kern + " (sccsum_ipv4_frames)", sel, args,
+                           else f"cfg3 (ii): Zipf(s=1.2) IPv4/UDP frames 64..9000 B, each at a {align} B boundary")
+                          + ("; step = generate over a tx batch + verify over an rx batch" if multi
+                             else "; step = verify over one batch"),
+              "packets_per_gpu": (2 * n if multi else n), "bytes_per_gpu": total,
+              "mean_len": round(total / (2 * n if multi else n), 1),
+              "launch": ("one sccsum_ipv4_frames_multi launch per step over the tx and rx batches" if multi
+                         else "one sccsum_ipv4_frames launch per step"),
+              "rotation": f"{R} distinct batch {'pairs' if multi else 'sets'} launched in turn",
+              "streams": f"{ns} (step k on stream k % {ns})", "parallelism": f"{world} independent shards"},
+             roofline(alg, launch_s, "mixed", kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi
+                                                      else " (sccsum_ipv4_frames)"), sel, args,
                       {"measured_read_ceiling_GBps": round(ceiling, 1)}))
 
 

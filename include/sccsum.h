@@ -115,7 +115,11 @@ int sccsum_spans(const void* d_bytes, uint64_t bytes_len,
  *                  that L4 span's length as uint16_t)
  *   For generate, pass frames whose checksum fields are zero and store the
  *   outputs; for verify, pass received frames and test the status bits.
- *   d_status may be NULL.  max_len as for sccsum_spans. */
+ *   d_status may be NULL.  max_len as for sccsum_spans.
+ *   Verify only: d_out2 may be NULL when d_status is given — the launch then
+ *   writes 1 status byte per frame instead of 4 + 1 (the reference's verify
+ *   keeps only get() != 0: ip.cc:121-127, tcp.hh:876-883).  The same holds
+ *   per batch in sccsum_ipv4_frames_multi.  Neither given: SCCSUM_EINVAL. */
 int sccsum_ipv4_frames(const void* d_bytes, uint64_t bytes_len,
                        const uint64_t* d_off, const uint32_t* d_len,
                        uint16_t* d_out2, uint8_t* d_status, uint64_t n, uint32_t max_len,

@@ -45,6 +45,16 @@ int sccsum_set_tile_bytes(int bytes);
  * dealt round robin (0). */
 int sccsum_set_dynamic_tiles(int on);
 
+/* Flat kernel: cut the launch's last tiles (quarters / 4 tiles per wave of the
+ * grid, 0..64) into `split` sub-tiles each (1 = no split, 2, 4 or 8), so the
+ * launch's drain waits on short tiles. */
+int sccsum_set_tail_split(int split, int quarters);
+
+/* Flat kernel: cache policy of the per-tile result stores (0 = plain global
+ * store; buffer stores with 1 = nt, the default, 2 = sc1, 3 = sc0 sc1,
+ * 4 = sc0).  SCCSUM_EINVAL outside 0..4. */
+int sccsum_set_out_policy(int policy);
+
 /* Stream-read `bytes` (multiple of 16) from d_src with the same
  * load width as the checksum kernels and write one 64-bit word per workgroup
  * to d_sink (capacity >= sccsum_read_probe_blocks()).  Used by bench.py as

@@ -102,6 +102,21 @@ def ipv4_frames(batch: PacketBatch, out2: torch.Tensor | None = None, status: to
     return out2[: 2 * n].view(n, 2) if n else out2[:0].view(0, 2)
 
 
+def verify_frames(batch: PacketBatch, status: torch.Tensor, stream=None) -> torch.Tensor:
+    """sccsum_ipv4_frames in verify-only form (no d_out2): per-frame status
+    bits only — what the reference's verify keeps of the sum (ip.cc:121-127,
+    tcp.hh:876-883: drop when get() != 0).  Returns status[:n]."""
+    lib = native.load()
+    n = batch.n
+    assert status is not None and status.dtype == torch.uint8 and status.numel() >= n
+    code = lib.sccsum_ipv4_frames(
+        ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length),
+        None, ctypes_ptr(status), n, batch.max_len, _stream(stream),
+    )
+    native.check(code, "sccsum_ipv4_frames")
+    return status[:n]
+
+
 def _multi(fn, name, items, max_len, stream, width, with_seed):
     lib = native.load()
     if len(items) > native.MAX_BATCHES:
@@ -139,9 +154,10 @@ def prepare_ipv4_frames_multi(items):
         raise ValueError(f"1..{native.MAX_BATCHES} batches per launch")
     arr = (native.Batch * len(items))()
     for i, (b, out, status) in enumerate(items):
-        assert out is not None and out.numel() >= 2 * b.n
+        # out None: a verify-only batch (status bits only)
+        assert (out is not None and out.numel() >= 2 * b.n) or (status is not None and status.numel() >= b.n)
         arr[i] = native.Batch(ctypes_ptr(b.data), b.bytes_len, ctypes_ptr(b.off), ctypes_ptr(b.length), None,
-                              ctypes_ptr(out), _ptr(status), b.n)
+                              _ptr(out), _ptr(status), b.n)
     ml = max(it[0].max_len for it in items)
     fn, ptr, nb = lib.sccsum_ipv4_frames_multi, ctypes.cast(arr, ctypes.c_void_p), len(items)
 

@@ -237,7 +237,7 @@ __global__ __launch_bounds__(kBlock) void csum_kernel(
         if (o > bytes_len || L > bytes_len - o || (IPV4 && L < 20)) {
             if (lane == 0) {
                 if (IPV4) {
-                    reinterpret_cast<uint32_t*>(out)[p] = 0;
+                    if (out) reinterpret_cast<uint32_t*>(out)[p] = 0;
                 } else {
                     out[p] = 0;
                 }
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(kBlock) void csum_kernel(
         const uint32_t r = raw ? S : ~S & 0xffffu;
         if (lane == 0) {
             if (IPV4) {
-                reinterpret_cast<uint32_t*>(out)[p] = ipc | (r << 16);
+                if (out) reinterpret_cast<uint32_t*>(out)[p] = ipc | (r << 16);
                 if (status) {
                     status[p] = st | (ipc == 0 ? SCCSUM_ST_OK : 0u) | (r == 0 ? SCCSUM_ST_L4_OK : 0u);
                 }
@@ -492,6 +492,36 @@ __device__ __forceinline__ uint32_t header_dword(const u32x4 (&h)[4], uint32_t h
     return __builtin_amdgcn_alignbyte(pick(i + 1), pick(i), head & 3u);
 }
 
+// Output stores of a tile (diagnostic A/B of the cache policy, flags bits
+// kOutPolicyShift..+2): 0 = plain global store; buffer stores with 1 = nt,
+// 2 = sc1, 3 = sc0 sc1, 4 = sc0.  t + lane is the element this lane writes.
+constexpr uint32_t kOutPolicyShift = 8;
+template <typename T>
+__device__ __forceinline__ void tile_store(T* t, uint32_t lane, T v, uint32_t pol) {
+    if (pol == 0) {
+        t[lane] = v;
+        return;
+    }
+    const auto r = rsrc(reinterpret_cast<const uint8_t*>(t), 64u * sizeof(T));
+    const int o = static_cast<int>(sizeof(T) * lane);
+    auto st = [&](auto aux) {
+        constexpr int a = decltype(aux)::value;
+        if constexpr (sizeof(T) == 4) {
+            __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(v), r, o, 0, a);
+        } else if constexpr (sizeof(T) == 2) {
+            __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(v), r, o, 0, a);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), r, o, 0, a);
+        }
+    };
+    switch (pol) {
+        case 1: st(std::integral_constant<int, 2>{}); break;
+        case 2: st(std::integral_constant<int, 16>{}); break;
+        case 3: st(std::integral_constant<int, 17>{}); break;
+        default: st(std::integral_constant<int, 1>{}); break;
+    }
+}
+
 constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B) between packets
 
 // The batches one flat-kernel launch works through: up to kMaxQueues
@@ -502,6 +532,13 @@ constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B)
 constexpr uint32_t kMaxQueues = 16;
 struct Queues {
     uint32_t nq;
+    // Tail split: tiles from `tsplit` on (the launch's last ones, dequeued
+    // last) are cut into 2^sub_log2 sub-tiles of `bsub` packets, so the
+    // launch's drain waits on short tiles.  Tile numbers are virtual:
+    // [0, tsplit) are whole tiles, then sub-tile s of whole tile
+    // tsplit + (v - tsplit) >> sub_log2.
+    uint64_t tsplit;
+    uint32_t sub_log2, bsub;
     uint64_t tile0[kMaxQueues + 1];
     const uint8_t* bytes[kMaxQueues];
     uint64_t bytes_len[kMaxQueues];
@@ -545,13 +582,33 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
     u32x4* ubuf = ubuf_all[wv];
     uint32_t* pbuf = pbuf_all[wv];
     const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
-    const uint64_t ntiles = Q.tile0[Q.nq];  // B packets per tile, numbered across the queues
+    // B packets per whole tile, numbered across the queues; the tail's whole
+    // tiles count 2^sub_log2 virtual tiles each
+    const uint64_t ntiles = Q.tsplit + ((Q.tile0[Q.nq] - Q.tsplit) << Q.sub_log2);
     const uint32_t vo = 16u * lane;
-    // queue of (wave-uniform) tile tt: a scalar walk over <= kMaxQueues prefixes
-    auto queue_of = [&](uint64_t tt) -> uint32_t {
-        uint32_t q = 0;
-        while (q + 1 < Q.nq && tt >= Q.tile0[q + 1]) ++q;
-        return q;
+    // (wave-uniform) virtual tile tt -> its queue, first packet and packet
+    // count (0 for a sub-tile past the end of a short last tile): a scalar
+    // walk over <= kMaxQueues prefixes
+    struct TileRef {
+        uint32_t q, cnt;
+        uint64_t base;
+    };
+    auto tile_ref = [&](uint64_t tt) -> TileRef {
+        const bool sub = tt >= Q.tsplit;
+        const uint64_t w = sub ? Q.tsplit + ((tt - Q.tsplit) >> Q.sub_log2) : tt;
+        TileRef r;
+        r.q = 0;
+        while (r.q + 1 < Q.nq && w >= Q.tile0[r.q + 1]) ++r.q;
+        r.base = (w - Q.tile0[r.q]) * B;
+        const uint64_t left = Q.n[r.q] - r.base;  // >= 1
+        r.cnt = left < B ? static_cast<uint32_t>(left) : B;
+        if (sub) {
+            const uint32_t s0 = static_cast<uint32_t>((tt - Q.tsplit) & ((1u << Q.sub_log2) - 1u)) * Q.bsub;
+            const uint32_t c = s0 < r.cnt ? r.cnt - s0 : 0u;
+            r.base += s0 < r.cnt ? s0 : 0u;  // an empty sub-tile keeps a valid base
+            r.cnt = c < Q.bsub ? c : Q.bsub;
+        }
+        return r;
     };
 
     // Tile order.  Wave w first takes tile w (static: no start-up contention).
@@ -588,12 +645,10 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
     if (t >= ntiles && heads != nullptr) t = next_tile(t);
     uint64_t t1 = t < ntiles ? next_tile(t) : ntiles;
     auto plan_load = [&](uint64_t tt, uint64_t& o_, uint32_t& L_, uint32_t& sd_) {
-        const uint64_t t_ = tt < ntiles ? tt : 0;
-        const uint32_t qq = queue_of(t_);
-        const uint64_t b_ = (t_ - Q.tile0[qq]) * B;
-        const uint64_t nq_ = Q.n[qq];
-        const uint32_t c_ = tt < ntiles ? static_cast<uint32_t>(nq_ - b_ < B ? nq_ - b_ : B) : 0u;
-        const uint64_t q_ = b_ + (lane < c_ ? lane : 0);
+        const TileRef tr = tile_ref(tt < ntiles ? tt : 0);
+        const uint32_t qq = tr.q;
+        const uint32_t c_ = tt < ntiles ? tr.cnt : 0u;
+        const uint64_t q_ = tr.base + (lane < c_ ? lane : 0);
         o_ = Q.off[qq][q_];
         L_ = lane < c_ ? Q.len[qq][q_] : 0u;
         const uint32_t* sq = IPV4 ? nullptr : Q.seed[qq];
@@ -610,10 +665,10 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
     };
     auto derive = [&](uint64_t tt, uint64_t o_, uint32_t L_, uint32_t sd_) {
         Tile c;
-        c.q = queue_of(tt);
-        c.base = (tt - Q.tile0[c.q]) * B;
-        const uint64_t left = Q.n[c.q] - c.base;
-        c.cnt = left < B ? static_cast<uint32_t>(left) : B;
+        const TileRef tr = tile_ref(tt);
+        c.q = tr.q;
+        c.base = tr.base;
+        c.cnt = tr.cnt;
         c.mine = lane < c.cnt;
         c.o = o_;
         c.L = L_;
@@ -871,12 +926,13 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
         uint16_t* const out = Q.out[cur.q];
         uint8_t* const status = Q.status[cur.q];
         if (mine) {
+            const uint32_t pol = (flags >> kOutPolicyShift) & 7u;
             if (IPV4) {
-                if (out) reinterpret_cast<uint32_t*>(out)[base + lane] = word;
+                if (out) tile_store(reinterpret_cast<uint32_t*>(out) + base, lane, word, pol);
             } else {
-                out[base + lane] = static_cast<uint16_t>(word);
+                tile_store(out + base, lane, static_cast<uint16_t>(word), pol);
             }
-            if (status) status[base + lane] = static_cast<uint8_t>(st);
+            if (status) tile_store(status + base, lane, static_cast<uint8_t>(st), pol);
         }
         t = t1;
         t1 = t2;
@@ -1069,6 +1125,21 @@ int cu_count() {
 // packets per tile run slower than 64 (profiles/r02_ab_tiles2.log).
 constexpr int kTileBytes = 49152;
 
+// Tail split: the launch's last whole tiles (kTailQuarters / 4 per wave of the
+// grid) are cut into kTailSplit sub-tiles each.  When the dequeue runs dry
+// every wave is part-way through a tile and the launch ends with its slowest;
+// short tiles at the end shorten that drain.
+// A/B (profiles/r02_ab_tail.log): no gain on 1500 B frames (split 2-4: -0.3 %
+// to -0.5 %), a loss on Zipf frames (split 4: +1.5 %, 8: +6.5 % time), so off.
+constexpr int kTailSplit = 1;
+constexpr int kTailQuarters = 4;
+
+// Result stores nontemporal by default: the per-tile out2 / status stores mix
+// into the read stream, and an nt (or sc1) store leaves less in the way than a
+// plain one (profiles/r02_ab_outpol.log: 2 M frames 464.8 -> 460.2 us, Zipf
+// frames 237.4 -> 235.5 us; sc1 / sc0 sc1 the same, sc0 no gain).
+constexpr int kOutPolicy = 1;
+
 // Diagnostic knobs (include/sccsum_diag.h): per host thread, so one shard's
 // A/B settings never leak into another thread's launches.
 struct Knobs {
@@ -1078,6 +1149,9 @@ struct Knobs {
     int tile_packets = kWave;        // flat kernel: max packets per tile
     int dynamic = 1;                 // flat kernel: dequeue tiles (1) or static round robin (0)
     int tile_bytes = kTileBytes;     // flat kernel: target bytes per tile (0 = packets cap only)
+    int tail_split = kTailSplit;     // flat kernel: sub-tiles per tail tile (1, 2, 4 or 8; 1 = no split)
+    int tail_quarters = kTailQuarters;  // flat kernel: tail = tail_quarters / 4 whole tiles per wave of the grid
+    int out_policy = kOutPolicy;     // flat kernel: cache policy of the result stores (tile_store)
 };
 thread_local Knobs t_knobs;
 
@@ -1231,11 +1305,20 @@ void launch_flat(FlatKernel kern, hipStream_t s, Queues& Q, uint64_t n_total, ui
     B = B < 1 ? 1 : (B > bmax ? bmax : B);
     Q.tile0[0] = 0;
     for (uint32_t q = 0; q < Q.nq; ++q) Q.tile0[q + 1] = Q.tile0[q] + (Q.n[q] + B - 1) / B;
-    const uint64_t tiles = Q.tile0[Q.nq];
+    const uint64_t whole = Q.tile0[Q.nq];
+    // tail split (sub-tiles of at least one packet, a power of two per tile)
+    uint32_t lg = 0;
+    while ((2u << lg) <= static_cast<uint32_t>(K.tail_split) && (2ull << lg) <= B) ++lg;
+    const uint64_t tail = lg ? static_cast<uint64_t>(K.tail_quarters) * slots / 4 : 0;
+    Q.tsplit = whole > tail ? whole - tail : 0;
+    Q.sub_log2 = lg;
+    Q.bsub = static_cast<uint32_t>((B + (1u << lg) - 1) >> lg);
+    const uint64_t tiles = Q.tsplit + ((whole - Q.tsplit) << lg);
     uint64_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     blocks = blocks < cap ? blocks : cap;
     blocks = (blocks + 15) & ~uint64_t(15);  // multiple of 16: XCD mapping, waves divide into kGroups
     uint32_t* heads = K.dynamic ? heads_for(s) : nullptr;
+    flags |= static_cast<uint32_t>(K.out_policy) << kOutPolicyShift;
     kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(Q, static_cast<uint32_t>(B), heads, flags, rss);
 }
 
@@ -1290,8 +1373,11 @@ const RssParams kNoRss{};
 // One batch's arguments, checked as every entry point checks them.
 template <bool IPV4>
 bool batch_ok(const void* d_bytes, const uint64_t* d_off, const uint32_t* d_len, const uint32_t* d_seed,
-              const void* d_out, uint32_t flags) {
-    if (!d_bytes || !d_off || !d_len || (!d_out && !(flags & kFlagFillL4))) return false;
+              const void* d_out, const uint8_t* d_status, uint32_t flags) {
+    // frames: a verify-only launch may pass the status array alone (the
+    // reference's verify only tests get() != 0, ip.cc:121-127, tcp.hh:876-883)
+    const bool out_optional = (flags & kFlagFillL4) || (IPV4 && d_status != nullptr);
+    if (!d_bytes || !d_off || !d_len || (!d_out && !out_optional)) return false;
     return !((reinterpret_cast<uintptr_t>(d_bytes) & 15u) || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
              (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_seed) & 3u) ||
              (reinterpret_cast<uintptr_t>(d_out) & (IPV4 ? 3u : 1u)));
@@ -1313,7 +1399,7 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
            const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n, uint32_t max_len,
            void* stream, uint32_t flags = 0, const RssParams& rss = kNoRss) {
     if (n == 0) return SCCSUM_OK;
-    if (!batch_ok<IPV4>(d_bytes, d_off, d_len, d_seed, d_out, flags)) return SCCSUM_EINVAL;
+    if (!batch_ok<IPV4>(d_bytes, d_off, d_len, d_seed, d_out, d_status, flags)) return SCCSUM_EINVAL;
     const int variant = pick_variant(n, bytes_len, flags);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
@@ -1346,7 +1432,7 @@ int launch_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
     uint64_t n_total = 0, bytes_total = 0;
     for (uint32_t i = 0; i < nbatch; ++i) {
         const sccsum_batch& x = batches[i];
-        if (x.n && !batch_ok<IPV4>(x.d_bytes, x.d_off, x.d_len, IPV4 ? nullptr : x.d_seed, x.d_out, 0)) {
+        if (x.n && !batch_ok<IPV4>(x.d_bytes, x.d_off, x.d_len, IPV4 ? nullptr : x.d_seed, x.d_out, x.d_status, 0)) {
             return SCCSUM_EINVAL;
         }
         if (IPV4 && x.d_seed) return SCCSUM_EINVAL;  // frames derive their pseudo-header in-kernel
@@ -1831,6 +1917,19 @@ int sccsum_set_tile_bytes(int bytes) {
 int sccsum_set_dynamic_tiles(int on) {
     if (on != 0 && on != 1) return SCCSUM_EINVAL;
     sccsum::t_knobs.dynamic = on;
+    return SCCSUM_OK;
+}
+
+int sccsum_set_out_policy(int policy) {
+    if (policy < 0 || policy > 4) return SCCSUM_EINVAL;
+    sccsum::t_knobs.out_policy = policy;
+    return SCCSUM_OK;
+}
+
+int sccsum_set_tail_split(int split, int quarters) {
+    if (!(split == 1 || split == 2 || split == 4 || split == 8) || quarters < 0 || quarters > 64) return SCCSUM_EINVAL;
+    sccsum::t_knobs.tail_split = split;
+    sccsum::t_knobs.tail_quarters = quarters;
     return SCCSUM_OK;
 }
 

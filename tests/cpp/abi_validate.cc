@@ -106,6 +106,11 @@ int main() {
     EXPECT(sccsum_set_tile_packets(65) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_tile_bytes(-1) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_dynamic_tiles(2) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_tail_split(3, 4) == SCCSUM_EINVAL && sccsum_set_tail_split(16, 4) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_tail_split(4, -1) == SCCSUM_EINVAL && sccsum_set_tail_split(4, 65) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_tail_split(4, 4) == SCCSUM_OK && sccsum_set_tail_split(1, 4) == SCCSUM_OK);
+    EXPECT(sccsum_set_out_policy(-1) == SCCSUM_EINVAL && sccsum_set_out_policy(5) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_out_policy(3) == SCCSUM_OK && sccsum_set_out_policy(0) == SCCSUM_OK);
     EXPECT(sccsum_set_burst_fused(3) == SCCSUM_EINVAL && sccsum_set_burst_fused(-1) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_burst_fused(2) == SCCSUM_OK);
     EXPECT(sccsum_pipeline_run(nullptr, SCCSUM_PIPE_IPV4, SCCSUM_GATHER_ZERO_COPY, nullptr, 0, nullptr, nullptr,

@@ -773,6 +773,105 @@ def test_tile_shapes_match_oracle(dev, kernel_variant, tile_bytes, tile_packets)
         native.check(lib.sccsum_set_tile_packets(64), "tile_packets")
 
 
+def test_verify_only_frames(dev, kernel_variant):
+    """Frames with no d_out2 and a status array (verify only): the status bits
+    equal the oracle's, single and multi launch; no d_out2 and no status is
+    refused."""
+    rng = np.random.default_rng(77)
+    buf, off, lens = _tx_frames(rng, 700)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
+    b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+    st = torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev)
+    got = batch.verify_frames(b, st)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy(), want_st)
+    buf2, off2, lens2, _ = synth.mixed_udp_frames(900, seed=78, max_gap=3)
+    want2, want_st2 = oracle.batch_ipv4(buf2, off2, lens2)
+    b2 = batch.PacketBatch.from_host(buf2, off2, lens2, device=dev)
+    st.fill_(0xEE)
+    st2 = torch.full((b2.n,), 0xEE, dtype=torch.uint8, device=dev)
+    o2 = torch.empty(2 * b2.n, dtype=torch.int16, device=dev)
+    batch.prepare_ipv4_frames_multi([(b, None, st), (b2, o2, st2)])(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), want_st) and np.array_equal(st2.cpu().numpy(), want_st2)
+    assert np.array_equal(batch.as_u16(o2).reshape(-1, 2), want2)
+    lib = native.load()
+    rc = lib.sccsum_ipv4_frames(batch.ctypes_ptr(b.data), b.bytes_len, batch.ctypes_ptr(b.off),
+                                batch.ctypes_ptr(b.length), None, None, b.n, b.max_len, None)
+    assert rc == native.SCCSUM_EINVAL
+
+
+@pytest.mark.parametrize("policy", [0, 1, 2, 3, 4])
+def test_out_policies_match_oracle(dev, kernel_variant, policy):
+    """The result stores' cache policy (sccsum_set_out_policy; nt by default)
+    changes nothing in the results: frames with and without status, spans."""
+    if kernel_variant not in (15, 16):
+        pytest.skip("the policy applies to the flat kernel")
+    lib = native.load()
+    native.check(lib.sccsum_set_out_policy(policy), "out_policy")
+    try:
+        rng = np.random.default_rng(500 + policy)
+        buf, off, lens = _tx_frames(rng, 900)
+        got, st = _frames(dev, buf, off, lens)
+        want, want_st = oracle.batch_ipv4(buf, off, lens)
+        assert np.array_equal(got, want) and np.array_equal(st, want_st)
+        lens = rng.integers(0, 3000, 3001).astype(np.uint32)
+        off, total = synth.pack(lens, seed=501, max_gap=7)
+        buf = rng.integers(0, 256, size=int(total), dtype=np.uint8)
+        got, st = _spans(dev, buf, off, lens, with_status=True)
+        want = oracle.batch_spans(buf, off, lens)
+        assert np.array_equal(got, want) and np.array_equal(st, (want == 0).astype(np.uint8))
+    finally:
+        native.check(lib.sccsum_set_out_policy(1), "out_policy")
+
+
+@pytest.mark.parametrize("split,quarters,tile_packets,bpc",[(2, 4, 64, 8), (4, 4, 64, 8), (8, 4, 64, 8),
+                                                             (4, 1, 7, 1), (8, 2, 13, 1), (4, 64, 64, 8),
+                                                             (2, 0, 64, 8)])
+def test_tail_split_matches_oracle(dev, kernel_variant, split, quarters, tile_packets, bpc):
+    """The tail split (the launch's last tiles cut into sub-tiles, some of them
+    empty when a queue's last tile is short) changes only the schedule: single
+    and multi-queue launches of frames and spans match the oracle, with the
+    split point inside the launch (small grid, 7 / 13-packet tiles) or before
+    its first tile."""
+    if kernel_variant not in (15, 16):
+        pytest.skip("tail split exercised on the default flat forms")
+    lib = native.load()
+    native.check(lib.sccsum_set_tail_split(split, quarters), "tail_split")
+    native.check(lib.sccsum_set_tile_packets(tile_packets), "tile_packets")
+    native.check(lib.sccsum_set_blocks_per_cu(bpc), "blocks_per_cu")
+    try:
+        buf, off, lens, _ = synth.udp_ipv4_frames(3001, 1500, seed=191)
+        got, st = _frames(dev, buf, off, lens)
+        want, want_st = oracle.batch_ipv4(buf, off, lens)
+        assert np.array_equal(got, want) and np.array_equal(st, want_st)
+        buf, off, lens, _ = synth.mixed_udp_frames(5003, seed=192, max_gap=3)
+        got, st = _frames(dev, buf, off, lens)
+        want, want_st = oracle.batch_ipv4(buf, off, lens)
+        assert np.array_equal(got, want) and np.array_equal(st, want_st)
+        items, wants = [], []
+        for q, n in enumerate([1, 257, 3000, 63, 1999]):
+            buf, off, lens, _ = synth.mixed_udp_frames(n, seed=300 + q, max_gap=2)
+            items.append((batch.PacketBatch.from_host(buf, off, lens, device=dev), None,
+                          torch.empty(n, dtype=torch.uint8, device=dev)))
+            wants.append(oracle.batch_ipv4(buf, off, lens))
+        outs = batch.ipv4_frames_multi(items)
+        torch.cuda.synchronize()
+        for o, it, (w, wst) in zip(outs, items, wants):
+            assert np.array_equal(batch.as_u16(o).reshape(-1), w.reshape(-1))
+            assert np.array_equal(it[2].cpu().numpy(), wst)
+        rng = np.random.default_rng(193)
+        lens = rng.integers(0, 9000, 4001).astype(np.uint32)
+        off, total = synth.pack(lens, seed=194, max_gap=5)
+        buf = rng.integers(0, 256, size=int(total), dtype=np.uint8)
+        seeds = rng.integers(0, 65536, lens.size).astype(np.uint32)
+        assert np.array_equal(_spans(dev, buf, off, lens, seeds), oracle.batch_spans(buf, off, lens, seeds))
+    finally:
+        native.check(lib.sccsum_set_tail_split(1, 4), "tail_split")
+        native.check(lib.sccsum_set_tile_packets(64), "tile_packets")
+        native.check(lib.sccsum_set_blocks_per_cu(8), "blocks_per_cu")
+
+
 @pytest.mark.parametrize("seed", [101, 202, 303])
 def test_random_layouts_shuffled_overlapping(dev, kernel_variant, seed):
     """Offsets in any order: shuffled, overlapping spans (packets sharing

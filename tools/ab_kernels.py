@@ -61,7 +61,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn[:tile_bytes]]]]]")
+    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn[:tile_bytes[:tail_split[:tail_quarters[:out_policy]]]]]]]]")
     ap.add_argument("--rotate", type=int, default=4, help="distinct copies of each batch, launched in turn")
     ap.add_argument("--cases", default="udp1500_frames,udp1500_spans,udp1500_frames_rss,zipf_spans,cfg3_zipf_frames,"
                                        "tcp64k_spans")
@@ -82,13 +82,15 @@ def main():
         turn = [0]
 
         def knobs(v):
-            parts = (v.split(":") + ["", "", "", "", "", ""])[:6]
+            parts = (v.split(":") + [""] * 9)[:9]
             native.check(lib.sccsum_set_kernel_variant(int(parts[0])), "variant")
             native.check(lib.sccsum_set_blocks_per_cu(int(parts[1] or 8)), "blocks_per_cu")
             native.check(lib.sccsum_set_group_units(int(parts[2] or 0)), "group_units")
             native.check(lib.sccsum_set_tile_packets(int(parts[3] or 64)), "tile_packets")
             native.check(lib.sccsum_set_dynamic_tiles(int(parts[4] or 1)), "dynamic")
             native.check(lib.sccsum_set_tile_bytes(int(parts[5] or 49152)), "tile_bytes")
+            native.check(lib.sccsum_set_tail_split(int(parts[6] or 1), int(parts[7] or 4)), "tail_split")
+            native.check(lib.sccsum_set_out_policy(int(parts[8] or 1)), "out_policy")
 
         def run(bb):
             if mode == "frames":
@@ -134,6 +136,8 @@ def main():
     native.check(lib.sccsum_set_tile_packets(64), "tile_packets")
     native.check(lib.sccsum_set_dynamic_tiles(1), "dynamic")
     native.check(lib.sccsum_set_tile_bytes(49152), "tile_bytes")
+    native.check(lib.sccsum_set_tail_split(1, 4), "tail_split")
+    native.check(lib.sccsum_set_out_policy(1), "out_policy")
 
 
 if __name__ == "__main__":
