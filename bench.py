@@ -79,10 +79,11 @@ def parse():
     ap.add_argument("--streams", type=int, default=1,
                     help="udp1500 / mixed / fill: step k launches on stream k %% S (A/B: with 2, consecutive steps' "
                          "launches run concurrently)")
-    ap.add_argument("--launch", default="multi", choices=["multi", "single"],
+    ap.add_argument("--launch", default=None, choices=["multi", "single"],
                     help="udp1500 / mixed: one sccsum_ipv4_frames_multi launch per step over the tx and rx batches "
-                         "(multi, default) or one sccsum_ipv4_frames launch per batch (single; mixed: the rx "
-                         "batch only)")
+                         "(multi; udp1500's default) or one sccsum_ipv4_frames launch per batch (single; mixed: "
+                         "the rx batch only, mixed's default — its multi step measured 1-2 %% slower on three "
+                         "boxes, DESIGN.md §5.3)")
     ap.add_argument("--rx-out2", action="store_true",
                     help="udp1500 / mixed: the verify (rx) half also writes both checksums per frame (default: status "
                          "bits only, what the reference's verify keeps: ip.cc:121-127, tcp.hh:876-883)")
@@ -370,6 +371,7 @@ def read_ceiling(data, nbytes, stream, reps=10):
 
 def run_udp1500(args, world, rank, dev):
     n = args.packets
+    args.launch = args.launch or "multi"
     # R distinct tx/rx batch pairs launched in turn: 2R x 1.5 GB per rank, so no
     # launch finds its batch's lines left in the 256 MB MALL by an earlier one
     # (a replay of one resident batch would measure cache reuse, not streaming)
@@ -495,16 +497,16 @@ def run_tcp64k(args, world, rank, dev):
 
 def run_mixed(args, world, rank, dev):
     """cfg 3: Zipf(1.2) frame lengths 64..9000 B, contiguous packing (odd
-    offsets), ~1.5 GB per batch, IPv4 + UDP checksums per frame.  Like cfg 2,
-    a step is both directions of the traffic: generate over a tx batch
-    (checksum fields zero) and verify over an rx batch (its own Zipf draw,
-    checksums stored in place by sccsum_ipv4_fill) — one
-    sccsum_ipv4_frames_multi launch (--launch multi, default), or one
-    sccsum_ipv4_frames launch over the rx batch alone (--launch single)."""
+    offsets), ~1.5 GB per batch, IPv4 + UDP checksums per frame.  A step is
+    one sccsum_ipv4_frames launch over an rx batch (checksums stored in place
+    by sccsum_ipv4_fill; --launch single, the default), or, like cfg 2, both
+    directions in one sccsum_ipv4_frames_multi launch: generate over a tx
+    batch (checksum fields zero) plus verify-only over the rx batch (its own
+    Zipf draw) (--launch multi; 1-2 % slower on three boxes)."""
     from seastar_amd import synth
 
     n = args.packets if args.packets != (1 << 20) else 3_400_000
-    multi = args.launch == "multi"
+    multi = (args.launch or "single") == "multi"
     lens = synth.zipf_lengths(n, seed=SEED + rank)
     lens_rx = synth.zipf_lengths(n, seed=SEED + 7717 + rank) if multi else lens
     R = max(1, args.rotate)  # distinct batches launched in turn (no cached-line replay)

@@ -793,6 +793,8 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
                     chunk(g + C, vb);
                 }
             } else {
+                // (a run's last chunk cut to the rows its units reach, U / 4 or
+                // U / 2, measured the same: profiles/r02_ab_short_chunks.log)
                 for (uint32_t g = 0; g < ext; g += C) {
                     u32x4 v[U];
                     load(r, g, v);
@@ -926,13 +928,20 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
         uint16_t* const out = Q.out[cur.q];
         uint8_t* const status = Q.status[cur.q];
         if (mine) {
+            // the policy applies to an array whose tile part spans >= 128 B
+            // (two lines); a smaller part is stored plain, so that the L2
+            // merges it with its neighbour tiles' parts into whole lines
+            // (nt parts of a line leave as separate partial writes: cfg 4's
+            // 1-segment tiles wrote 107 B per segment and ran 8 % slower)
             const uint32_t pol = (flags >> kOutPolicyShift) & 7u;
+            const uint32_t pol_out = B * (IPV4 ? 4u : 2u) >= 128u ? pol : 0u;
+            const uint32_t pol_st = B >= 128u ? pol : 0u;
             if (IPV4) {
-                if (out) tile_store(reinterpret_cast<uint32_t*>(out) + base, lane, word, pol);
+                if (out) tile_store(reinterpret_cast<uint32_t*>(out) + base, lane, word, pol_out);
             } else {
-                tile_store(out + base, lane, static_cast<uint16_t>(word), pol);
+                tile_store(out + base, lane, static_cast<uint16_t>(word), pol_out);
             }
-            if (status) tile_store(status + base, lane, static_cast<uint8_t>(st), pol);
+            if (status) tile_store(status + base, lane, static_cast<uint8_t>(st), pol_st);
         }
         t = t1;
         t1 = t2;
