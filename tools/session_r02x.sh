@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 GPU session (final tree: nt result stores, verify-only rx halves, cfg 3 tx + rx step): parity tests, every bench config, and for udp1500 /
+# Round-2 GPU session (final tree: nt result stores, verify-only rx halves): parity tests, every bench config, and for udp1500 /
 # mixed / fill / tcp64k a kernel trace plus separate FETCH_SIZE and WRITE_SIZE
 # passes, cut to the timed dispatches by tools/prof_timed.py.
 # Each GPU step has its own time limit; steps chain with && (first failure ends it).
@@ -31,8 +31,8 @@ timeout -k 10 300 python bench.py --config sweep --no-cpu > $O/bench_sweep.log 2
 timeout -k 10 300 python bench.py --config e2e --steps 5 --no-cpu > $O/bench_e2e.log 2>&1 && echo "e2e ok" >> $O/steps.log && \
 timeout -k 10 300 python bench.py --steps 20 --no-cpu --rx-out2 > $O/ab_rx_out2.log 2>&1 && \
 timeout -k 10 300 python bench.py --steps 20 --no-cpu >> $O/ab_rx_out2.log 2>&1 && \
-timeout -k 10 300 python bench.py --config mixed --steps 20 --no-cpu --rx-out2 >> $O/ab_rx_out2.log 2>&1 && \
-timeout -k 10 300 python bench.py --config mixed --steps 20 --no-cpu --launch single >> $O/ab_rx_out2.log 2>&1 && \
+timeout -k 10 300 python bench.py --config mixed --steps 20 --no-cpu --launch multi --rx-out2 >> $O/ab_rx_out2.log 2>&1 && \
+timeout -k 10 300 python bench.py --config mixed --steps 20 --no-cpu --launch multi >> $O/ab_rx_out2.log 2>&1 && \
 timeout -k 10 300 python bench.py --config mixed --steps 20 --no-cpu >> $O/ab_rx_out2.log 2>&1 && echo "ab rx_out2 ok" >> $O/steps.log && \
 timeout -k 10 300 python bench.py --config mixed --align 64 --steps 20 --no-cpu > $O/bench_mixed_align64.log 2>&1 && echo "mixed align64 ok" >> $O/steps.log && \
 PROBE_BYTES=1572864000 prof udp1500 && echo "prof udp1500 ok" >> $O/steps.log && \
