@@ -152,6 +152,10 @@ def dist_setup(dry_run=False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
+        # one node (the driver's torchrun uses --master-addr 127.0.0.1): keep gloo's control traffic on
+        # loopback rather than on whatever interface the box's hostname resolves to
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
     if dry_run:
         if world > 1:
             import torch.distributed as dist

@@ -54,3 +54,22 @@ def test_launcher_two_ranks_on_the_gpu():
                timeout=300)
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["config"]["global_batch"] == 2 * 65536
+
+
+def test_torchrun_launch_as_the_driver_runs_it():
+    """The driver's multi-GPU form: torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N; the ranks
+    come from the environment (no self-spawn) and gloo stays on loopback."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "GLOO_SOCKET_IFNAME")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+                        "--gpus", "2", "--dry-run"], capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 2
+    assert [x["rank"] for x in lines[0]["ranks"]] == [0, 1]
