@@ -88,6 +88,8 @@ public:
     }
 
     // out2[2i] = IPv4 header checksum, out2[2i+1] = TCP/UDP checksum of frame i.
+    // d_out2 may be null when d_status is given: verify only, 1 status byte
+    // written per frame (what the reference keeps of the sum, ip.cc:121-127).
     void ipv4_frames(const device_packet_batch& b, uint16_t* d_out2, uint8_t* d_status, void* stream) const {
         check(sccsum_ipv4_frames(b.bytes, b.bytes_len, b.off, b.len, d_out2, d_status, b.n, b.max_len, stream),
               "sccsum_ipv4_frames");

@@ -37,6 +37,9 @@ int main() {
                         static_cast<uint16_t*>(d16), nullptr, 3, 0, nullptr) == SCCSUM_EINVAL);
     EXPECT(sccsum_ipv4_frames(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16),
                               static_cast<uint16_t*>(odd), nullptr, 3, 0, nullptr) == SCCSUM_EINVAL);
+    // frames: neither d_out2 nor d_status (a verify-only launch needs the status array)
+    EXPECT(sccsum_ipv4_frames(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr,
+                              nullptr, 3, 0, nullptr) == SCCSUM_EINVAL);
     EXPECT(sccsum_fragments(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), 4,
                             static_cast<const uint32_t*>(d16), nullptr, static_cast<uint16_t*>(d16), nullptr, 2, 0,
                             nullptr, nullptr) == SCCSUM_EINVAL);
