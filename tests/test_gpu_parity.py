@@ -801,6 +801,44 @@ def test_verify_only_frames(dev, kernel_variant):
     assert rc == native.SCCSUM_EINVAL
 
 
+@pytest.mark.parametrize("bpc,tile_packets", [(8, 64), (1, 5), (3, 1)])
+def test_static_tile_order_matches_oracle(dev, kernel_variant, bpc, tile_packets):
+    """Static round-robin tiles (no dequeue counters: what a graph capture or a
+    stream past the slot cap gets) change only the schedule: frames, a
+    multi-queue launch and spans match the oracle on grids of 1-8 blocks per CU."""
+    if kernel_variant not in (15, 16):
+        pytest.skip("tile orders exercised on the default flat forms")
+    lib = native.load()
+    native.check(lib.sccsum_set_dynamic_tiles(0), "dynamic")
+    native.check(lib.sccsum_set_blocks_per_cu(bpc), "blocks_per_cu")
+    native.check(lib.sccsum_set_tile_packets(tile_packets), "tile_packets")
+    try:
+        buf, off, lens, _ = synth.mixed_udp_frames(20000, seed=700 + bpc, max_gap=3)
+        got, st = _frames(dev, buf, off, lens)
+        want, want_st = oracle.batch_ipv4(buf, off, lens)
+        assert np.array_equal(got, want) and np.array_equal(st, want_st)
+        items, wants = [], []
+        for q, n in enumerate([5000, 3, 12000]):
+            buf, off, lens, _ = synth.mixed_udp_frames(n, seed=710 + q, max_gap=1)
+            items.append((batch.PacketBatch.from_host(buf, off, lens, device=dev), None,
+                          torch.empty(n, dtype=torch.uint8, device=dev)))
+            wants.append(oracle.batch_ipv4(buf, off, lens))
+        outs = batch.ipv4_frames_multi(items)
+        torch.cuda.synchronize()
+        for o, it, (w, wst) in zip(outs, items, wants):
+            assert np.array_equal(batch.as_u16(o).reshape(-1, 2), w)
+            assert np.array_equal(it[2].cpu().numpy(), wst)
+        rng = np.random.default_rng(720)
+        lens = rng.integers(0, 5000, 30000).astype(np.uint32)
+        off, total = synth.pack(lens, seed=721, max_gap=2)
+        buf = rng.integers(0, 256, size=int(total), dtype=np.uint8)
+        assert np.array_equal(_spans(dev, buf, off, lens), oracle.batch_spans(buf, off, lens))
+    finally:
+        native.check(lib.sccsum_set_dynamic_tiles(1), "dynamic")
+        native.check(lib.sccsum_set_blocks_per_cu(8), "blocks_per_cu")
+        native.check(lib.sccsum_set_tile_packets(64), "tile_packets")
+
+
 @pytest.mark.parametrize("policy", [0, 1, 2, 3, 4])
 def test_out_policies_match_oracle(dev, kernel_variant, policy):
     """The result stores' cache policy (sccsum_set_out_policy; nt by default)
