@@ -55,6 +55,11 @@ int sccsum_set_tail_split(int split, int quarters);
  * 4 = sc0).  SCCSUM_EINVAL outside 0..4. */
 int sccsum_set_out_policy(int policy);
 
+/* Flat kernel forms without a chunk in flight (U 8 form 14, U 16): a run's
+ * last chunk loads and scans only the rows its units reach, U / 8 .. U (1, the
+ * default), or always U rows (0).  SCCSUM_EINVAL otherwise. */
+int sccsum_set_short_chunks(int on);
+
 /* Stream-read `bytes` (multiple of 16) from d_src with the same
  * load width as the checksum kernels and write one 64-bit word per workgroup
  * to d_sink (capacity >= sccsum_read_probe_blocks()).  Used by bench.py as

@@ -46,6 +46,7 @@ constexpr int kMaxDevices = 64;
 constexpr uint32_t kFlagRaw = 1;     // spans: output the folded span-relative sum (no seed, no complement)
 constexpr uint32_t kFlagFillL4 = 2;  // frames: generate the TCP/UDP checksum and store it in the frame
 constexpr uint32_t kFlagFillIp = 4;  // frames (with kFlagFillL4): also generate + store the IPv4 header checksum
+constexpr uint32_t kFlagFullChunks = 16;  // flat kernel: a run's last chunk loads all U rows (diagnostic A/B)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -573,6 +574,7 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
     constexpr uint32_t C = kWave * U;  // units per chunk
     constexpr uint32_t kLdsUnits = C;
     constexpr int kHead = FILL ? 4 : (IPV4 ? 3 : 1);
+    const bool short_chunks = (flags & kFlagFullChunks) == 0;
     const bool raw = !IPV4 && (flags & kFlagRaw);
     const bool fill_ip = FILL && (flags & kFlagFillIp);
     __shared__ u32x4 ubuf_all[kWavesPerBlock][kLdsUnits];
@@ -717,9 +719,11 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
         return rn;
     };
     auto run_rsrc = [&](const Run& rn) { return rsrc(reinterpret_cast<const uint8_t*>(rn.F << 4), 16u * rn.ext); };
-    auto load = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t g, u32x4 (&v)[U]) {
+    // a chunk's loads: R <= U rows of 64 units
+    auto load = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t g, auto& v) {
+        constexpr int R = std::extent<std::remove_reference_t<decltype(v)>>::value;
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < R; ++u)
             v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(16u * g + vo + 1024u * u), 0, kNT);
     };
 
@@ -752,32 +756,34 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
             const int rf = cap ? static_cast<int>(static_cast<uint32_t>(cur.fu - F)) : -0x40000000;
             const int rl = cap ? static_cast<int>(static_cast<uint32_t>(cur.lu - F)) : -0x40000000;
             uint32_t carry = 0;
-            // one chunk = U rows of 64 units: unit sums, scanned, parked in
-            // LDS with the units; packet lanes pick up what falls in it
-            auto chunk = [&](uint32_t g, const u32x4 (&v)[U]) {
-                uint32_t x[U];
+            // one chunk = R <= U rows of 64 units: unit sums, scanned, parked
+            // in LDS with the units; packet lanes pick up what falls in it
+            auto chunk = [&](uint32_t g, const auto& v) {
+                constexpr int R = std::extent<std::remove_reference_t<decltype(v)>>::value;
+                constexpr uint32_t CR = kWave * R;  // units in this chunk
+                uint32_t x[R];
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[u] = sad4(v[u], 0u);
-                wave_scan_n<U>(x);
+                for (int u = 0; u < R; ++u) x[u] = sad4(v[u], 0u);
+                wave_scan_n<R>(x);
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
+                for (int u = 0; u < R; ++u) {
                     pbuf[kWave * u + lane] = carry + x[u];
                     ubuf[kWave * u + lane] = v[u];
                     carry += __builtin_amdgcn_readlane(x[u], 63);
                 }
                 __builtin_amdgcn_wave_barrier();
                 const int a = rf - static_cast<int>(g);
-                if (static_cast<uint32_t>(a) < C) {
+                if (static_cast<uint32_t>(a) < CR) {
                     const u32x4 w = ubuf[a];
                     pst = pbuf[a] - sad4(w, 0u);  // prefix just before the first unit
                     hs[0] = w;
                 }
 #pragma unroll
                 for (int j = 1; j < kHead; ++j) {
-                    if (static_cast<uint32_t>(a + j) < C) hs[j] = ubuf[a + j];
+                    if (static_cast<uint32_t>(a + j) < CR) hs[j] = ubuf[a + j];
                 }
                 const int b = rl - static_cast<int>(g);
-                if (static_cast<uint32_t>(b) < C) {
+                if (static_cast<uint32_t>(b) < CR) {
                     pend = pbuf[b];
                     hl = ubuf[b];
                 }
@@ -793,12 +799,29 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
                     chunk(g + C, vb);
                 }
             } else {
-                // (a run's last chunk cut to the rows its units reach, U / 4 or
-                // U / 2, measured the same: profiles/r02_ab_short_chunks.log)
+                // a run's last chunk loads and scans only the rows its units
+                // reach (U / 8 .. U): a run of one 1500 B frame in an mbuf slot
+                // is 2 rows, not 16 (packed layouts: no change,
+                // profiles/r02_ab_short_chunks.log)
                 for (uint32_t g = 0; g < ext; g += C) {
-                    u32x4 v[U];
-                    load(r, g, v);
-                    chunk(g, v);
+                    const uint32_t left = ext - g;
+                    if (!short_chunks || left > C / 2) {
+                        u32x4 v[U];
+                        load(r, g, v);
+                        chunk(g, v);
+                    } else if (left > C / 4) {
+                        u32x4 v[U / 2];
+                        load(r, g, v);
+                        chunk(g, v);
+                    } else if (U < 8 || left > C / 8) {
+                        u32x4 v[U / 4];
+                        load(r, g, v);
+                        chunk(g, v);
+                    } else {
+                        u32x4 v[U >= 8 ? U / 8 : 1];
+                        load(r, g, v);
+                        chunk(g, v);
+                    }
                 }
             }
         }
@@ -1161,6 +1184,7 @@ struct Knobs {
     int tail_split = kTailSplit;     // flat kernel: sub-tiles per tail tile (1, 2, 4 or 8; 1 = no split)
     int tail_quarters = kTailQuarters;  // flat kernel: tail = tail_quarters / 4 whole tiles per wave of the grid
     int out_policy = kOutPolicy;     // flat kernel: cache policy of the result stores (tile_store)
+    int short_chunks = 1;            // flat kernel (no chunk in flight): a run's last chunk covers only its rows
 };
 thread_local Knobs t_knobs;
 
@@ -1328,6 +1352,7 @@ void launch_flat(FlatKernel kern, hipStream_t s, Queues& Q, uint64_t n_total, ui
     blocks = (blocks + 15) & ~uint64_t(15);  // multiple of 16: XCD mapping, waves divide into kGroups
     uint32_t* heads = K.dynamic ? heads_for(s) : nullptr;
     flags |= static_cast<uint32_t>(K.out_policy) << kOutPolicyShift;
+    if (!K.short_chunks) flags |= kFlagFullChunks;
     kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(Q, static_cast<uint32_t>(B), heads, flags, rss);
 }
 
@@ -1396,10 +1421,20 @@ bool batch_ok(const void* d_bytes, const uint64_t* d_off, const uint32_t* d_len,
 // chunk for big launches (>= 512 Ki packets and 256 MiB), else 8 units with
 // the next chunk in flight: the 16-unit form runs 2 waves per SIMD, too few
 // tiles per wave on smaller launches (DESIGN.md §5.1 has the A/B)
-int pick_variant(uint64_t n_total, uint64_t bytes_total, uint32_t flags) {
+//
+// Sparse layouts go to the one-wave-per-packet kernel: when the buffer holds
+// at least max_len + 64 bytes per packet, the mean gap between packets is over
+// 4 units, each packet is its own run and a flat-kernel wave waits out one
+// round trip per packet, one after another.  1500 B frames in 2304 B mbuf
+// slots (data at +256): flat 537 us per 1 M frames (920 without short
+// chunks), one wave per packet 359 us (profiles/r02_ab_slots.log).
+int pick_variant(uint64_t n_total, uint64_t bytes_total, uint32_t flags, uint32_t max_len) {
     int variant = t_knobs.variant;
     const int dflt = (n_total >= (512u << 10) && bytes_total >= (256ull << 20)) ? 16 : 15;
-    if (variant == 0 || (variant == 1 && (flags & kFlagFillL4))) variant = dflt;  // in-place write-back: flat only
+    const bool fill = (flags & kFlagFillL4) != 0;
+    const bool sparse = max_len != 0 && n_total != 0 && bytes_total / n_total >= uint64_t(max_len) + 64u;
+    if (variant == 0 && sparse && !fill) return 1;
+    if (variant == 0 || (variant == 1 && fill)) variant = dflt;  // in-place write-back: flat only
     return variant;
 }
 
@@ -1409,7 +1444,7 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
            void* stream, uint32_t flags = 0, const RssParams& rss = kNoRss) {
     if (n == 0) return SCCSUM_OK;
     if (!batch_ok<IPV4>(d_bytes, d_off, d_len, d_seed, d_out, d_status, flags)) return SCCSUM_EINVAL;
-    const int variant = pick_variant(n, bytes_len, flags);
+    const int variant = pick_variant(n, bytes_len, flags, max_len);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
     if (variant == 1) {
@@ -1449,7 +1484,7 @@ int launch_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
         bytes_total += x.n ? x.bytes_len : 0;
     }
     if (n_total == 0) return SCCSUM_OK;
-    const int variant = pick_variant(n_total, bytes_total, 0);
+    const int variant = pick_variant(n_total, bytes_total, 0, max_len);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     if (variant == 1) {  // the simple kernel takes one batch per launch
         for (uint32_t i = 0; i < nbatch; ++i) {
@@ -1932,6 +1967,12 @@ int sccsum_set_dynamic_tiles(int on) {
 int sccsum_set_out_policy(int policy) {
     if (policy < 0 || policy > 4) return SCCSUM_EINVAL;
     sccsum::t_knobs.out_policy = policy;
+    return SCCSUM_OK;
+}
+
+int sccsum_set_short_chunks(int on) {
+    if (on != 0 && on != 1) return SCCSUM_EINVAL;
+    sccsum::t_knobs.short_chunks = on;
     return SCCSUM_OK;
 }
 

@@ -801,6 +801,33 @@ def test_verify_only_frames(dev, kernel_variant):
     assert rc == native.SCCSUM_EINVAL
 
 
+@pytest.mark.parametrize("short", [1, 0])
+def test_slot_layout_one_run_per_packet(dev, kernel_variant, short):
+    """Packets in 4 KiB slots at every start alignment (mbuf-like: every
+    packet its own run): lengths 0..3071 give runs of 1..193 units, so a
+    run's one chunk is cut to 2, 4, 8 or 16 rows (short chunks, the default)
+    or always full; spans and frames against the oracle."""
+    lib = native.load()
+    native.check(lib.sccsum_set_short_chunks(short), "short_chunks")
+    try:
+        rng = np.random.default_rng(800 + short)
+        lens = np.arange(0, 3072, dtype=np.uint32)
+        off = (np.arange(lens.size, dtype=np.uint64) * 4096 + 256 + (np.arange(lens.size) % 16)).astype(np.uint64)
+        buf = rng.integers(0, 256, size=lens.size * 4096 + 64, dtype=np.uint8)
+        seeds = rng.integers(0, 65536, lens.size).astype(np.uint32)
+        assert np.array_equal(_spans(dev, buf, off, lens, seeds), oracle.batch_spans(buf, off, lens, seeds))
+        fl = np.maximum(lens, 20).astype(np.uint32)
+        fbuf = buf.copy()
+        for i in range(fl.size):  # IPv4/UDP headers, ip_len = frame length
+            o, L = int(off[i]), int(fl[i])
+            fbuf[o], fbuf[o + 2], fbuf[o + 3], fbuf[o + 9] = 0x45, L >> 8, L & 0xFF, 17
+        got, st = _frames(dev, fbuf, off, fl)
+        want, want_st = oracle.batch_ipv4(fbuf, off, fl)
+        assert np.array_equal(got, want) and np.array_equal(st, want_st)
+    finally:
+        native.check(lib.sccsum_set_short_chunks(1), "short_chunks")
+
+
 @pytest.mark.parametrize("bpc,tile_packets", [(8, 64), (1, 5), (3, 1)])
 def test_static_tile_order_matches_oracle(dev, kernel_variant, bpc, tile_packets):
     """Static round-robin tiles (no dequeue counters: what a graph capture or a

@@ -55,13 +55,25 @@ def cases(dev):
                            length=torch.full((n64,), 65536, dtype=torch.int32, device=dev),
                            bytes_len=n64 * 65536, max_len=65536)
     yield "tcp64k_spans", lb, "spans", n64 * (65536 + 14)
+    if "udp1500_slots" in CASES:  # frames where a NIC would DMA them: DPDK mbuf slots (2304 B, data at +256)
+        del lb, seg
+        torch.cuda.empty_cache()
+        ns = 1 << 20
+        fr = devsynth.udp_frames(ns, 1500, seed=8, device=dev)
+        slots = torch.zeros(ns * 2304 + 16, dtype=torch.uint8, device=dev)
+        slots[: ns * 2304].view(ns, 2304)[:, 256:1756] = fr.data[: ns * 1500].view(ns, 1500)
+        sb = batch.PacketBatch(data=slots, off=torch.arange(ns, device=dev, dtype=torch.int64) * 2304 + 256,
+                               length=torch.full((ns,), 1500, dtype=torch.int32, device=dev),
+                               bytes_len=ns * 2304, max_len=1500)
+        del fr
+        yield "udp1500_slots", sb, "frames", ns * (1500 + 12 + 4)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn[:tile_bytes[:tail_split[:tail_quarters[:out_policy]]]]]]]]")
+    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn[:tile_bytes[:tail_split[:tail_quarters[:out_policy[:short_chunks]]]]]]]]]")
     ap.add_argument("--rotate", type=int, default=4, help="distinct copies of each batch, launched in turn")
     ap.add_argument("--cases", default="udp1500_frames,udp1500_spans,udp1500_frames_rss,zipf_spans,cfg3_zipf_frames,"
                                        "tcp64k_spans")
@@ -82,7 +94,7 @@ def main():
         turn = [0]
 
         def knobs(v):
-            parts = (v.split(":") + [""] * 9)[:9]
+            parts = (v.split(":") + [""] * 10)[:10]
             native.check(lib.sccsum_set_kernel_variant(int(parts[0])), "variant")
             native.check(lib.sccsum_set_blocks_per_cu(int(parts[1] or 8)), "blocks_per_cu")
             native.check(lib.sccsum_set_group_units(int(parts[2] or 0)), "group_units")
@@ -91,6 +103,7 @@ def main():
             native.check(lib.sccsum_set_tile_bytes(int(parts[5] or 49152)), "tile_bytes")
             native.check(lib.sccsum_set_tail_split(int(parts[6] or 1), int(parts[7] or 4)), "tail_split")
             native.check(lib.sccsum_set_out_policy(int(parts[8] or 1)), "out_policy")
+            native.check(lib.sccsum_set_short_chunks(int(parts[9] or 1)), "short_chunks")
 
         def run(bb):
             if mode == "frames":
@@ -138,6 +151,7 @@ def main():
     native.check(lib.sccsum_set_tile_bytes(49152), "tile_bytes")
     native.check(lib.sccsum_set_tail_split(1, 4), "tail_split")
     native.check(lib.sccsum_set_out_policy(1), "out_policy")
+    native.check(lib.sccsum_set_short_chunks(1), "short_chunks")
 
 
 if __name__ == "__main__":
