@@ -16,10 +16,13 @@ extern "C" {
 #endif
 
 /* Kernel family for this thread's later launches.
- * 0 = default: flat kernel, form 16 (>= 512 Ki packets and >= 256 MiB) else 15.
+ * 0 = default: flat kernel, form 16 (>= 512 Ki packets and >= 256 MiB) else 15;
+ *     variant 2 for sparse layouts (bytes_len / n >= max_len + 64).
  * 1 = one packet per wave, per-lane byte masks (an independent second
  *     implementation kept for cross-checking; in-place fill uses the flat
  *     kernel whatever the variant).
+ * 2 = one packet per 16-lane row, four packets per wave at a time (sparse
+ *     layouts: packets far apart, e.g. in mbuf slots).
  * 14-16 = flat kernel forms: each tile's byte extent streamed densely, unit
  *     sums prefix-scanned across the wave; U = 8 (14, 15: the next chunk in
  *     flight) or 16 (16) units per lane per chunk.  (The U = 2 / 4 forms and

@@ -272,6 +272,127 @@ __global__ __launch_bounds__(kBlock) void csum_kernel(
     }
 }
 
+// Sum of v over each 16-lane row, in every lane of the row (the first four
+// steps of wave_sum).  All lanes of a row must be active.
+__device__ __forceinline__ uint32_t row_sum(uint32_t v) {
+    v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xF, 0xF, false));
+    v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4E, 0xF, 0xF, false));
+    v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x124, 0xF, 0xF, false));
+    v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x128, 0xF, 0xF, false));
+    return v;
+}
+
+// Lane k of each 16-lane row, broadcast to the whole row (DPP row_newbcast).
+template <int K>
+__device__ __forceinline__ uint32_t row_bcast(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x150 + K, 0xF, 0xF, false));
+}
+
+// One packet per 16-lane ROW (four packets per wave at a time): for sparse
+// layouts, where every packet is its own run (DPDK mbuf slots a NIC wrote
+// into HBM: 1500 B of every 2304).  Each lane loads V 16-byte units, so one
+// load instruction covers four packets and a wave keeps four packets' round
+// trips in flight together; the row's sum is four DPP steps.  Same arithmetic
+// and outputs as csum_kernel (frame mode: the IPv4 header from the row's first
+// dwords, broadcast with row_newbcast; L4 range and pseudo-header as
+// frame_header).  Packets longer than 16 V units loop over groups.
+template <int V, bool IPV4>
+__global__ __launch_bounds__(kBlock) void csum_row_kernel(
+    const uint8_t* __restrict__ bytes, uint64_t bytes_len,
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
+    const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
+    uint8_t* __restrict__ status, uint64_t n, uint32_t flags) {
+    constexpr uint32_t kRow = 16;
+    constexpr uint32_t kRowsPerBlock = kBlock / kRow;
+    const bool raw = !IPV4 && (flags & kFlagRaw);
+    const uint32_t r = threadIdx.x & (kRow - 1);
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kRowsPerBlock;
+    for (uint64_t p = static_cast<uint64_t>(xcd_block_id()) * kRowsPerBlock + threadIdx.x / kRow; p < n;
+         p += stride) {
+        const uint64_t o = off[p];
+        const uint32_t L = len[p];
+        if (o > bytes_len || L > bytes_len - o || (IPV4 && L < 20)) {
+            if (r == 0) {
+                if (IPV4) {
+                    if (out) reinterpret_cast<uint32_t*>(out)[p] = 0;
+                } else {
+                    out[p] = 0;
+                }
+                if (status) {
+                    status[p] = (o > bytes_len || L > bytes_len - o) ? SCCSUM_ST_RANGE : SCCSUM_ST_MALFORMED;
+                }
+            }
+            continue;
+        }
+        const uint8_t* ptr = bytes + o;
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(ptr);
+        const int head = static_cast<int>(addr & 15u);
+        const uint8_t* a0 = ptr - head;
+        const uint32_t nunits = L ? (static_cast<uint32_t>(head) + L + 15u) >> 4 : 0u;
+        // frame mode: header dwords re-aligned to the packet start (row lanes
+        // 0..5 load the covering dwords, as span_packet)
+        uint32_t hv = 0;
+        const int sh = static_cast<int>(addr & 3u);
+        if (IPV4 && (r < 5 || (r == 5 && sh != 0))) hv = *reinterpret_cast<const uint32_t*>(ptr - sh + 4 * r);
+        u32x4 v[V];
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+            const uint32_t c = static_cast<uint32_t>(u) * kRow + r;
+            v[u] = c < nunits ? load_unit(a0 + 16u * c) : u32x4{0, 0, 0, 0};
+        }
+        int rs = head, re = head + static_cast<int>(L);
+        uint32_t ipc = 0, pseudo = 0;
+        uint8_t st = 0;
+        if (IPV4) {
+            const uint32_t nxt = static_cast<uint32_t>(
+                __builtin_amdgcn_update_dpp(0, static_cast<int>(hv), 0x101, 0xF, 0xF, false));  // row_shl:1
+            const uint32_t al = __builtin_amdgcn_alignbyte(nxt, hv, static_cast<uint32_t>(sh));
+            const FrameHeader F = frame_header(row_bcast<0>(al), row_bcast<1>(al), row_bcast<2>(al),
+                                               row_bcast<3>(al), row_bcast<4>(al), L);
+            ipc = F.ipc;
+            st = F.st;
+            pseudo = F.pseudo;
+            rs = head + static_cast<int>(F.l4_off);
+            re = rs + static_cast<int>(F.l4_len);
+        }
+        uint64_t acc = 0;
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+            const int c16 = 16 * static_cast<int>(static_cast<uint32_t>(u) * kRow + r);
+            acc += unit_sum(v[u], rs - c16, re - c16);
+        }
+        for (uint32_t g = V * kRow; g < nunits; g += V * kRow) {
+#pragma unroll
+            for (int u = 0; u < V; ++u) {
+                const uint32_t c = g + static_cast<uint32_t>(u) * kRow + r;
+                v[u] = c < nunits ? load_unit(a0 + 16u * c) : u32x4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < V; ++u) {
+                const int c16 = 16 * static_cast<int>(g + static_cast<uint32_t>(u) * kRow + r);
+                acc += unit_sum(v[u], rs - c16, re - c16);
+            }
+        }
+        uint32_t S = fold16(row_sum(fold16(acc)));
+        if (addr & 1u) S = swap16(S);
+        if (IPV4) {
+            S = fold16(static_cast<uint64_t>(S) + pseudo);
+        } else if (seed && !raw) {
+            S = fold16(static_cast<uint64_t>(S) + swap16(fold16(seed[p])));
+        }
+        const uint32_t res = raw ? S : ~S & 0xffffu;
+        if (r == 0) {
+            if (IPV4) {
+                if (out) reinterpret_cast<uint32_t*>(out)[p] = ipc | (res << 16);
+                if (status) status[p] = st | (ipc == 0 ? SCCSUM_ST_OK : 0u) | (res == 0 ? SCCSUM_ST_L4_OK : 0u);
+            } else {
+                out[p] = static_cast<uint16_t>(res);
+                if (status) status[p] = (!raw && res == 0) ? SCCSUM_ST_OK : 0u;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- flat-kernel helpers
 
 // Keep bytes [lo, hi) of a 64-bit half unit (half-relative byte indices).
@@ -1369,6 +1490,27 @@ void launch_simple(int uc, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
     }
 }
 
+template <bool IPV4>
+void launch_rows(uint32_t max_len, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
+                 const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
+                 uint32_t flags) {
+    const uint64_t units = max_len ? (static_cast<uint64_t>(max_len) + 30u) / 16u : 128u;  // worst-case head of 15
+    const uint64_t cap = static_cast<uint64_t>(cu_count()) * t_knobs.blocks_per_cu;
+    uint64_t blocks = (n + 15u) / 16u;  // 16 rows (packets at a time) per block
+    blocks = blocks < cap ? blocks : cap;
+    blocks = (blocks + 7u) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
+    const dim3 g(static_cast<unsigned>(blocks)), t(kBlock);
+    if (units <= 32) {
+        csum_row_kernel<2, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+    } else if (units <= 64) {
+        csum_row_kernel<4, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+    } else if (units <= 96) {  // 1500 B frames: 95 units
+        csum_row_kernel<6, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+    } else {
+        csum_row_kernel<8, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+    }
+}
+
 // Flat-kernel forms: 14 / 15 = U 8 (15: the next chunk in flight), 16 = U 16.
 // (U 2 / 4 forms and rolling rows lost their A/Bs in rounds 1-2 and were
 // removed: profiles/r01_ab_variants.log, r02_ab_roll.log.)  Frames may fill
@@ -1422,19 +1564,20 @@ bool batch_ok(const void* d_bytes, const uint64_t* d_off, const uint32_t* d_len,
 // the next chunk in flight: the 16-unit form runs 2 waves per SIMD, too few
 // tiles per wave on smaller launches (DESIGN.md §5.1 has the A/B)
 //
-// Sparse layouts go to the one-wave-per-packet kernel: when the buffer holds
-// at least max_len + 64 bytes per packet, the mean gap between packets is over
-// 4 units, each packet is its own run and a flat-kernel wave waits out one
-// round trip per packet, one after another.  1500 B frames in 2304 B mbuf
-// slots (data at +256): flat 537 us per 1 M frames (920 without short
-// chunks), one wave per packet 359 us (profiles/r02_ab_slots.log).
+// Sparse layouts go to the row kernel (one packet per 16-lane row): when the
+// buffer holds at least max_len + 64 bytes per packet, the mean gap between
+// packets is over 4 units, each packet is its own run and a flat-kernel wave
+// waits out one round trip per packet, one after another.  1500 B frames in
+// 2304 B mbuf slots (data at +256), per 1 M frames: flat 537 us (920 without
+// short chunks), one wave per packet 359-368 us, one row per packet 253-259 us
+// (profiles/r02_ab_slots.log, r02_ab_rows.log).
 int pick_variant(uint64_t n_total, uint64_t bytes_total, uint32_t flags, uint32_t max_len) {
     int variant = t_knobs.variant;
     const int dflt = (n_total >= (512u << 10) && bytes_total >= (256ull << 20)) ? 16 : 15;
     const bool fill = (flags & kFlagFillL4) != 0;
     const bool sparse = max_len != 0 && n_total != 0 && bytes_total / n_total >= uint64_t(max_len) + 64u;
-    if (variant == 0 && sparse && !fill) return 1;
-    if (variant == 0 || (variant == 1 && fill)) variant = dflt;  // in-place write-back: flat only
+    if (variant == 0 && sparse && !fill) return 2;
+    if (variant == 0 || ((variant == 1 || variant == 2) && fill)) variant = dflt;  // in-place write-back: flat only
     return variant;
 }
 
@@ -1447,8 +1590,13 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
     const int variant = pick_variant(n, bytes_len, flags, max_len);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
-    if (variant == 1) {
-        launch_simple<IPV4>(units_class(max_len), s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+    if (variant == 1 || variant == 2) {
+        if (variant == 1) {
+            launch_simple<IPV4>(units_class(max_len), s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n,
+                                flags);
+        } else {
+            launch_rows<IPV4>(max_len, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+        }
         if (IPV4 && rss.hash != nullptr) {  // RSS is fused only in the flat kernel
             rss_kernel<<<dim3(static_cast<unsigned>((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s>>>(
                 b, bytes_len, d_off, d_len, nullptr, n, rss);
@@ -1486,12 +1634,16 @@ int launch_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
     if (n_total == 0) return SCCSUM_OK;
     const int variant = pick_variant(n_total, bytes_total, 0, max_len);
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    if (variant == 1) {  // the simple kernel takes one batch per launch
+    if (variant == 1 || variant == 2) {  // the per-packet kernels take one batch per launch
         for (uint32_t i = 0; i < nbatch; ++i) {
             const sccsum_batch& x = batches[i];
-            if (x.n) {
+            if (!x.n) continue;
+            if (variant == 1) {
                 launch_simple<IPV4>(units_class(max_len), s, static_cast<const uint8_t*>(x.d_bytes), x.bytes_len,
                                     x.d_off, x.d_len, x.d_seed, static_cast<uint16_t*>(x.d_out), x.d_status, x.n, 0);
+            } else {
+                launch_rows<IPV4>(max_len, s, static_cast<const uint8_t*>(x.d_bytes), x.bytes_len, x.d_off, x.d_len,
+                                  x.d_seed, static_cast<uint16_t*>(x.d_out), x.d_status, x.n, 0);
             }
         }
         return static_cast<int>(hipGetLastError());
@@ -1929,7 +2081,7 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
 }
 
 int sccsum_set_kernel_variant(int variant) {
-    if (!(variant == 0 || variant == 1 || (variant >= 14 && variant <= 16))) return SCCSUM_EINVAL;
+    if (!(variant == 0 || variant == 1 || variant == 2 || (variant >= 14 && variant <= 16))) return SCCSUM_EINVAL;
     sccsum::t_knobs.variant = variant;
     return SCCSUM_OK;
 }
