@@ -68,10 +68,11 @@ def parse():
     ap.add_argument("--pmc", default=None, help="PMC summary JSON for roofline.traffic (default: newest for the config)")
     ap.add_argument("--rotate", type=int, default=4,
                     help="distinct batches (pairs for udp1500) launched in turn, so no launch replays cached lines")
-    ap.add_argument("--config", default="udp1500", choices=["udp1500", "mixed", "tcp64k", "e2e", "fill", "sweep"],
+    ap.add_argument("--config", default="udp1500", choices=["udp1500", "mixed", "tcp64k", "e2e", "fill", "sweep", "slots"],
                     help="udp1500 = the metric's config (cfg 2, default); mixed = cfg 3; tcp64k = cfg 4 "
                          "(per-GPU shard); e2e = cfg 5 (pinned host mbufs, PCIe-inclusive); fill = cfg 2 tx "
-                         "generate with in-place write-back (sccsum_ipv4_fill); sweep = rate against batch size")
+                         "generate with in-place write-back (sccsum_ipv4_fill); sweep = rate against batch size; "
+                         "slots = cfg 2 frames in DPDK-mbuf-shaped slots in HBM (a sparse layout)")
     ap.add_argument("--tile-bytes", type=int, default=None, help="A/B: flat-kernel tile target (sccsum_diag.h)")
     ap.add_argument("--seg-len", type=int, default=65536, help="tcp64k: segment bytes (65536, or 65535: odd offsets)")
     ap.add_argument("--align", type=int, default=1, help="mixed: frame start alignment (1 = packed, SURVEY §8(d) (i); "
@@ -576,6 +577,55 @@ def run_mixed(args, world, rank, dev):
                       {"measured_read_ceiling_GBps": round(ceiling, 1)}))
 
 
+def run_slots(args, world, rank, dev):
+    """cfg 2's 1500 B frames where a NIC DMAs them: one per DPDK-mbuf-shaped
+    slot in HBM (2304 B: 128 B rte_mbuf + 128 B headroom + 2048 B data room,
+    frame at +256, src/net/dpdk.cc:139-156) — the device-resident form of
+    cfg 5's pool.  A sparse layout (each frame its own run), which the library
+    hands to the row kernel.  Step = verify over one batch of
+    1 M slots, R rotated batches."""
+    n = args.packets
+    R = max(1, args.rotate)
+    slot, data_off = 2304, 256
+    bs = []
+    for r in range(R):
+        fr = devsynth.udp_frames(n, FRAME, seed=SEED + 17 * rank + 3 * r, device=dev)
+        first = batch.ipv4_frames(fr)
+        fr = devsynth.store_checksums(fr, first)
+        slots = torch.zeros(n * slot + 16, dtype=torch.uint8, device=dev)
+        slots[: n * slot].view(n, slot)[:, data_off:data_off + FRAME] = fr.data[: n * FRAME].view(n, FRAME)
+        del fr, first
+        bs.append(batch.PacketBatch(data=slots, off=torch.arange(n, device=dev, dtype=torch.int64) * slot + data_off,
+                                    length=torch.full((n,), FRAME, dtype=torch.int32, device=dev),
+                                    bytes_len=n * slot, max_len=FRAME))
+    LAUNCHES.add(flat_kernel(True, False, n, n * FRAME), 2 * R)  # the frames were built packed
+    torch.cuda.empty_cache()
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    for b in bs:  # every frame verifies (checksums stored before the scatter into slots)
+        batch.verify_frames(b, st)
+        torch.cuda.synchronize()
+        assert int((st != 3).sum()) == 0, "slot frames do not verify"
+    kern = "csum_row_kernel<6, true>"
+    LAUNCHES.add(kern, R)
+    stream = torch.cuda.current_stream()
+    warm = max(args.warmup, R)
+    LAUNCHES.add(kern, warm)
+    sel = LAUNCHES.select(kern, args.steps)
+    sts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(R)]
+    pre = {r: batch.prepare_call("sccsum_ipv4_frames", bs[r].data, bs[r].bytes_len, bs[r].off, bs[r].length, None,
+                                 sts[r], n, FRAME) for r in range(R)}
+    wall, launch_s = timed(lambda k: pre[k % R](stream), args.steps, warm, world, stream)
+    alg = n * (FRAME + META_BYTES + 1)  # frame bytes + metadata + 1 status byte (verify only)
+    if rank == 0:
+        emit("GiB/s device-resident Internet checksum, 1500 B frames in mbuf-shaped slots (sparse layout)",
+             world * n * FRAME * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
+             {"workload": f"{n} x 1500 B IPv4/UDP frames, one per 2304 B mbuf-shaped slot in HBM (frame at +256), "
+                          "verify only (status bits)",
+              "packets_per_gpu": n, "rotation": f"{R} distinct batches launched in turn",
+              "parallelism": f"{world} independent shards"},
+             roofline(alg, launch_s, "slots", kern + " (sccsum_ipv4_frames, sparse layout -> row kernel)", sel, args))
+
+
 def run_fill(args, world, rank, dev):
     """cfg 2 tx side with in-place write-back: IPv4 header +
     UDP checksums generated and stored into the frames (wire-ready), over R
@@ -787,7 +837,7 @@ def main():
         if args.tile_bytes is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_tile_bytes(args.tile_bytes), "sccsum_set_tile_bytes")
         {"udp1500": run_udp1500, "tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e, "fill": run_fill,
-         "sweep": run_sweep}[args.config](args, world, rank, dev)
+         "sweep": run_sweep, "slots": run_slots}[args.config](args, world, rank, dev)
     if world > 1:
         import torch.distributed as dist
 
