@@ -46,6 +46,20 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             t[r].append(e0.elapsed_time(e1) * 1e3)
+    # chains: K launches back to back inside one event pair (K = 1, 2, 4, 8), over distinct batches
+    for K in (1, 2, 4, 8):
+        tk = []
+        for _ in range(8):
+            pre[R - 1](s)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for j in range(K):
+                pre[j % R](s)
+            e1.record()
+            torch.cuda.synchronize()
+            tk.append(e0.elapsed_time(e1) * 1e3)
+        print(json.dumps({"kind": kind, "chain": K, "median_us": round(float(np.median(tk)), 1),
+                          "per_launch_us": round(float(np.median(tk)) / K, 1)}), flush=True)
     for r, b in enumerate(bs):
         print(json.dumps({"kind": kind, "batch": r, "median_us": round(float(np.median(t[r])), 1),
                           "min_us": round(float(np.min(t[r])), 1),
