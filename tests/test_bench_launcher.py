@@ -73,3 +73,23 @@ def test_torchrun_launch_as_the_driver_runs_it():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1 and lines[0]["n_gpus"] == 2
     assert [x["rank"] for x in lines[0]["ranks"]] == [0, 1]
+
+
+@pytest.mark.gpu
+def test_torchrun_two_ranks_on_the_gpu():
+    """The driver's multi-GPU command form (torch.distributed.run, loopback
+    rendezvous) with two ranks sharing the box's one GPU, through the full
+    bench: each rank builds, checks and times its own shard."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "GLOO_SOCKET_IFNAME")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--packets", "65536", "--rotate", "1",
+                        "--no-cpu"], capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and lines[0]["value"] > 0
