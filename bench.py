@@ -68,11 +68,13 @@ def parse():
     ap.add_argument("--pmc", default=None, help="PMC summary JSON for roofline.traffic (default: newest for the config)")
     ap.add_argument("--rotate", type=int, default=4,
                     help="distinct batches (pairs for udp1500) launched in turn, so no launch replays cached lines")
-    ap.add_argument("--config", default="udp1500", choices=["udp1500", "mixed", "tcp64k", "e2e", "fill", "sweep", "slots"],
+    ap.add_argument("--config", default="udp1500",
+                    choices=["udp1500", "mixed", "tcp64k", "e2e", "fill", "sweep", "slots", "frags"],
                     help="udp1500 = the metric's config (cfg 2, default); mixed = cfg 3; tcp64k = cfg 4 "
                          "(per-GPU shard); e2e = cfg 5 (pinned host mbufs, PCIe-inclusive); fill = cfg 2 tx "
                          "generate with in-place write-back (sccsum_ipv4_fill); sweep = rate against batch size; "
-                         "slots = cfg 2 frames in DPDK-mbuf-shaped slots in HBM (a sparse layout)")
+                         "slots = cfg 2 frames in DPDK-mbuf-shaped slots in HBM (a sparse layout); frags = 9000 B "
+                         "jumbo packets as 5-fragment mbuf chains in HBM (checksummer::sum(const packet&))")
     ap.add_argument("--tile-bytes", type=int, default=None, help="A/B: flat-kernel tile target (sccsum_diag.h)")
     ap.add_argument("--seg-len", type=int, default=65536, help="tcp64k: segment bytes (65536, or 65535: odd offsets)")
     ap.add_argument("--align", type=int, default=1, help="mixed: frame start alignment (1 = packed, SURVEY §8(d) (i); "
@@ -626,6 +628,84 @@ def run_slots(args, world, rank, dev):
              roofline(alg, launch_s, "slots", kern + " (sccsum_ipv4_frames, sparse layout -> row kernel)", sel, args))
 
 
+def run_frags(args, world, rank, dev):
+    """SURVEY §8(f)1 at device-resident scale: checksummer::sum(const packet&)
+    (src/net/ip_checksum.cc:64-68) over 9000 B jumbo packets held as DPDK
+    multi-segment mbuf chains (src/net/dpdk.cc:2040-2057): fragments of 2048,
+    2048, 2048, 2048 and 808 B, each in its own 2304 B mbuf slot (data room at
+    +256) in HBM, with a pseudo-header seed per packet.  Step = one
+    sccsum_fragments call (the fragments' raw sums, then their combination with
+    the odd-offset byte swap); R rotated slot pools.  Also timed: the
+    fragment-list kernel (sccsum_spans_desc) over the same fragments."""
+    n = args.packets if args.packets != (1 << 20) else 174_763  # ~1.57 GB of packet bytes
+    R = max(1, args.rotate)
+    pkt, slot, data_off = 9000, 2304, 256
+    fl = [2048, 2048, 2048, 2048, 808]
+    nf = len(fl)
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED + rank)
+    frag_len = torch.tensor(fl * n, dtype=torch.int32, device=dev)
+    frag_off = torch.arange(n * nf, device=dev, dtype=torch.int64) * slot + data_off
+    first = torch.arange(n + 1, device=dev, dtype=torch.int32) * nf
+    seeds = torch.randint(0, 65536, (n,), dtype=torch.int32, device=dev, generator=g)
+    pools = [devsynth.random_bytes(n * nf * slot + 16, g, dev) for _ in range(R)]
+    ws = torch.empty(int(native.load().sccsum_fragments_workspace(n * nf)), dtype=torch.uint8, device=dev)
+    out = torch.empty(n, dtype=torch.int16, device=dev)
+    # parity: a sample of packets gathered contiguously on the device and summed as spans
+    k = min(n, 4096)
+    want = []
+    for pool in pools:
+        got = batch.fragments(pool, n * nf * slot, frag_off, frag_len, first, seeds=seeds, max_frag_len=2048)
+        parts = [pool[i * slot + data_off:i * slot + data_off + fl[i % nf]] for i in range(k * nf)]
+        contig = batch.PacketBatch(data=torch.cat(parts + [torch.zeros(16, dtype=torch.uint8, device=dev)]),
+                                   off=torch.arange(k, device=dev, dtype=torch.int64) * pkt,
+                                   length=torch.full((k,), pkt, dtype=torch.int32, device=dev),
+                                   bytes_len=k * pkt, max_len=pkt)
+        ref = batch.spans(contig, seeds=seeds[:k])
+        torch.cuda.synchronize()
+        assert torch.equal(got[:k], ref), "fragment lists differ from the contiguous packets"
+        want.append(got.clone())
+    kern = "csum_row_kernel<8, false>"  # the raw pass over the fragments (a sparse layout)
+    LAUNCHES.add(kern, R)
+    stream = torch.cuda.current_stream()
+    pre = [batch.prepare_call("sccsum_fragments", pools[r], n * nf * slot, frag_off, frag_len, n * nf, first, seeds,
+                              out, None, n, 2048, ws) for r in range(R)]
+    warm = max(args.warmup, R)
+    LAUNCHES.add(kern, warm)
+    sel = LAUNCHES.select(kern, args.steps)
+    wall, launch_s = timed(lambda k_: pre[k_ % R](stream), args.steps, warm, world, stream)
+    # the same fragments through the fragment-list kernel (one wave per packet, fragments where they lie)
+    desc = []
+    for pool in pools:
+        src = (pool.data_ptr() + frag_off).cpu().numpy().astype(np.uint64)
+        dst = (torch.arange(n, device=dev, dtype=torch.int64).repeat_interleave(nf) * pkt +
+               torch.tensor([0, 2048, 4096, 6144, 8192] * n, device=dev)).cpu().numpy()
+        desc.append(torch.from_numpy(batch.make_desc(src, dst, np.array(fl * n)).view(np.uint8)).to(dev))
+    poff = torch.arange(n, device=dev, dtype=torch.int64) * pkt
+    plen = torch.full((n,), pkt, dtype=torch.int32, device=dev)
+    for r in range(R):
+        d_out = batch.spans_desc(desc[r], first, poff, plen, pkt, seeds=seeds)
+        torch.cuda.synchronize()
+        assert torch.equal(d_out, want[r]), "fragment-list kernel differs from sccsum_fragments"
+    pre_d = [batch.prepare_call("sccsum_spans_desc", desc[r], first, poff, plen, seeds, None, out, None, n, pkt)
+             for r in range(R)]
+    _, desc_s = timed(lambda k_: pre_d[k_ % R](stream), max(4, args.steps // 2), R, world, stream)
+    alg = n * (pkt + nf * 12 + 4 + 4 + 2)  # packet bytes + fragment (offset, length) + first + seed + result
+    if rank == 0:
+        emit("GiB/s device-resident Internet checksum, 9000 B jumbo packets as 5-fragment mbuf chains (f1)",
+             world * n * pkt * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
+             {"workload": f"{n} x 9000 B packets, each as mbuf fragments of 2048/2048/2048/2048/808 B in 2304 B slots "
+                          "in HBM, pseudo-header seed per packet; step = one sccsum_fragments call",
+              "packets_per_gpu": n, "rotation": f"{R} distinct slot pools launched in turn",
+              "parallelism": f"{world} independent shards"},
+             roofline(alg, launch_s, "frags", kern + " + frag_combine_kernel (sccsum_fragments)", sel, args,
+                      {"trace_select_extra": [{"kernel": "frag_combine_kernel", "skip": sel["skip"],
+                                               "count": sel["count"]}]}),
+             extra={"fragment_list_kernel": {"us_per_call": round(desc_s * 1e6, 2),
+                                             "GiBps_packet_bytes": round(n * pkt / desc_s / 2**30, 1),
+                                             "note": "sccsum_spans_desc over the same HBM fragments"}})
+
+
 def run_fill(args, world, rank, dev):
     """cfg 2 tx side with in-place write-back: IPv4 header +
     UDP checksums generated and stored into the frames (wire-ready), over R
@@ -837,7 +917,7 @@ def main():
         if args.tile_bytes is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_tile_bytes(args.tile_bytes), "sccsum_set_tile_bytes")
         {"udp1500": run_udp1500, "tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e, "fill": run_fill,
-         "sweep": run_sweep, "slots": run_slots}[args.config](args, world, rank, dev)
+         "sweep": run_sweep, "slots": run_slots, "frags": run_frags}[args.config](args, world, rank, dev)
     if world > 1:
         import torch.distributed as dist
 

@@ -36,11 +36,13 @@ timeout -k 10 300 python bench.py --config mixed --steps 20 --no-cpu --launch mu
 timeout -k 10 300 python bench.py --config mixed --steps 20 --no-cpu >> $O/ab_rx_out2.log 2>&1 && echo "ab rx_out2 ok" >> $O/steps.log && \
 timeout -k 10 300 python bench.py --config mixed --align 64 --steps 20 --no-cpu > $O/bench_mixed_align64.log 2>&1 && echo "mixed align64 ok" >> $O/steps.log && \
 timeout -k 10 300 python bench.py --config slots --steps 20 --no-cpu > $O/bench_slots.log 2>&1 && echo "slots ok" >> $O/steps.log && \
+timeout -k 10 300 python bench.py --config frags --steps 20 --no-cpu > $O/bench_frags.log 2>&1 && echo "frags ok" >> $O/steps.log && \
 PROBE_BYTES=1572864000 prof udp1500 && echo "prof udp1500 ok" >> $O/steps.log && \
 PROBE_BYTES=1572864000 prof fill && echo "prof fill ok" >> $O/steps.log && \
 prof mixed && echo "prof mixed ok" >> $O/steps.log && \
 prof tcp64k --packets 262144 && echo "prof tcp64k ok" >> $O/steps.log && \
-prof slots && echo "prof slots ok" >> $O/steps.log
+prof slots && echo "prof slots ok" >> $O/steps.log && \
+prof frags && echo "prof frags ok" >> $O/steps.log
 rc=$?
 echo "exit=$rc $(date)" >> $O/steps.log
 grep -h '^{' $O/bench*.log | cut -c1-400
