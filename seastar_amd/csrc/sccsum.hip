@@ -304,11 +304,19 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
     uint8_t* __restrict__ status, uint64_t n, uint32_t flags) {
     constexpr uint32_t kRow = 16;
     constexpr uint32_t kRowsPerBlock = kBlock / kRow;
+    constexpr uint32_t kChunk = 4 * kRowsPerBlock;  // packets a block takes at a time
     const bool raw = !IPV4 && (flags & kFlagRaw);
     const uint32_t r = threadIdx.x & (kRow - 1);
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kRowsPerBlock;
-    for (uint64_t p = static_cast<uint64_t>(xcd_block_id()) * kRowsPerBlock + threadIdx.x / kRow; p < n;
-         p += stride) {
+    const uint32_t row = threadIdx.x / kRow;
+    // A block takes 64 consecutive packets at a time (4 steps of 16 rows), so
+    // the 64 status bytes (and 256 B of results) of a chunk are written by one
+    // block, into one XCD's L2, and leave as whole lines; a plain grid stride
+    // spread each line over four blocks on different XCDs (partial writes).
+    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
+    for (uint64_t ch = xcd_block_id(); ch < nchunks; ch += gridDim.x)
+    for (uint32_t step = 0; step < kChunk / kRowsPerBlock; ++step) {
+        const uint64_t p = ch * kChunk + step * kRowsPerBlock + row;
+        if (p >= n) break;
         const uint64_t o = off[p];
         const uint32_t L = len[p];
         if (o > bytes_len || L > bytes_len - o || (IPV4 && L < 20)) {
@@ -1418,20 +1426,19 @@ int units_class(uint32_t max_len) {
 // numbered across the queue set.
 using FlatKernel = void (*)(const Queues, uint32_t, uint32_t*, uint32_t, const RssParams);
 
-int flat_occupancy(FlatKernel k) {
+// Resident 256-thread blocks per CU of a kernel (from its VGPR and LDS use),
+// cached per kernel.
+int kernel_occupancy(const void* k) {
     constexpr int kSlots = 32;
-    static std::atomic<FlatKernel> keys[kSlots];
+    static std::atomic<const void*> keys[kSlots];
     static std::atomic<int> vals[kSlots];
     for (int i = 0; i < kSlots; ++i) {
         if (keys[i].load(std::memory_order_acquire) == k) return vals[i].load(std::memory_order_relaxed);
     }
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k), kBlock, 0) != hipSuccess ||
-        nb <= 0) {
-        nb = 1;
-    }
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBlock, 0) != hipSuccess || nb <= 0) nb = 1;
     for (int i = 0; i < kSlots; ++i) {
-        FlatKernel expect = nullptr;
+        const void* expect = nullptr;
         if (keys[i].load(std::memory_order_relaxed) == nullptr) {
             vals[i].store(nb, std::memory_order_relaxed);
             if (keys[i].compare_exchange_strong(expect, k, std::memory_order_release)) break;
@@ -1439,6 +1446,8 @@ int flat_occupancy(FlatKernel k) {
     }
     return nb;
 }
+
+int flat_occupancy(FlatKernel k) { return kernel_occupancy(reinterpret_cast<const void*>(k)); }
 
 // Q holds the queues (nq >= 1); tile0 is filled here from the tile size.
 void launch_flat(FlatKernel kern, hipStream_t s, Queues& Q, uint64_t n_total, uint64_t bytes_total, uint32_t flags,
@@ -1495,19 +1504,26 @@ void launch_rows(uint32_t max_len, hipStream_t s, const uint8_t* b, uint64_t byt
                  const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
                  uint32_t flags) {
     const uint64_t units = max_len ? (static_cast<uint64_t>(max_len) + 30u) / 16u : 128u;  // worst-case head of 15
-    const uint64_t cap = static_cast<uint64_t>(cu_count()) * t_knobs.blocks_per_cu;
-    uint64_t blocks = (n + 15u) / 16u;  // 16 rows (packets at a time) per block
-    blocks = blocks < cap ? blocks : cap;
-    blocks = (blocks + 7u) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
-    const dim3 g(static_cast<unsigned>(blocks)), t(kBlock);
+    // the grid is what the chip holds at once (a grid-stride kernel: blocks
+    // that only start when others end would make the tail)
+    auto go = [&](auto kern) {
+        const int occ = kernel_occupancy(reinterpret_cast<const void*>(kern));
+        const uint64_t bpc = static_cast<uint64_t>(occ < t_knobs.blocks_per_cu ? occ : t_knobs.blocks_per_cu);
+        const uint64_t cap = static_cast<uint64_t>(cu_count()) * bpc;
+        uint64_t blocks = (n + 63u) / 64u;  // a block takes 64-packet chunks
+        blocks = blocks < cap ? blocks : cap;
+        blocks = (blocks + 7u) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
+        kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out,
+                                                                         d_status, n, flags);
+    };
     if (units <= 32) {
-        csum_row_kernel<2, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+        go(csum_row_kernel<2, IPV4>);
     } else if (units <= 64) {
-        csum_row_kernel<4, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+        go(csum_row_kernel<4, IPV4>);
     } else if (units <= 96) {  // 1500 B frames: 95 units
-        csum_row_kernel<6, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+        go(csum_row_kernel<6, IPV4>);
     } else {
-        csum_row_kernel<8, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+        go(csum_row_kernel<8, IPV4>);
     }
 }
 

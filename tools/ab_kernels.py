@@ -67,6 +67,8 @@ def cases(dev):
                                bytes_len=ns * 2304, max_len=1500)
         del fr
         yield "udp1500_slots", sb, "frames", ns * (1500 + 12 + 4)
+        if "udp1500_slots_verify" in CASES:  # the same, verify only (status bytes, no out2)
+            yield "udp1500_slots_verify", sb, "verify", ns * (1500 + 12 + 1)
 
 
 def main():
@@ -105,9 +107,13 @@ def main():
             native.check(lib.sccsum_set_out_policy(int(parts[8] or 1)), "out_policy")
             native.check(lib.sccsum_set_short_chunks(int(parts[9] or 1)), "short_chunks")
 
+        st_buf = torch.empty(max(b.n, 1), dtype=torch.uint8, device=dev)
+
         def run(bb):
             if mode == "frames":
                 return batch.ipv4_frames(bb)
+            if mode == "verify":
+                return batch.verify_frames(bb, st_buf)
             if mode == "frames_rss":
                 return batch.ipv4_frames_rss(bb)[1]
             return batch.spans(bb)
