@@ -968,3 +968,54 @@ def test_random_layouts_shuffled_overlapping(dev, kernel_variant, seed):
     got, st = _frames(dev, fb, off, lens)
     want, want_st = oracle.batch_ipv4(fb, off, lens)
     assert np.array_equal(got, want) and np.array_equal(st, want_st)
+
+
+@pytest.mark.parametrize("case", ["zipf_frames", "spans_zero_lengths", "spans_shuffled", "fill_tx_frames"])
+def test_full_tiles_match_oracle(dev, kernel_variant, case):
+    """Full 64-packet tiles.  The small cases above get tiles of a few
+    packets (B = n / waves); a grid of one block per CU (1 024 waves) and
+    ~100 K packets fills every tile to the cap, so runs span whole tiles,
+    last tiles end ragged, and slow-path packets (IP options, over-long spans)
+    sit among 63 fast ones: Zipf frames, spans with zero lengths, shuffled
+    spans (one run per packet), in-place fill of the tx generator's frames.
+    (This test also carried the round-2 A/B of two packets per lane,
+    profiles/r02_ab_p2.log.)"""
+    if kernel_variant not in (15, 16):
+        pytest.skip("full tiles exercised on the default flat forms")
+    lib = native.load()
+    native.check(lib.sccsum_set_blocks_per_cu(1), "blocks_per_cu")
+    native.check(lib.sccsum_set_tile_bytes(0 if case != "zipf_frames" else 49152), "tile_bytes")
+    rng = np.random.default_rng(0x7A11)
+    try:
+        if case == "zipf_frames":
+            buf, off, lens, _ = synth.mixed_udp_frames(150_000, seed=0x7A12, max_gap=3)
+            got, st = _frames(dev, buf, off, lens)
+            want, want_st = oracle.batch_ipv4(buf, off, lens)
+            assert np.array_equal(got, want) and np.array_equal(st, want_st)
+        elif case.startswith("spans"):
+            n = 110_000
+            lens = rng.integers(0, 3000, n).astype(np.uint32)
+            lens[rng.random(n) < 0.05] = 0
+            lens[rng.integers(0, n, 20)] = 140_000  # over kExactMax: phase D
+            off, total = synth.pack(lens, seed=0x7A13, max_gap=2)
+            if case == "spans_shuffled":  # every packet its own run (spans stay inside the buffer)
+                order = rng.permutation(n)
+                off, lens = off[order], lens[order]
+            buf = rng.integers(0, 256, size=int(total), dtype=np.uint8)
+            seeds = rng.integers(0, 65536, n).astype(np.uint32)
+            assert np.array_equal(_spans(dev, buf, off, lens, seeds), oracle.batch_spans(buf, off, lens, seeds))
+        else:
+            m = native.FILL_IP | native.FILL_L4
+            buf, off, length = _tx_frames(rng, 100_000)
+            b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+            out2 = torch.empty(2 * b.n, dtype=torch.int16, device=dev)
+            st = torch.empty(b.n, dtype=torch.uint8, device=dev)
+            batch.ipv4_fill(b, m, out2=out2, status=st)
+            torch.cuda.synchronize()
+            want_buf, want_out2, want_st = oracle.batch_ipv4_fill(buf, off, length, m)
+            assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want_out2)
+            assert np.array_equal(st.cpu().numpy(), want_st)
+            assert np.array_equal(b.data.cpu().numpy()[: buf.size], want_buf)
+    finally:
+        native.check(lib.sccsum_set_blocks_per_cu(8), "blocks_per_cu")
+        native.check(lib.sccsum_set_tile_bytes(49152), "tile_bytes")
