@@ -77,6 +77,7 @@ def parse():
                          "jumbo packets as 5-fragment mbuf chains in HBM (checksummer::sum(const packet&))")
     ap.add_argument("--tile-bytes", type=int, default=None, help="A/B: flat-kernel tile target (sccsum_diag.h)")
     ap.add_argument("--variant", type=int, default=None, help="A/B: kernel form (sccsum_set_kernel_variant)")
+    ap.add_argument("--run-align", type=int, default=None, help="A/B: run-start alignment in units (sccsum_set_run_align)")
     ap.add_argument("--seg-len", type=int, default=65536, help="tcp64k: segment bytes (65536, or 65535: odd offsets)")
     ap.add_argument("--align", type=int, default=1, help="mixed: frame start alignment (1 = packed, SURVEY §8(d) (i); "
                                                          "64 = layout (ii))")
@@ -919,6 +920,8 @@ def main():
             native.check(native.load().sccsum_set_tile_bytes(args.tile_bytes), "sccsum_set_tile_bytes")
         if args.variant is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_kernel_variant(args.variant), "sccsum_set_kernel_variant")
+        if args.run_align is not None:  # A/B only (sccsum_diag.h)
+            native.check(native.load().sccsum_set_run_align(args.run_align), "sccsum_set_run_align")
         {"udp1500": run_udp1500, "tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e, "fill": run_fill,
          "sweep": run_sweep, "slots": run_slots, "frags": run_frags}[args.config](args, world, rank, dev)
     if world > 1:

@@ -63,6 +63,12 @@ int sccsum_set_out_policy(int policy);
  * default), or always U rows (0).  SCCSUM_EINVAL otherwise. */
 int sccsum_set_short_chunks(int on);
 
+/* Flat kernel: each run's streamed extent starts on a boundary of `units`
+ * 16-byte units (1, 4 = 64 B or 8 = 128 B, the default; clamped to the
+ * batch's first unit), so a wave's 1 KiB load rows cover whole cache lines.
+ * SCCSUM_EINVAL otherwise. */
+int sccsum_set_run_align(int units);
+
 /* Stream-read `bytes` (multiple of 16) from d_src with the same
  * load width as the checksum kernels and write one 64-bit word per workgroup
  * to d_sink (capacity >= sccsum_read_probe_blocks()).  Used by bench.py as

@@ -47,6 +47,7 @@ constexpr uint32_t kFlagRaw = 1;     // spans: output the folded span-relative s
 constexpr uint32_t kFlagFillL4 = 2;  // frames: generate the TCP/UDP checksum and store it in the frame
 constexpr uint32_t kFlagFillIp = 4;  // frames (with kFlagFillL4): also generate + store the IPv4 header checksum
 constexpr uint32_t kFlagFullChunks = 16;  // flat kernel: a run's last chunk loads all U rows (diagnostic A/B)
+constexpr uint32_t kRunAlignShift = 12;   // flat kernel, flags bits 12-13: run extents start on 1 / 4 / 8-unit boundaries
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -704,6 +705,10 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
     constexpr uint32_t kLdsUnits = C;
     constexpr int kHead = FILL ? 4 : (IPV4 ? 3 : 1);
     const bool short_chunks = (flags & kFlagFullChunks) == 0;
+    // a run's streamed extent starts on a 64 / 128-byte boundary (clamped to
+    // the batch's first unit), so each 1 KiB load row covers whole lines
+    const uint32_t ra_code = (flags >> kRunAlignShift) & 3u;
+    const uint64_t ra_mask = ra_code == 0 ? 0ull : (ra_code == 1 ? 3ull : 7ull);
     const bool raw = !IPV4 && (flags & kFlagRaw);
     const bool fill_ip = FILL && (flags & kFlagFillIp);
     __shared__ u32x4 ubuf_all[kWavesPerBlock][kLdsUnits];
@@ -843,6 +848,9 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
         const uint32_t Fhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(c.fu >> 32), k);
         const uint32_t Flo = __builtin_amdgcn_readlane(static_cast<uint32_t>(c.fu), k);
         rn.F = (static_cast<uint64_t>(Fhi) << 32) | Flo;
+        const uint64_t lo_u = reinterpret_cast<uint64_t>(Q.bytes[c.q]) >> 4;  // the batch's first unit
+        const uint64_t Fa = rn.F & ~ra_mask;
+        rn.F = Fa >= lo_u ? Fa : lo_u;  // (F >= lo_u: the run's first packet lies in the batch)
         const uint32_t Llo = __builtin_amdgcn_readlane(static_cast<uint32_t>(c.lu), rn.k2 - 1);
         rn.ext = Llo - static_cast<uint32_t>(rn.F) + 1u;  // units in the run's extent
         return rn;
@@ -1301,6 +1309,14 @@ constexpr int kTailQuarters = 4;
 // frames 237.4 -> 235.5 us; sc1 / sc0 sc1 the same, sc0 no gain).
 constexpr int kOutPolicy = 1;
 
+// Run extents start on a 128-byte L2 line (8 units): a wave's 1 KiB load rows
+// then cover 8 whole lines instead of 9 partial ones when a tile starts
+// mid-line (odd offsets, 65 535 B segments).  Same-box A/B
+// (profiles/r02_ab_run_align.log): Zipf frames 237.9 -> 234.2 us, 65 535 B
+// spans 168.8 -> 166.7 us, 1500 B frames and 64 KiB spans -0.4-0.5 %; 64 B
+// (4 units) lands in between.
+constexpr int kRunAlign = 8;
+
 // Diagnostic knobs (include/sccsum_diag.h): per host thread, so one shard's
 // A/B settings never leak into another thread's launches.
 struct Knobs {
@@ -1314,6 +1330,7 @@ struct Knobs {
     int tail_quarters = kTailQuarters;  // flat kernel: tail = tail_quarters / 4 whole tiles per wave of the grid
     int out_policy = kOutPolicy;     // flat kernel: cache policy of the result stores (tile_store)
     int short_chunks = 1;            // flat kernel (no chunk in flight): a run's last chunk covers only its rows
+    int run_align = kRunAlign;       // flat kernel: run extents start on 1 / 4 / 8-unit (16 / 64 / 128 B) boundaries
 };
 thread_local Knobs t_knobs;
 
@@ -1483,6 +1500,7 @@ void launch_flat(FlatKernel kern, hipStream_t s, Queues& Q, uint64_t n_total, ui
     uint32_t* heads = K.dynamic ? heads_for(s) : nullptr;
     flags |= static_cast<uint32_t>(K.out_policy) << kOutPolicyShift;
     if (!K.short_chunks) flags |= kFlagFullChunks;
+    flags |= static_cast<uint32_t>(K.run_align == 8 ? 2 : (K.run_align == 4 ? 1 : 0)) << kRunAlignShift;
     kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(Q, static_cast<uint32_t>(B), heads, flags, rss);
 }
 
@@ -2141,6 +2159,12 @@ int sccsum_set_out_policy(int policy) {
 int sccsum_set_short_chunks(int on) {
     if (on != 0 && on != 1) return SCCSUM_EINVAL;
     sccsum::t_knobs.short_chunks = on;
+    return SCCSUM_OK;
+}
+
+int sccsum_set_run_align(int units) {
+    if (units != 1 && units != 4 && units != 8) return SCCSUM_EINVAL;
+    sccsum::t_knobs.run_align = units;
     return SCCSUM_OK;
 }
 

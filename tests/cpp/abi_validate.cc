@@ -116,6 +116,9 @@ int main() {
     EXPECT(sccsum_set_out_policy(3) == SCCSUM_OK && sccsum_set_out_policy(0) == SCCSUM_OK);
     EXPECT(sccsum_set_short_chunks(2) == SCCSUM_EINVAL && sccsum_set_short_chunks(-1) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_short_chunks(0) == SCCSUM_OK && sccsum_set_short_chunks(1) == SCCSUM_OK);
+    EXPECT(sccsum_set_run_align(0) == SCCSUM_EINVAL && sccsum_set_run_align(2) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_run_align(16) == SCCSUM_EINVAL && sccsum_set_run_align(8) == SCCSUM_OK);
+    EXPECT(sccsum_set_run_align(4) == SCCSUM_OK && sccsum_set_run_align(1) == SCCSUM_OK);
     EXPECT(sccsum_set_burst_fused(3) == SCCSUM_EINVAL && sccsum_set_burst_fused(-1) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_burst_fused(2) == SCCSUM_OK);
     EXPECT(sccsum_pipeline_run(nullptr, SCCSUM_PIPE_IPV4, SCCSUM_GATHER_ZERO_COPY, nullptr, 0, nullptr, nullptr,

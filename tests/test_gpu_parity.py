@@ -1019,3 +1019,49 @@ def test_full_tiles_match_oracle(dev, kernel_variant, case):
     finally:
         native.check(lib.sccsum_set_blocks_per_cu(8), "blocks_per_cu")
         native.check(lib.sccsum_set_tile_bytes(49152), "tile_bytes")
+
+
+@pytest.mark.parametrize("units", [1, 4, 8])
+def test_run_align_matches_oracle(dev, kernel_variant, units):
+    """Run extents started on 16 / 64 / 128-byte boundaries (sccsum_set_run_align;
+    128 B is the default) change only which bytes a wave loads before a run's
+    first packet: Zipf
+    frames at odd offsets, a batch whose first packet sits in its first unit
+    (the clamp), 65 535 B spans at odd offsets and shuffled spans match the
+    oracle."""
+    if kernel_variant not in (14, 15, 16):
+        pytest.skip("run alignment applies to the flat forms")
+    lib = native.load()
+    native.check(lib.sccsum_set_run_align(units), "run_align")
+    try:
+        for gap in (0, 3):
+            buf, off, lens, _ = synth.mixed_udp_frames(6000, seed=0xA11 + gap, max_gap=gap)
+            got, st = _frames(dev, buf, off, lens)
+            want, want_st = oracle.batch_ipv4(buf, off, lens)
+            assert np.array_equal(got, want) and np.array_equal(st, want_st)
+        rng = np.random.default_rng(0xA12)
+        lens = np.full(40, 65535, np.uint32)
+        off, total = synth.pack(lens, seed=0xA13, max_gap=5)
+        buf = rng.integers(0, 256, size=int(total), dtype=np.uint8)
+        assert np.array_equal(_spans(dev, buf, off, lens), oracle.batch_spans(buf, off, lens))
+        lens = rng.integers(0, 2000, 20000).astype(np.uint32)
+        off, total = synth.pack(lens, seed=0xA14, max_gap=2)
+        order = rng.permutation(lens.size)
+        off, lens = off[order], lens[order]
+        buf = rng.integers(0, 256, size=int(total), dtype=np.uint8)
+        assert np.array_equal(_spans(dev, buf, off, lens), oracle.batch_spans(buf, off, lens))
+        # a batch based 16 B past a 128 B boundary: the first runs' aligned start
+        # would fall before the batch, so it is clamped to the batch's first unit
+        buf, off, lens, _ = synth.mixed_udp_frames(3000, seed=0xA15)
+        big = torch.zeros(buf.size + 64, dtype=torch.uint8, device=dev)
+        big[16:16 + buf.size] = torch.from_numpy(buf).to(dev)
+        b = batch.PacketBatch(data=big[16:], off=torch.from_numpy(off.astype(np.int64)).to(dev),
+                              length=torch.from_numpy(lens.astype(np.int32)).to(dev), bytes_len=buf.size,
+                              max_len=int(lens.max()))
+        st = torch.empty(b.n, dtype=torch.uint8, device=dev)
+        got = batch.as_u16(batch.ipv4_frames(b, status=st))
+        torch.cuda.synchronize()
+        want, want_st = oracle.batch_ipv4(buf, off, lens)
+        assert np.array_equal(got, want) and np.array_equal(st.cpu().numpy(), want_st)
+    finally:
+        native.check(lib.sccsum_set_run_align(8), "run_align")

@@ -55,6 +55,12 @@ def cases(dev):
                            length=torch.full((n64,), 65536, dtype=torch.int32, device=dev),
                            bytes_len=n64 * 65536, max_len=65536)
     yield "tcp64k_spans", lb, "spans", n64 * (65536 + 14)
+    if "tcp65535_spans" in CASES:  # 65 535 B segments back to back: every tile starts mid-line
+        ob = batch.PacketBatch(data=seg, off=torch.arange(n64, device=dev, dtype=torch.int64) * 65535,
+                               length=torch.full((n64,), 65535, dtype=torch.int32, device=dev),
+                               bytes_len=n64 * 65535, max_len=65535)
+        yield "tcp65535_spans", ob, "spans", n64 * (65535 + 14)
+        del ob
     if "udp1500_slots" in CASES:  # frames where a NIC would DMA them: DPDK mbuf slots (2304 B, data at +256)
         del lb, seg
         torch.cuda.empty_cache()
@@ -75,7 +81,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn[:tile_bytes[:tail_split[:tail_quarters[:out_policy[:short_chunks]]]]]]]]]")
+    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn[:tile_bytes[:tail_split[:tail_quarters[:out_policy[:short_chunks[:run_align]]]]]]]]]]")
     ap.add_argument("--rotate", type=int, default=4, help="distinct copies of each batch, launched in turn")
     ap.add_argument("--cases", default="udp1500_frames,udp1500_spans,udp1500_frames_rss,zipf_spans,cfg3_zipf_frames,"
                                        "tcp64k_spans")
@@ -96,7 +102,7 @@ def main():
         turn = [0]
 
         def knobs(v):
-            parts = (v.split(":") + [""] * 10)[:10]
+            parts = (v.split(":") + [""] * 11)[:11]
             native.check(lib.sccsum_set_kernel_variant(int(parts[0])), "variant")
             native.check(lib.sccsum_set_blocks_per_cu(int(parts[1] or 8)), "blocks_per_cu")
             native.check(lib.sccsum_set_group_units(int(parts[2] or 0)), "group_units")
@@ -106,6 +112,7 @@ def main():
             native.check(lib.sccsum_set_tail_split(int(parts[6] or 1), int(parts[7] or 4)), "tail_split")
             native.check(lib.sccsum_set_out_policy(int(parts[8] or 1)), "out_policy")
             native.check(lib.sccsum_set_short_chunks(int(parts[9] or 1)), "short_chunks")
+            native.check(lib.sccsum_set_run_align(int(parts[10] or 8)), "run_align")
 
         st_buf = torch.empty(max(b.n, 1), dtype=torch.uint8, device=dev)
 
@@ -158,6 +165,7 @@ def main():
     native.check(lib.sccsum_set_tail_split(1, 4), "tail_split")
     native.check(lib.sccsum_set_out_policy(1), "out_policy")
     native.check(lib.sccsum_set_short_chunks(1), "short_chunks")
+    native.check(lib.sccsum_set_run_align(8), "run_align")
 
 
 if __name__ == "__main__":
