@@ -29,6 +29,24 @@ class PacketBatch:
     bytes_len: int
     max_len: int
 
+    def __post_init__(self):
+        # the kernels trust these: a short buffer or a mistyped array would be
+        # read (or, for in-place fill, written) past its end on the device
+        d, o, ln = self.data, self.off, self.length
+        if d.dtype != torch.uint8 or d.dim() != 1 or not d.is_contiguous():
+            raise ValueError("PacketBatch.data must be a contiguous 1-D uint8 tensor")
+        if not (0 <= int(self.bytes_len) and _round16(int(self.bytes_len)) <= d.numel()):
+            raise ValueError(f"PacketBatch.data holds {d.numel()} bytes; bytes_len {self.bytes_len} needs "
+                             f"{_round16(int(self.bytes_len))} (padded to 16)")
+        if o.dtype != torch.int64 or o.dim() != 1 or not o.is_contiguous():
+            raise ValueError("PacketBatch.off must be a contiguous 1-D int64 tensor")
+        if ln.dtype != torch.int32 or ln.dim() != 1 or not ln.is_contiguous() or ln.numel() != o.numel():
+            raise ValueError("PacketBatch.length must be a contiguous 1-D int32 tensor with one entry per offset")
+        if o.device != d.device or ln.device != d.device:
+            raise ValueError("PacketBatch tensors must be on one device")
+        if int(self.max_len) < 0:
+            raise ValueError("PacketBatch.max_len must be >= 0 (0 = unknown)")
+
     @property
     def n(self) -> int:
         return int(self.off.numel())
@@ -59,6 +77,15 @@ def _ptr(t):
     return None if t is None else ctypes_ptr(t)
 
 
+def _need(t: torch.Tensor | None, numel: int, dtype: torch.dtype, what: str, device: torch.device) -> None:
+    """A caller-supplied array the kernel reads or writes numel elements of."""
+    if t is None:
+        return
+    if t.dtype != dtype or not t.is_contiguous() or t.numel() < numel or t.device != device:
+        raise ValueError(f"{what}: need a contiguous {dtype} tensor of >= {numel} elements on {device}, got "
+                         f"{t.dtype} x {t.numel()} on {t.device}")
+
+
 def ctypes_ptr(t: torch.Tensor) -> int:
     if not t.is_cuda:
         raise ValueError("sccsum kernels need device tensors")
@@ -77,8 +104,9 @@ def spans(batch: PacketBatch, seeds: torch.Tensor | None = None, out: torch.Tens
     n = batch.n
     if out is None:
         out = torch.empty(max(n, 1), dtype=torch.int16, device=batch.device)
-    if seeds is not None:
-        assert seeds.dtype == torch.int32 and seeds.numel() >= n
+    _need(out, n, torch.int16, "out", batch.device)
+    _need(seeds, n, torch.int32, "seeds", batch.device)
+    _need(status, n, torch.uint8, "status", batch.device)
     code = lib.sccsum_spans(
         ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length),
         _ptr(seeds), ctypes_ptr(out), _ptr(status), n, batch.max_len, _stream(stream),
@@ -94,6 +122,8 @@ def ipv4_frames(batch: PacketBatch, out2: torch.Tensor | None = None, status: to
     n = batch.n
     if out2 is None:
         out2 = torch.empty(max(2 * n, 2), dtype=torch.int16, device=batch.device)
+    _need(out2, 2 * n, torch.int16, "out2", batch.device)
+    _need(status, n, torch.uint8, "status", batch.device)
     code = lib.sccsum_ipv4_frames(
         ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length),
         ctypes_ptr(out2), _ptr(status), n, batch.max_len, _stream(stream),
@@ -108,7 +138,9 @@ def verify_frames(batch: PacketBatch, status: torch.Tensor, stream=None) -> torc
     tcp.hh:876-883: drop when get() != 0).  Returns status[:n]."""
     lib = native.load()
     n = batch.n
-    assert status is not None and status.dtype == torch.uint8 and status.numel() >= n
+    if status is None:
+        raise ValueError("verify_frames needs a status tensor")
+    _need(status, n, torch.uint8, "status", batch.device)
     code = lib.sccsum_ipv4_frames(
         ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length),
         None, ctypes_ptr(status), n, batch.max_len, _stream(stream),
@@ -122,14 +154,19 @@ def _multi(fn, name, items, max_len, stream, width, with_seed):
     if len(items) > native.MAX_BATCHES:
         raise ValueError(f"at most {native.MAX_BATCHES} batches per launch")
     arr = (native.Batch * max(len(items), 1))()
-    outs = []
-    for i, it in enumerate(items):
+    outs, rows = [], []
+    for i, it in enumerate(items):  # every batch checked before any address is taken
         b, out, status = it[0], it[1], it[2]
         seeds = it[3] if len(it) > 3 else None
+        if seeds is not None and not with_seed:
+            raise ValueError(f"{name}: frames take no seeds")
+        _need(out, width * b.n, torch.int16, f"batch {i} out", b.device)
+        _need(seeds, b.n, torch.int32, f"batch {i} seeds", b.device)
+        _need(status, b.n, torch.uint8, f"batch {i} status", b.device)
+        rows.append((b, out, status, seeds))
+    for i, (b, out, status, seeds) in enumerate(rows):
         if out is None:
             out = torch.empty(max(width * b.n, width), dtype=torch.int16, device=b.device)
-        if seeds is not None:
-            assert with_seed and seeds.dtype == torch.int32 and seeds.numel() >= b.n
         arr[i] = native.Batch(ctypes_ptr(b.data), b.bytes_len, ctypes_ptr(b.off), ctypes_ptr(b.length), _ptr(seeds),
                               ctypes_ptr(out), _ptr(status), b.n)
         outs.append(out)
@@ -153,9 +190,13 @@ def prepare_ipv4_frames_multi(items):
     if not items or len(items) > native.MAX_BATCHES:
         raise ValueError(f"1..{native.MAX_BATCHES} batches per launch")
     arr = (native.Batch * len(items))()
-    for i, (b, out, status) in enumerate(items):
+    for i, (b, out, status) in enumerate(items):  # every batch checked before any address is taken
         # out None: a verify-only batch (status bits only)
-        assert (out is not None and out.numel() >= 2 * b.n) or (status is not None and status.numel() >= b.n)
+        if out is None and status is None:
+            raise ValueError(f"batch {i}: give out2, status or both")
+        _need(out, 2 * b.n, torch.int16, f"batch {i} out2", b.device)
+        _need(status, b.n, torch.uint8, f"batch {i} status", b.device)
+    for i, (b, out, status) in enumerate(items):
         arr[i] = native.Batch(ctypes_ptr(b.data), b.bytes_len, ctypes_ptr(b.off), ctypes_ptr(b.length), None,
                               _ptr(out), _ptr(status), b.n)
     ml = max(it[0].max_len for it in items)
@@ -202,6 +243,8 @@ def ipv4_fill(batch: PacketBatch, mode: int = native.FILL_IP | native.FILL_L4, o
     given = out2
     if out2 is None and mode & native.FILL_L4:  # the generate and store passes hand the values over in out2
         out2 = torch.empty(max(2 * n, 2), dtype=torch.int16, device=batch.device)
+    _need(out2, 2 * n, torch.int16, "out2", batch.device)
+    _need(status, n, torch.uint8, "status", batch.device)
     code = lib.sccsum_ipv4_fill(
         ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length),
         _ptr(out2), _ptr(status), n, batch.max_len, mode, _stream(stream),
@@ -227,6 +270,8 @@ def ipv4_rss(batch: PacketBatch, key: bytes = RSS_KEY_40, mode: int = native.RSS
     n = batch.n
     if hash_out is None:
         hash_out = torch.empty(max(n, 1), dtype=torch.int32, device=batch.device)
+    _need(hash_out, n, torch.int32, "hash_out", batch.device)
+    _need(status, n, torch.uint8, "status", batch.device)
     kb, kl = _key(key)
     code = lib.sccsum_ipv4_rss(ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off),
                                ctypes_ptr(batch.length), ctypes.addressof(kb), kl, mode, ctypes_ptr(hash_out),
@@ -245,6 +290,9 @@ def ipv4_frames_rss(batch: PacketBatch, key: bytes = RSS_KEY_40, mode: int = nat
         out2 = torch.empty(max(2 * n, 2), dtype=torch.int16, device=batch.device)
     if hash_out is None:
         hash_out = torch.empty(max(n, 1), dtype=torch.int32, device=batch.device)
+    _need(out2, 2 * n, torch.int16, "out2", batch.device)
+    _need(hash_out, n, torch.int32, "hash_out", batch.device)
+    _need(status, n, torch.uint8, "status", batch.device)
     kb, kl = _key(key)
     code = lib.sccsum_ipv4_frames_rss(
         ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length), ctypes_ptr(out2),
@@ -262,6 +310,15 @@ def fragments(data: torch.Tensor, bytes_len: int, frag_off: torch.Tensor, frag_l
     nfrag = int(frag_off.numel())
     if out is None:
         out = torch.empty(max(n, 1), dtype=torch.int16, device=data.device)
+    dev = data.device
+    if n < 0:
+        raise ValueError("pkt_first needs n + 1 entries")
+    _need(frag_off, nfrag, torch.int64, "frag_off", dev)
+    _need(frag_len, nfrag, torch.int32, "frag_len", dev)
+    _need(pkt_first, n + 1, torch.int32, "pkt_first", dev)
+    _need(seeds, n, torch.int32, "seeds", dev)
+    _need(out, n, torch.int16, "out", dev)
+    _need(status, n, torch.uint8, "status", dev)
     ws = torch.empty(int(lib.sccsum_fragments_workspace(nfrag)), dtype=torch.uint8, device=data.device)
     code = lib.sccsum_fragments(
         ctypes_ptr(data), bytes_len, ctypes_ptr(frag_off), ctypes_ptr(frag_len), nfrag, ctypes_ptr(pkt_first),
@@ -288,9 +345,14 @@ def _desc_call(name, desc, first, off, length, max_len, width, seeds, stage, out
     lib = native.load()
     n = int(off.numel())
     dev = off.device
-    assert int(first.numel()) == n + 1 and first.dtype == torch.int32 and desc.dtype == torch.uint8
+    if int(first.numel()) != n + 1 or first.dtype != torch.int32 or desc.dtype != torch.uint8:
+        raise ValueError(f"{name}: first must be int32 [n + 1] and desc uint8 records")
     if out is None:
         out = torch.empty(max(width * n, width), dtype=torch.int16, device=dev)
+    _need(length, n, torch.int32, "length", dev)
+    _need(seeds, n, torch.int32, "seeds", dev)
+    _need(out, width * n, torch.int16, "out", dev)
+    _need(status, n, torch.uint8, "status", dev)
     args = [ctypes_ptr(desc), ctypes_ptr(first), ctypes_ptr(off), ctypes_ptr(length)]
     if width == 1:
         args.append(_ptr(seeds))
