@@ -109,15 +109,22 @@ class HostPipeline:
         2 = one 2D DMA of each slot's packet bytes, 3 = no copies: the kernel
         reads the packets in place (buf must be pinned: pinned_empty)
         (native.GATHER_*)."""
+        # the native side reads buf.size bytes at buf's address and n entries of
+        # every metadata array: a strided / wider-typed buf or a short array
+        # would be read past its end
+        if not (isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and buf.flags.c_contiguous):
+            raise ValueError("buf must be a contiguous uint8 array")
         if gather == native.GATHER_ZERO_COPY and buf.size and not is_pinned(buf):
             raise ValueError("zero-copy pipeline runs need a pinned buffer (pinned_empty)")
         off = np.ascontiguousarray(off, dtype=np.uint64)
         length = np.ascontiguousarray(length, dtype=np.uint32)
         n = off.size
+        sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+        if length.size != n or (sd is not None and sd.size != n):
+            raise ValueError(f"off, length and seeds need one entry per packet ({n})")
         width = 2 if mode == native.PIPE_IPV4 else 1
         out = np.empty((n, width) if width == 2 else n, dtype=np.uint16)
         st = np.empty(n, dtype=np.uint8) if status else None
-        sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
         code = self._lib.sccsum_pipeline_run(
             self._h, mode, int(gather), buf.ctypes.data if buf.size else None, buf.size, off.ctypes.data,
             length.ctypes.data, None if sd is None else sd.ctypes.data, n, max_len,

@@ -72,3 +72,23 @@ def test_wrappers_refuse_short_outputs():
         batch.fragments(b.data, b.bytes_len, b.off, b.length, torch.arange(4, dtype=torch.int64))
     with pytest.raises(ValueError, match="frag_len"):
         batch.fragments(b.data, b.bytes_len, b.off, b.length[:5], torch.arange(4, dtype=torch.int32))
+
+
+def test_host_pipeline_refuses_mismatched_arrays():
+    """HostPipeline.run checks its host arrays before the native call (the
+    pipeline object here is never created on a device)."""
+    from seastar_amd import native, pipeline
+
+    pl = pipeline.HostPipeline.__new__(pipeline.HostPipeline)
+    pl._lib, pl._h = native.load(), None
+    buf = np.zeros(4096, np.uint8)
+    off = np.array([0, 100, 200], np.uint64)
+    lens = np.array([50, 50, 50], np.uint32)
+    with pytest.raises(ValueError, match="one entry per packet"):
+        pl.run(native.PIPE_IPV4, buf, off, lens[:2])
+    with pytest.raises(ValueError, match="one entry per packet"):
+        pl.run(native.PIPE_SPANS, buf, off, lens, seeds=np.zeros(2, np.uint32))
+    with pytest.raises(ValueError, match="contiguous uint8"):
+        pl.run(native.PIPE_IPV4, buf.view(np.uint32), off, lens)
+    with pytest.raises(ValueError, match="contiguous uint8"):
+        pl.run(native.PIPE_IPV4, buf[::2], off, lens)
