@@ -1,6 +1,7 @@
 #!/bin/bash
 # Whole GPU suite (now with the two-packet forms 17 / 18), smoke, default
-# bench, then the same-box A/B of forms 17 / 18 against 16 / 15.
+# bench, then the same-box A/B of forms 17 / 18 against 16 / 15.  Forms 17 / 18
+# lost (profiles/r02_ab_p2.log) and were removed: this script records the run.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/s3c
