@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--tile-bytes", type=int, default=None, help="A/B: flat-kernel tile target (sccsum_diag.h)")
     ap.add_argument("--variant", type=int, default=None, help="A/B: kernel form (sccsum_set_kernel_variant)")
     ap.add_argument("--run-align", type=int, default=None, help="A/B: run-start alignment in units (sccsum_set_run_align)")
+    ap.add_argument("--sync", default="auto", choices=["auto", "spin", "yield"],
+                    help="how the host thread waits on the device (hipSetDeviceFlags schedule)")
     ap.add_argument("--seg-len", type=int, default=65536, help="tcp64k: segment bytes (65536, or 65535: odd offsets)")
     ap.add_argument("--align", type=int, default=1, help="mixed: frame start alignment (1 = packed, SURVEY §8(d) (i); "
                                                          "64 = layout (ii))")
@@ -153,6 +155,26 @@ def _imports():
 BACKEND = os.environ.get("SCCSUM_DIST_BACKEND", "gloo")
 
 
+SYNC_MODE = "auto"
+_SCHEDULE = {"auto": 0, "spin": 1, "yield": 2}  # hipDeviceScheduleAuto / Spin / Yield (hip_runtime_api.h)
+
+
+def set_sync_mode(dev: int, mode: str) -> None:
+    """How this rank's host thread waits on its device.  "spin" polls, as
+    Seastar's reactor polls its queues (include/seastar/core/internal/poll.hh:26-29);
+    HIP's "auto" yields the core while the GPU works, unless contexts outnumber
+    the logical CPUs.  Set before the device's context exists."""
+    if mode == "auto":
+        return
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    for rc, what in ((hip.hipSetDevice(ctypes.c_int(dev)), "hipSetDevice"),
+                     (hip.hipSetDeviceFlags(ctypes.c_uint(_SCHEDULE[mode])), "hipSetDeviceFlags")):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed ({rc})")
+
+
 def dist_setup(dry_run=False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -169,6 +191,7 @@ def dist_setup(dry_run=False):
         return world, rank, local
     ndev = torch.cuda.device_count()
     dev = local % max(ndev, 1)
+    set_sync_mode(dev, SYNC_MODE)
     torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
@@ -357,8 +380,8 @@ def roofline(alg_bytes_launch: float, launch_s: float, config: str, kernel: str,
 def emit(metric, value, unit, args, world, wall, dtype, config, roof=None, cpu=None, extra=None):
     d = {"metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": world, "steps": args.steps,
          "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
-         "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic", "config": config,
-         "roofline": roof, "cpu_baseline": cpu}
+         "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
+         "config": dict(config, host_wait=SYNC_MODE), "roofline": roof, "cpu_baseline": cpu}
     if extra:
         d.update(extra)
     print(json.dumps(d), flush=True)
@@ -908,6 +931,8 @@ def run_dry(args, world, rank):
 
 def main():
     args = parse()
+    global SYNC_MODE
+    SYNC_MODE = args.sync
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     _imports()

@@ -1063,5 +1063,15 @@ def test_run_align_matches_oracle(dev, kernel_variant, units):
         torch.cuda.synchronize()
         want, want_st = oracle.batch_ipv4(buf, off, lens)
         assert np.array_equal(got, want) and np.array_equal(st.cpu().numpy(), want_st)
+        # the same batch as the second queue of a multi launch: the clamp is per queue
+        buf0, off0, lens0, _ = synth.mixed_udp_frames(2000, seed=0xA16)
+        b0 = batch.PacketBatch.from_host(buf0, off0, lens0, device=dev)
+        st0 = torch.empty(b0.n, dtype=torch.uint8, device=dev)
+        st1 = torch.empty(b.n, dtype=torch.uint8, device=dev)
+        o0, o1 = batch.ipv4_frames_multi([(b0, None, st0), (b, None, st1)])
+        torch.cuda.synchronize()
+        w0, ws0 = oracle.batch_ipv4(buf0, off0, lens0)
+        assert np.array_equal(batch.as_u16(o0), w0) and np.array_equal(st0.cpu().numpy(), ws0)
+        assert np.array_equal(batch.as_u16(o1), want) and np.array_equal(st1.cpu().numpy(), want_st)
     finally:
         native.check(lib.sccsum_set_run_align(8), "run_align")
