@@ -69,12 +69,6 @@ int sccsum_set_short_chunks(int on);
  * SCCSUM_EINVAL otherwise. */
 int sccsum_set_run_align(int units);
 
-/* Flat kernel: load a run's first row (the line it shares with the tile
- * before) with the default cache policy instead of nontemporal: 0 never (the
- * default), 1 always, 2 in launches of single-packet tiles (packets of at
- * least the tile target).  SCCSUM_EINVAL otherwise. */
-int sccsum_set_head_cached(int mode);
-
 /* Stream-read `bytes` (multiple of 16) from d_src with the same
  * load width as the checksum kernels and write one 64-bit word per workgroup
  * to d_sink (capacity >= sccsum_read_probe_blocks()).  Used by bench.py as

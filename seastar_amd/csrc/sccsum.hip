@@ -48,7 +48,6 @@ constexpr uint32_t kFlagFillL4 = 2;  // frames: generate the TCP/UDP checksum an
 constexpr uint32_t kFlagFillIp = 4;  // frames (with kFlagFillL4): also generate + store the IPv4 header checksum
 constexpr uint32_t kFlagFullChunks = 16;  // flat kernel: a run's last chunk loads all U rows (diagnostic A/B)
 constexpr uint32_t kRunAlignShift = 12;   // flat kernel, flags bits 12-13: run extents start on 1 / 4 / 8-unit boundaries
-constexpr uint32_t kFlagHeadCached = 1u << 14;  // flat kernel: a run's first row loads with the default cache policy
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -858,19 +857,10 @@ __global__ __launch_bounds__(kBlock) void csum_flat_kernel(const Queues Q, uint3
     };
     auto run_rsrc = [&](const Run& rn) { return rsrc(reinterpret_cast<const uint8_t*>(rn.F << 4), 16u * rn.ext); };
     // a chunk's loads: R <= U rows of 64 units
-    const bool head_cached = (flags & kFlagHeadCached) != 0;
     auto load = [&](const __amdgpu_buffer_rsrc_t& r, uint32_t g, auto& v) {
         constexpr int R = std::extent<std::remove_reference_t<decltype(v)>>::value;
-        // a run's first row holds the line it shares with the tile before
-        // (line-aligned run starts); loaded with the default policy, that
-        // tile's later read of the line can hit the caches
-        if (head_cached && g == 0) {
-            v[0] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(vo), 0, 0);
-        } else {
-            v[0] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(16u * g + vo), 0, kNT);
-        }
 #pragma unroll
-        for (int u = 1; u < R; ++u)
+        for (int u = 0; u < R; ++u)
             v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(16u * g + vo + 1024u * u), 0, kNT);
     };
 
@@ -1341,7 +1331,6 @@ struct Knobs {
     int out_policy = kOutPolicy;     // flat kernel: cache policy of the result stores (tile_store)
     int short_chunks = 1;            // flat kernel (no chunk in flight): a run's last chunk covers only its rows
     int run_align = kRunAlign;       // flat kernel: run extents start on 1 / 4 / 8-unit (16 / 64 / 128 B) boundaries
-    int head_cached = 0;             // flat kernel: a run's first row cached: 0 never, 1 always, 2 single-packet tiles
 };
 thread_local Knobs t_knobs;
 
@@ -1512,7 +1501,6 @@ void launch_flat(FlatKernel kern, hipStream_t s, Queues& Q, uint64_t n_total, ui
     flags |= static_cast<uint32_t>(K.out_policy) << kOutPolicyShift;
     if (!K.short_chunks) flags |= kFlagFullChunks;
     flags |= static_cast<uint32_t>(K.run_align == 8 ? 2 : (K.run_align == 4 ? 1 : 0)) << kRunAlignShift;
-    if (K.head_cached == 1 || (K.head_cached == 2 && B == 1)) flags |= kFlagHeadCached;
     kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(Q, static_cast<uint32_t>(B), heads, flags, rss);
 }
 
@@ -2171,12 +2159,6 @@ int sccsum_set_out_policy(int policy) {
 int sccsum_set_short_chunks(int on) {
     if (on != 0 && on != 1) return SCCSUM_EINVAL;
     sccsum::t_knobs.short_chunks = on;
-    return SCCSUM_OK;
-}
-
-int sccsum_set_head_cached(int mode) {
-    if (mode < 0 || mode > 2) return SCCSUM_EINVAL;
-    sccsum::t_knobs.head_cached = mode;
     return SCCSUM_OK;
 }
 

@@ -81,7 +81,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn[:tile_bytes[:tail_split[:tail_quarters[:out_policy[:short_chunks[:run_align[:head_cached]]]]]]]]]]]")
+    ap.add_argument("--variants", default="1,0", help="comma list of variant[:blocks_per_cu[:U[:tile[:dyn[:tile_bytes[:tail_split[:tail_quarters[:out_policy[:short_chunks[:run_align]]]]]]]]]]")
     ap.add_argument("--rotate", type=int, default=4, help="distinct copies of each batch, launched in turn")
     ap.add_argument("--cases", default="udp1500_frames,udp1500_spans,udp1500_frames_rss,zipf_spans,cfg3_zipf_frames,"
                                        "tcp64k_spans")
@@ -102,7 +102,7 @@ def main():
         turn = [0]
 
         def knobs(v):
-            parts = (v.split(":") + [""] * 12)[:12]
+            parts = (v.split(":") + [""] * 11)[:11]
             native.check(lib.sccsum_set_kernel_variant(int(parts[0])), "variant")
             native.check(lib.sccsum_set_blocks_per_cu(int(parts[1] or 8)), "blocks_per_cu")
             native.check(lib.sccsum_set_group_units(int(parts[2] or 0)), "group_units")
@@ -113,7 +113,6 @@ def main():
             native.check(lib.sccsum_set_out_policy(int(parts[8] or 1)), "out_policy")
             native.check(lib.sccsum_set_short_chunks(int(parts[9] or 1)), "short_chunks")
             native.check(lib.sccsum_set_run_align(int(parts[10] or 8)), "run_align")
-            native.check(lib.sccsum_set_head_cached(int(parts[11] or 0)), "head_cached")
 
         st_buf = torch.empty(max(b.n, 1), dtype=torch.uint8, device=dev)
 
@@ -167,7 +166,6 @@ def main():
     native.check(lib.sccsum_set_out_policy(1), "out_policy")
     native.check(lib.sccsum_set_short_chunks(1), "short_chunks")
     native.check(lib.sccsum_set_run_align(8), "run_align")
-    native.check(lib.sccsum_set_head_cached(0), "head_cached")
 
 
 if __name__ == "__main__":
