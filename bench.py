@@ -285,9 +285,9 @@ def cpu_baseline(tx, budget_s: float):
 
 
 def pmc_traffic(path: str | None, config: str, kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
-    summary for this config (tools/pmc_summary.py: profiles/rNN_pmc_<config>.json);
-    None when no summary exists."""
+    """(HBM bytes, algorithmic bytes) per launch of `kernel` from the newest
+    committed rocprofv3 PMC summary for this config (tools/prof_timed.py:
+    profiles/rNN_pmc_<config>.json), and its path; Nones when none exists."""
     cands = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", f"*pmc_{config}.json")))
     for p in reversed(cands):
         try:
@@ -296,8 +296,8 @@ def pmc_traffic(path: str | None, config: str, kernel: str):
             continue
         k = d.get("kernels", {}).get(kernel)
         if k and k.get("hbm_bytes_per_launch"):
-            return float(k["hbm_bytes_per_launch"]), os.path.relpath(p, REPO)
-    return None, None
+            return float(k["hbm_bytes_per_launch"]), k.get("alg_bytes_per_launch"), os.path.relpath(p, REPO)
+    return None, None, None
 
 
 class Launches:
@@ -366,12 +366,20 @@ def timed(step, steps, warmup, world, streams):
 
 
 def roofline(alg_bytes_launch: float, launch_s: float, config: str, kernel: str, sel: dict, args, extra=None):
-    traffic, src = pmc_traffic(args.pmc, config, "csum_flat_kernel")
+    traffic, prof_alg, src = pmc_traffic(args.pmc, config, "csum_flat_kernel")
+    scaled = None
+    if traffic is not None and prof_alg and abs(prof_alg - alg_bytes_launch) > 0.001 * alg_bytes_launch:
+        # the profile's launch had another size (a shorter batch, or the 65 535 B variant): its
+        # traffic per algorithmic byte, applied to this launch's algorithmic bytes
+        scaled = {"profile_alg_bytes_per_launch": int(prof_alg), "profile_hbm_bytes_per_launch": traffic}
+        traffic = round(traffic / prof_alg * alg_bytes_launch, 1)
     achieved = alg_bytes_launch / launch_s / 1e9
     d = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": src,
          "alg_bytes_per_launch": int(alg_bytes_launch), "avg_launch_us": round(launch_s * 1e6, 2),
          "trace_select": sel}
+    if scaled:
+        d["traffic_scaled_from"] = scaled
     if extra:
         d.update(extra)
     return d
