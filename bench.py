@@ -531,8 +531,8 @@ def run_tcp64k(args, world, rank, dev):
              world * n * seg * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": f"cfg4: {seg} B TCP segments + pseudo-header seed per segment, verify pass",
               "segments_per_gpu": n, "segment_bytes": seg, "parallelism": f"{world} independent shards"},
-             roofline(alg, launch_s, "tcp64k", kern + " (sccsum_spans)", sel, args,
-                      {"measured_read_ceiling_GBps": round(ceiling, 1), "read_ceiling_bytes": cbytes}))
+             roofline(alg, launch_s, "tcp64k" if seg == 65536 else f"tcp64k_seg{seg}", kern + " (sccsum_spans)",
+                      sel, args, {"measured_read_ceiling_GBps": round(ceiling, 1), "read_ceiling_bytes": cbytes}))
 
 
 def run_mixed(args, world, rank, dev):
@@ -607,7 +607,8 @@ def run_mixed(args, world, rank, dev):
                          else "one sccsum_ipv4_frames launch per step"),
               "rotation": f"{R} distinct batch {'pairs' if multi else 'sets'} launched in turn",
               "streams": f"{ns} (step k on stream k % {ns})", "parallelism": f"{world} independent shards"},
-             roofline(alg, launch_s, "mixed", kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi
+             roofline(alg, launch_s, "mixed" if align == 1 else f"mixed_align{align}",
+                      kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi
                                                       else " (sccsum_ipv4_frames)"), sel, args,
                       {"measured_read_ceiling_GBps": round(ceiling, 1)}))
 
