@@ -330,6 +330,9 @@ def make_streams(args, dev):
     return [torch.cuda.Stream(device=dev) for _ in range(ns)]
 
 
+OWN = {}  # this rank's own timing of the last timed() region (per_rank diagnostics)
+
+
 def timed(step, steps, warmup, world, streams):
     """Warm up, then time `steps` calls bracketed by barrier + sync; returns
     (max-over-ranks wall seconds, seconds per step from ONE pair of HIP events
@@ -362,7 +365,41 @@ def timed(step, steps, warmup, world, streams):
     t1 = time.perf_counter()  # this rank's end, before the closing barrier's own latency
     barrier(world)
     wall = max_over_ranks(t1 - t0, world)
+    OWN.update(wall_s=t1 - t0, step_s=e0.elapsed_time(e1) / 1e3 / steps)
     return wall, e0.elapsed_time(e1) / 1e3 / steps
+
+
+def device_id(dev) -> dict:
+    """Which GPU a rank ran on: its index and PCI address (so a slow device
+    or box shows up by name in a multi-GPU line)."""
+    if dev is None:
+        return {"device": None, "pci_bus_id": None}
+    p = torch.cuda.get_device_properties(dev)
+    return {"device": dev.index, "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0",
+            "device_name": p.name}
+
+
+def per_rank(world, rank, dev, **fields):
+    """Every rank's own figures — device, wall time, rate, average launch,
+    read ceiling — gathered on rank 0 with one all_gather_object, so an N > 1
+    line shows a slow rank or device beside the max-over-ranks `value`
+    (reference analogue: independent per-shard engines, src/net/net.cc:309-341).
+    Collective: every rank calls it."""
+    me = {"rank": rank, "host": socket.gethostname(), **device_id(dev),
+          **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in fields.items()}}
+    if world == 1:
+        return [me]
+    import torch.distributed as dist
+
+    out = [None] * world
+    dist.all_gather_object(out, me)
+    return out
+
+
+def rank_rate(nbytes_per_step, steps):
+    """This rank's own GiB/s and launch figures from its last timed() region."""
+    return {"wall_s": OWN["wall_s"], "GiBps": nbytes_per_step * steps / OWN["wall_s"] / 2**30,
+            "ms_per_step": OWN["wall_s"] / steps * 1e3}
 
 
 def roofline(alg_bytes_launch: float, launch_s: float, config: str, kernel: str, sel: dict, args, extra=None):
@@ -485,6 +522,8 @@ def run_udp1500(args, world, rank, dev):
     rx_out = 4 if (args.rx_out2 or not multi) else 0
     alg = (n * (FRAME + META_BYTES + 4) + n * (FRAME + META_BYTES + 1 + rx_out)) // per_step
     ceiling = read_ceiling(txs[0].data, txs[0].bytes_len, stream)
+    ranks = per_rank(world, rank, dev, **rank_rate(2 * n * FRAME, args.steps), avg_launch_us=avg_launch_s * 1e6,
+                     read_ceiling_GBps=ceiling, frac=alg / avg_launch_s / 1e9 / HBM_PEAK_GBPS)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(txs[0], args.cpu_seconds)
@@ -500,7 +539,7 @@ def run_udp1500(args, world, rank, dev):
               "global_batch": n * world, "parallelism": f"{world} independent shards, no collective"},
              roofline(alg, avg_launch_s, "udp1500", kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi
                                                                    else " (sccsum_ipv4_frames)"), sel, args,
-                      {"measured_read_ceiling_GBps": round(ceiling, 1)}), cpu)
+                      {"measured_read_ceiling_GBps": round(ceiling, 1)}), cpu, extra={"per_rank": ranks})
 
 
 def run_tcp64k(args, world, rank, dev):
@@ -526,13 +565,16 @@ def run_tcp64k(args, world, rank, dev):
     alg = n * (seg + META_BYTES + 4 + 2 + 1)  # + seed in, result + status out
     cbytes = min(b.bytes_len, 16 << 30)
     ceiling = read_ceiling(b.data, cbytes, stream, reps=3)
+    ranks = per_rank(world, rank, dev, **rank_rate(n * seg, args.steps), avg_launch_us=launch_s * 1e6,
+                     read_ceiling_GBps=ceiling, frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS)
     if rank == 0:
         emit("GiB/s device-resident Internet checksum, 64 KiB TCP segments (cfg 4)",
              world * n * seg * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": f"cfg4: {seg} B TCP segments + pseudo-header seed per segment, verify pass",
               "segments_per_gpu": n, "segment_bytes": seg, "parallelism": f"{world} independent shards"},
              roofline(alg, launch_s, "tcp64k" if seg == 65536 else f"tcp64k_seg{seg}", kern + " (sccsum_spans)",
-                      sel, args, {"measured_read_ceiling_GBps": round(ceiling, 1), "read_ceiling_bytes": cbytes}))
+                      sel, args, {"measured_read_ceiling_GBps": round(ceiling, 1), "read_ceiling_bytes": cbytes}),
+             extra={"per_rank": ranks})
 
 
 def run_mixed(args, world, rank, dev):
@@ -594,6 +636,8 @@ def run_mixed(args, world, rank, dev):
     alg = (total + n * (META_BYTES + 4) + n * (META_BYTES + 1 + (4 if args.rx_out2 else 0)) if multi
            else total + n * (META_BYTES + 4))
     ceiling = read_ceiling(rxs[0].data, rxs[0].bytes_len, stream)
+    ranks = per_rank(world, rank, dev, **rank_rate(nbytes, args.steps), avg_launch_us=launch_s * 1e6,
+                     read_ceiling_GBps=ceiling, frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS)
     if rank == 0:
         emit("GiB/s device-resident Internet checksum, mixed-MTU Zipf batches (cfg 3)",
              world * nbytes * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
@@ -610,7 +654,7 @@ def run_mixed(args, world, rank, dev):
              roofline(alg, launch_s, "mixed" if align == 1 else f"mixed_align{align}",
                       kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi
                                                       else " (sccsum_ipv4_frames)"), sel, args,
-                      {"measured_read_ceiling_GBps": round(ceiling, 1)}))
+                      {"measured_read_ceiling_GBps": round(ceiling, 1)}), extra={"per_rank": ranks})
 
 
 def run_slots(args, world, rank, dev):
@@ -652,6 +696,8 @@ def run_slots(args, world, rank, dev):
                                  sts[r], n, FRAME) for r in range(R)}
     wall, launch_s = timed(lambda k: pre[k % R](stream), args.steps, warm, world, stream)
     alg = n * (FRAME + META_BYTES + 1)  # frame bytes + metadata + 1 status byte (verify only)
+    ranks = per_rank(world, rank, dev, **rank_rate(n * FRAME, args.steps), avg_launch_us=launch_s * 1e6,
+                     frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS)
     if rank == 0:
         emit("GiB/s device-resident Internet checksum, 1500 B frames in mbuf-shaped slots (sparse layout)",
              world * n * FRAME * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
@@ -659,7 +705,8 @@ def run_slots(args, world, rank, dev):
                           "verify only (status bits)",
               "packets_per_gpu": n, "rotation": f"{R} distinct batches launched in turn",
               "parallelism": f"{world} independent shards"},
-             roofline(alg, launch_s, "slots", kern + " (sccsum_ipv4_frames, sparse layout -> row kernel)", sel, args))
+             roofline(alg, launch_s, "slots", kern + " (sccsum_ipv4_frames, sparse layout -> row kernel)", sel, args),
+             extra={"per_rank": ranks})
 
 
 def run_frags(args, world, rank, dev):
@@ -708,6 +755,7 @@ def run_frags(args, world, rank, dev):
     LAUNCHES.add(kern, warm)
     sel = LAUNCHES.select(kern, args.steps)
     wall, launch_s = timed(lambda k_: pre[k_ % R](stream), args.steps, warm, world, stream)
+    own = rank_rate(n * pkt, args.steps)
     # the same fragments through the fragment-list kernel (one wave per packet, fragments where they lie)
     desc = []
     for pool in pools:
@@ -725,6 +773,7 @@ def run_frags(args, world, rank, dev):
              for r in range(R)]
     _, desc_s = timed(lambda k_: pre_d[k_ % R](stream), max(4, args.steps // 2), R, world, stream)
     alg = n * (pkt + nf * 12 + 4 + 4 + 2)  # packet bytes + fragment (offset, length) + first + seed + result
+    ranks = per_rank(world, rank, dev, **own, avg_launch_us=launch_s * 1e6, frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS)
     if rank == 0:
         emit("GiB/s device-resident Internet checksum, 9000 B jumbo packets as 5-fragment mbuf chains (f1)",
              world * n * pkt * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
@@ -735,7 +784,7 @@ def run_frags(args, world, rank, dev):
              roofline(alg, launch_s, "frags", kern + " + frag_combine_kernel (sccsum_fragments)", sel, args,
                       {"trace_select_extra": [{"kernel": "frag_combine_kernel", "skip": sel["skip"],
                                                "count": sel["count"]}]}),
-             extra={"fragment_list_kernel": {"us_per_call": round(desc_s * 1e6, 2),
+             extra={"per_rank": ranks, "fragment_list_kernel": {"us_per_call": round(desc_s * 1e6, 2),
                                              "GiBps_packet_bytes": round(n * pkt / desc_s / 2**30, 1),
                                              "note": "sccsum_spans_desc over the same HBM fragments"}})
 
@@ -771,6 +820,8 @@ def run_fill(args, world, rank, dev):
            for r in range(R) for i in range(ns)}
     wall, launch_s = timed(lambda k: pre[(k % R, k % ns)](streams[k % ns]), args.steps, warm, world, streams)
     alg = n * (FRAME + META_BYTES + 4)  # read every byte + metadata, write the two 2-byte fields
+    ranks = per_rank(world, rank, dev, **rank_rate(n * FRAME, args.steps), avg_launch_us=launch_s * 1e6,
+                     frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS)
     if rank == 0:
         emit("GiB/s device-resident Internet checksum, 1500B-packet batches, in-place generate (cfg 2 tx)",
              world * n * FRAME * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
@@ -780,7 +831,7 @@ def run_fill(args, world, rank, dev):
              roofline(alg, launch_s, "fill", kern + " + fill_store_kernel (sccsum_ipv4_fill: generate pass, "
                                                     "then the field-store pass)", sel, args,
                       {"trace_select_extra": [{"kernel": "fill_store_kernel", "skip": sel["skip"],
-                                               "count": sel["count"]}]}))
+                                               "count": sel["count"]}]}), extra={"per_rank": ranks})
 
 
 def run_sweep(args, world, rank, dev):
@@ -892,7 +943,7 @@ def run_e2e(args, world, rank, dev):
     length = np.full(n, FRAME, dtype=np.uint32)
     del tx
     torch.cuda.empty_cache()
-    res = {}
+    res, own_rates = {}, {}
     for name, gather, chunk_bytes in (("A_slots_as_is", native.GATHER_NONE, 65536 * pipeline.MBUF_SLOT),
                                       ("B_gathered", native.GATHER_HOST, 65536 * FRAME),
                                       ("C_strided_dma", native.GATHER_STRIDED, 65536 * ((FRAME + 15) & ~15)),
@@ -900,17 +951,22 @@ def run_e2e(args, world, rank, dev):
         pl = pipeline.HostPipeline(dev.index or 0, chunk_bytes=chunk_bytes, chunk_packets=65536, depth=3)
         got = pl.run(native.PIPE_IPV4, pool, off, length, gather=gather, max_len=FRAME)
         assert np.array_equal(got, want), f"e2e {name} mismatch vs device-resident results"
-        times = []
+        times, own = [], []
         for _ in range(max(1, args.steps // 4)):
             barrier(world)  # every rank's batch crosses its own PCIe link at the same time
             t0 = time.perf_counter()
             pl.run(native.PIPE_IPV4, pool, off, length, gather=gather, max_len=FRAME)
-            times.append(max_over_ranks(time.perf_counter() - t0, world))
+            own.append(time.perf_counter() - t0)
+            times.append(max_over_ranks(own[-1], world))
         pl.close()
         t = float(np.median(times))  # median over runs of the slowest rank's time
         pcie = n * (pipeline.MBUF_SLOT if gather == native.GATHER_NONE else FRAME) + n * (12 + 4)
         res[name] = {"GiBps_packet_bytes": round(n * FRAME / t / 2**30, 2), "ms_per_batch": round(t * 1e3, 2),
                      "pcie_GBps_h2d_plus_d2h": round(pcie / t / 1e9, 2)}
+        to = float(np.median(own))
+        own_rates[name] = {"GiBps_packet_bytes": round(n * FRAME / to / 2**30, 2),
+                           "pcie_GBps_h2d_plus_d2h": round(pcie / to / 1e9, 2)}
+    ranks = per_rank(world, rank, dev, variants=own_rates)
     if rank == 0:
         best = max(res.values(), key=lambda r: r["GiBps_packet_bytes"])
         emit("GiB/s Internet checksum incl. PCIe: pinned mbuf-shaped host buffers -> HBM -> host (cfg 5)",
@@ -918,7 +974,7 @@ def run_e2e(args, world, rank, dev):
              {"workload": "cfg5: 1,048,576 x 1500 B IPv4/UDP frames in 2304-B mbuf slots (pinned), "
                           "H2D + kernel + D2H of 4 B/frame (or the kernel reading the slots in place), 3-deep "
                           "pipeline, 64Ki-frame chunks; value = the best variant",
-              "parallelism": f"{world} independent shards"}, extra={"variants": res})
+              "parallelism": f"{world} independent shards"}, extra={"variants": res, "per_rank": ranks})
 
 
 def run_dry(args, world, rank):
@@ -933,8 +989,11 @@ def run_dry(args, world, rank):
     ranks = [None] * world
     if world > 1:
         dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid(), "local": os.environ.get("LOCAL_RANK")})
+    # the per_rank block of a real line, with the figures a device-less rank has
+    pr = per_rank(world, rank, None, wall_s=time.perf_counter() - t0, GiBps=None, avg_launch_us=None,
+                  read_ceiling_GBps=None)
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "ranks": ranks,
+        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "ranks": ranks, "per_rank": pr,
                           "barrier_s": round(wall, 6)}), flush=True)
 
 

@@ -41,16 +41,24 @@
  *   - d_bytes must be 16-byte aligned, d_off 8-byte aligned, d_len/d_seed/d_out2 4-byte aligned,
  *     d_out 2-byte aligned.
  *   - Launches are asynchronous on `stream` (a hipStream_t; NULL = the
- *     device's null stream), one kernel each.  No allocation on the launch
- *     path (a stream's first launch may allocate its 16 KiB of tile
- *     counters once), no host synchronisation: the calls are safe inside
- *     hipStreamBeginCapture.  Any number of launches may be in flight: each
- *     stream has its own tile counters (launches on one stream run in order);
- *     captured launches, and streams beyond the first 4096 of a device, use a
- *     static tile order instead (same results).
+ *     device's null stream), one kernel each (two for in-place fill and
+ *     fragment lists).  No allocation, no memset and no host synchronisation
+ *     on the launch path — sccsum_init allocates the device's pool of tile
+ *     counters once — so the calls are safe inside hipStreamBeginCapture
+ *     (global or relaxed mode) and never stall another stream.  Any number
+ *     of launches may be in flight, on any streams: a launch takes a counter
+ *     slot no unfinished launch holds, and the kernel itself reports when it
+ *     is done with it (streams may be created and destroyed freely; a
+ *     destroyed stream's address reused by a new stream shares nothing).
+ *     Captured launches, and launches that find no free slot, use a static
+ *     tile order instead (same results, without the dynamic balance).
  *
- * Threading: one host thread per device (Seastar's shard-per-core model).
- * Calls are re-entrant per stream.
+ * Threading: Seastar's model — one reactor thread per shard, all of them
+ * on one device or each on its own — is supported: any number of host
+ * threads may call concurrently, each on its own streams (the counter pool
+ * is shared under a per-device lock held for a few ring probes per launch).
+ * Diagnostic knobs (sccsum_diag.h) are per thread.  A burst queue or a
+ * pipeline object belongs to one thread.
  */
 #ifndef SCCSUM_H
 #define SCCSUM_H
@@ -62,7 +70,11 @@
 extern "C" {
 #endif
 
-#define SCCSUM_ABI_VERSION 1
+/* 2 (round 3): frames leave IP fragments' L4 alone (SCCSUM_ST_IPFRAG), L4
+ * values of protocols other than TCP / UDP carry no pseudo-header, fill gained
+ * SCCSUM_FILL_ICMP_ECHO and needs d_out2 with SCCSUM_FILL_L4 (INTEGRATION.md,
+ * "Migration from ABI 1"). */
+#define SCCSUM_ABI_VERSION 2
 
 #define SCCSUM_OK 0
 #define SCCSUM_EINVAL (-1)   /* bad argument (null pointer, misalignment) */
@@ -72,8 +84,12 @@ extern "C" {
 /* per-packet status bits (d_status) */
 #define SCCSUM_ST_OK        0x01u /* spans: result == 0; frames: IPv4 header verifies */
 #define SCCSUM_ST_L4_OK     0x02u /* frames: L4 (pseudo-header + segment) verifies */
-#define SCCSUM_ST_MALFORMED 0x04u /* frames: len < 20, len < ip total length, or 4*ihl > ip length */
+#define SCCSUM_ST_MALFORMED 0x04u /* frames: len < 20, len < ip total length, 4*ihl > ip length, or
+                                     fragment offset + ip length > 65535 (ip.cc:115-144: dropped) */
 #define SCCSUM_ST_RANGE     0x08u /* [off, off+len) outside the byte buffer: not read */
+#define SCCSUM_ST_IPFRAG    0x10u /* frames: an IP fragment (MF set or fragment offset != 0, ip.hh:400-402):
+                                     its L4 value is not computed (0, never SCCSUM_ST_L4_OK) — the
+                                     reference sums L4 over the reassembled datagram only (ip.cc:164-220) */
 
 /* ABI version of the loaded library (== SCCSUM_ABI_VERSION it was built with). */
 int sccsum_abi_version(void);
@@ -85,10 +101,11 @@ const char* sccsum_strerror(int err);
 int sccsum_device_count(int* count);
 
 /* Bind the calling host thread to `device` (hipSetDevice), cache its
- * compute-unit count for launch sizing and enable the per-stream tile
- * counters the flat kernel dequeues from.  Call it on every thread that
- * launches; launches on a device nobody initialised use the static tile
- * order (same results). */
+ * compute-unit count for launch sizing and, on the device's first call,
+ * allocate its pool of tile counters (2048 slots, 34 MB of HBM, plus 8 KiB
+ * of pinned memory the kernels report completion to; zeroed, synchronously).
+ * Call it on every thread that launches; launches on a device nobody
+ * initialised use the static tile order (same results). */
 int sccsum_init(int device);
 
 /* Pseudo-header partial sum exactly as ipv4_traits::*_pseudo_header_checksum
@@ -108,11 +125,19 @@ int sccsum_spans(const void* d_bytes, uint64_t bytes_len,
                  uint16_t* d_out, uint8_t* d_status, uint64_t n, uint32_t max_len,
                  void* stream);
 
-/* Checksum n IPv4 frames (IPv4 header first, no Ethernet header).
- *   d_out2[2i]   = IPv4 header checksum over 20 bytes
- *   d_out2[2i+1] = L4 checksum over [4*ihl, min(ip_len, len)) seeded with the
- *                  pseudo-header (src, dst, proto from the header; length =
- *                  that L4 span's length as uint16_t)
+/* Checksum n IPv4 frames (IPv4 header first, no Ethernet header), as the rx
+ * path ipv4::handle_received_packet (ip.cc:114-229) takes them.
+ *   d_out2[2i]   = IPv4 header checksum over 20 bytes (ip.cc:121-127; checked
+ *                  on every frame, fragments included)
+ *   d_out2[2i+1] = L4 checksum over [4*ihl, min(ip_len, len)): for TCP (6) and
+ *                  UDP (17) seeded with the pseudo-header (src, dst, proto from
+ *                  the header; length = that L4 span's length as uint16_t:
+ *                  tcp.hh:876-883, udp.cc:184-195); for ICMP and every other
+ *                  protocol the plain sum, no pseudo-header (ip.cc:471-474);
+ *                  0 for an IP fragment (SCCSUM_ST_IPFRAG): the reference
+ *                  checks L4 only on the reassembled datagram — sum that with
+ *                  sccsum_spans_desc over the fragments' payloads and the
+ *                  pseudo-header seed ("Fragments")
  *   For generate, pass frames whose checksum fields are zero and store the
  *   outputs; for verify, pass received frames and test the status bits.
  *   d_status may be NULL.  max_len as for sccsum_spans.
@@ -206,23 +231,32 @@ int sccsum_ipv4_frames_rss(const void* d_bytes, uint64_t bytes_len, const uint64
 #define SCCSUM_FILL_L4_PSEUDO 0x04u /* tx-offload partial: the folded pseudo-header alone, i.e. the
                                        reference's `~csum.get()` (udp.cc:188-189, tcp.hh:1688-1689) */
 #define SCCSUM_FILL_TSO       0x08u /* with L4_PSEUDO: TCP pseudo-header length 0 (tcp.hh:1674-1676) */
+#define SCCSUM_FILL_ICMP_ECHO 0x10u /* ICMP echo request -> echo reply in place: type 0, code 0, checksum
+                                       over the ICMP message, no pseudo-header (icmp::received,
+                                       ip.cc:464-474); other ICMP types are left alone */
 
 /* GENERATE checksums for n IPv4 frames and STORE them in the frames, in
  * place: wire-ready frames, the tx half of the native stack.  Each checksum
  * is computed as if its own field were zero, as the reference does (fresh
  * headers are value-initialised, packet.hh:586-589; ip.cc:270), so the
  * fields' current contents do not matter.  The L4 field is UDP +6 / TCP +16
- * after 4*ihl; other protocols' L4 is left alone, as is any frame that is
- * malformed (as in sccsum_ipv4_frames) or too short to hold the field.
+ * (ICMP +2 with SCCSUM_FILL_ICMP_ECHO) after 4*ihl; other protocols' L4 is
+ * left alone, as is any frame that is malformed (as in sccsum_ipv4_frames) or
+ * too short to hold the field.  An IP fragment gets the IP header checksum
+ * only (ipv4::send checksums each fragment's header, ip.cc:256-278, after the
+ * L4 writer summed the whole datagram, ip.cc:283-294): its L4 bytes — the
+ * first fragment's L4 header, a later fragment's payload — are never written.
  *   mode: SCCSUM_FILL_IP and/or one of SCCSUM_FILL_L4 / SCCSUM_FILL_L4_PSEUDO
- *         (| SCCSUM_FILL_TSO).  FILL_L4 reads every byte (the flat kernel
- *         generates into d_out2, then a second pass stores the fields); the
- *         others read only the 20-byte header.
+ *         (| SCCSUM_FILL_TSO), and/or SCCSUM_FILL_ICMP_ECHO (not with
+ *         L4_PSEUDO).  FILL_L4 and FILL_ICMP_ECHO read every byte (the flat
+ *         kernel generates into d_out2, then a second pass stores the
+ *         fields); the others read only the 20-byte header.
  *   d_out2[2i] / [2i+1] = the IP / L4 values stored (0 where nothing was
- *         stored); REQUIRED with SCCSUM_FILL_L4 (the two passes hand the
- *         values over in it), else may be NULL.
+ *         stored); REQUIRED with SCCSUM_FILL_L4 or SCCSUM_FILL_ICMP_ECHO (the
+ *         two passes hand the values over in it), else may be NULL.
  *   d_status[i] = SCCSUM_ST_OK if the IP field was written, SCCSUM_ST_L4_OK
- *         if the L4 field was written, plus MALFORMED / RANGE; may be NULL.
+ *         if the L4 field was written, plus MALFORMED / RANGE / IPFRAG; may
+ *         be NULL.
  * Frames must not overlap each other. */
 int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len,
                      const uint64_t* d_off, const uint32_t* d_len,

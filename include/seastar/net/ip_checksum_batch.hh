@@ -56,6 +56,7 @@ enum class checksum_status : uint8_t {
     l4_ok = SCCSUM_ST_L4_OK,         // frames: TCP/UDP checksum verifies
     malformed = SCCSUM_ST_MALFORMED, // frames: shorter than 20 B / than the IP length, bad ihl
     out_of_range = SCCSUM_ST_RANGE,  // span outside the byte buffer (not read)
+    ip_fragment = SCCSUM_ST_IPFRAG,  // frames: MF or offset set — L4 is checked after reassembly (ip.cc:164-220)
 };
 
 class batch_checksummer {
@@ -95,9 +96,11 @@ public:
               "sccsum_ipv4_frames");
     }
 
-    // Generate IPv4 header and/or TCP/UDP checksums and store them into the
-    // frames (mode: SCCSUM_FILL_*; d_status may be null; d_out2 may be null
-    // except with SCCSUM_FILL_L4, whose two passes hand the values over in it).
+    // Generate IPv4 header and/or TCP/UDP checksums (ICMP echo replies with
+    // SCCSUM_FILL_ICMP_ECHO) and store them into the frames (mode:
+    // SCCSUM_FILL_*; d_status may be null; d_out2 may be null except with
+    // SCCSUM_FILL_L4 / SCCSUM_FILL_ICMP_ECHO, whose two passes hand the values
+    // over in it).  IP fragments get their IPv4 header checksum only.
     void ipv4_fill(const device_packet_batch& b, uint32_t mode, uint16_t* d_out2, uint8_t* d_status,
                    void* stream) const {
         check(sccsum_ipv4_fill(const_cast<void*>(b.bytes), b.bytes_len, b.off, b.len, d_out2, d_status, b.n,

@@ -149,15 +149,57 @@ static void one_span(const uint8_t* bytes, const uint64_t* off, const uint32_t* 
     out[i] = oracle_get(&c);
 }
 
-/* One IPv4 frame, following the rx path src/net/ip.cc:114-140, 220-225
- * (header checksum over sizeof(ip_hdr)=20 B, drop if shorter than the IP
- * total length, trim beyond it, strip 4*ihl) and the L4 checksum of
- * include/seastar/net/tcp.hh:876-883 / src/net/udp.cc:184-195. */
+/* IPv4 header fields the rx path decodes (ip_hdr, include/seastar/net/ip.hh:381-403). */
+typedef struct {
+    uint32_t ihl, ip_len, proto, l4_off, l4_len;
+    int frag;      /* MF set or fragment offset != 0 (ip.hh:400-402, ip.cc:165-166) */
+    uint8_t st;    /* MALFORMED / IPFRAG bits */
+} frame_info;
+
+/* The length / fragment checks of ipv4::handle_received_packet
+ * (src/net/ip.cc:129-144, 165-166) for a frame of n >= 20 bytes. */
+static frame_info decode_frame(const uint8_t* p, uint32_t n) {
+    frame_info f;
+    f.st = 0;
+    f.ihl = p[0] & 0xf;
+    f.ip_len = ((uint32_t)p[2] << 8) | p[3];
+    f.proto = p[9];
+    f.l4_off = 4 * f.ihl;
+    const uint32_t fragw = ((uint32_t)p[6] << 8) | p[7];
+    const uint32_t offset = (fragw & 0x1fff) * 8; /* ip_hdr::offset(): frag << 3, 16 bits (ip.hh:402) */
+    f.frag = (fragw & 0x3fff) != 0;               /* mf() (0x2000) or offset != 0 */
+    const uint32_t l4_end = f.ip_len < n ? f.ip_len : n;
+    if (n < f.ip_len) f.st |= 4; /* :137-139 drop when shorter than the IP length (:134-136 trim when longer) */
+    if (offset + l4_end > 65535) f.st |= 4; /* :141-144 (net::ip_packet_len_max, const.hh:42) */
+    f.l4_len = 0;
+    if (f.l4_off > l4_end) {
+        f.st |= 4; /* the 4*ihl strip (:225) would run past the datagram */
+    } else {
+        f.l4_len = l4_end - f.l4_off;
+    }
+    if (f.frag) f.st |= 16;
+    return f;
+}
+
+/* One received IPv4 frame, following ipv4::handle_received_packet
+ * (src/net/ip.cc:114-229) and the L4 receivers it hands the datagram to:
+ *   :115-118   get_header<ip_hdr>(0): a frame shorter than 20 B     -> MALFORMED
+ *   :121-127   header checksum over sizeof(ip_hdr) = 20 B           -> out2[2i], bit0
+ *   :129-144   length checks (decode_frame)                          -> MALFORMED
+ *   :164-220   MF set or offset != 0: the fragment goes to reassembly and no
+ *              L4 checksum is computed on it — only on the reassembled
+ *              datagram, whose IP header is not checked again (:120-121,
+ *              :456-460)                                             -> IPFRAG, out2[2i+1] = 0
+ *   :222-227   otherwise [4*ihl, ip_len) goes to the L4 receiver:
+ *              TCP verifies pseudo-header + segment (tcp.hh:876-883);
+ *              UDP's value is the same sum (what udp.cc:184-195 generates;
+ *              its rx does not verify, udp.cc:164-173); ICMP and any other
+ *              protocol: the plain sum, no pseudo-header (ip.cc:471-474)
+ *                                                                    -> out2[2i+1], bit1 */
 static void one_ipv4(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                      uint16_t* out2, uint8_t* status, uint64_t i) {
     const uint8_t* p = bytes + off[i];
     uint32_t n = len[i];
-    uint8_t st = 0;
     if (n < 20) {
         out2[2 * i] = 0;
         out2[2 * i + 1] = 0;
@@ -165,29 +207,22 @@ static void one_ipv4(const uint8_t* bytes, const uint64_t* off, const uint32_t* 
         return;
     }
     uint16_t ipc = oracle_ip_checksum(p, 20);
-    uint32_t ihl = p[0] & 0xf;
-    uint32_t ip_len = ((uint32_t)p[2] << 8) | p[3];
-    uint8_t proto = p[9];
-    uint32_t src = rd_be32(p + 12);
-    uint32_t dst = rd_be32(p + 16);
-    uint32_t l4_off = 4 * ihl;
-    uint32_t l4_end = ip_len < n ? ip_len : n;
-    if (n < ip_len) st |= 4;
-    uint32_t l4_len = 0;
-    if (l4_off > l4_end) {
-        st |= 4;
-    } else {
-        l4_len = l4_end - l4_off;
+    const frame_info f = decode_frame(p, n);
+    uint8_t st = f.st;
+    uint16_t l4c = 0;
+    if (!f.frag) {
+        oracle_checksummer c;
+        oracle_init(&c);
+        if (f.proto == 6 || f.proto == 17) {
+            oracle_pseudo_header(&c, rd_be32(p + 12), rd_be32(p + 16), (uint8_t)f.proto, (uint16_t)f.l4_len);
+        }
+        oracle_sum_bytes(&c, p + f.l4_off, f.l4_len);
+        l4c = oracle_get(&c);
+        if (l4c == 0) st |= 2;
     }
-    oracle_checksummer c;
-    oracle_init(&c);
-    oracle_pseudo_header(&c, src, dst, proto, (uint16_t)l4_len);
-    oracle_sum_bytes(&c, p + l4_off, l4_len);
-    uint16_t l4c = oracle_get(&c);
     out2[2 * i] = ipc;
     out2[2 * i + 1] = l4c;
     if (ipc == 0) st |= 1;
-    if (l4c == 0) st |= 2;
     if (status) status[i] = st;
 }
 
@@ -275,40 +310,48 @@ void oracle_batch_ipv4_fill(uint8_t* bytes, const uint64_t* off, const uint32_t*
         if (L < 20) {
             st = 4;
         } else {
-            uint32_t ihl = p[0] & 0xf;
-            uint32_t ip_len = ((uint32_t)p[2] << 8) | p[3];
-            uint8_t proto = p[9];
-            uint32_t l4_off = 4 * ihl;
-            uint32_t l4_end = ip_len < L ? ip_len : L;
-            uint32_t l4_len = 0;
-            if (L < ip_len) st |= 4;
-            if (l4_off > l4_end) {
-                st |= 4;
-            } else {
-                l4_len = l4_end - l4_off;
-            }
-            if (mode & 1) {
+            const frame_info f = decode_frame(p, L);
+            st = f.st;
+            const uint8_t proto = (uint8_t)f.proto;
+            if (mode & 1) { /* every frame, fragments included: ipv4::send's send_pkt per fragment, ip.cc:256-278 */
                 p[10] = p[11] = 0;
                 ipw = oracle_ip_checksum(p, 20);
                 memcpy(p + 10, &ipw, 2);
                 st |= 1;
             }
+            /* L4 writers never touch a fragment: the reference sums the whole
+             * datagram before ipv4::send cuts it (udp.cc:184-195 / tcp.hh:1656-1694
+             * run first, ip.cc:283-294 fragments after) */
+            const int atomic = !f.frag && !(st & 4);
             uint32_t fo = proto == 17 ? 6 : (proto == 6 ? 16 : 0);
-            if ((mode & 6) && fo && l4_len >= fo + 2 && !(st & 4)) {
-                uint8_t* field = p + l4_off + fo;
+            if ((mode & 6) && fo && atomic && f.l4_len >= fo + 2) {
+                uint8_t* field = p + f.l4_off + fo;
                 oracle_checksummer c;
                 oracle_init(&c);
                 if (mode & 2) {
                     field[0] = field[1] = 0;
-                    oracle_pseudo_header(&c, rd_be32(p + 12), rd_be32(p + 16), proto, (uint16_t)l4_len);
-                    oracle_sum_bytes(&c, p + l4_off, l4_len);
+                    oracle_pseudo_header(&c, rd_be32(p + 12), rd_be32(p + 16), proto, (uint16_t)f.l4_len);
+                    oracle_sum_bytes(&c, p + f.l4_off, f.l4_len);
                     l4w = oracle_get(&c);
                 } else {
-                    uint32_t plen = ((mode & 8) && proto == 6) ? 0 : l4_len;
+                    uint32_t plen = ((mode & 8) && proto == 6) ? 0 : f.l4_len;
                     oracle_pseudo_header(&c, rd_be32(p + 12), rd_be32(p + 16), proto, (uint16_t)plen);
                     l4w = (uint16_t)~oracle_get(&c);
                 }
                 memcpy(field, &l4w, 2);
+                st |= 2;
+            }
+            /* icmp::received (ip.cc:464-474): get_header<icmp_hdr>(0) needs the
+             * 8-byte header (ip.hh:143-156); an echo request becomes the reply
+             * in place: type echo_reply, code 0, csum 0, sum over p.len() (the
+             * message after the 4*ihl strip), csum = get() */
+            uint8_t* ih = p + f.l4_off;
+            if ((mode & 16) && proto == 1 && atomic && f.l4_len >= 8 && ih[0] == 8) {
+                ih[0] = 0;
+                ih[1] = 0;
+                ih[2] = ih[3] = 0;
+                l4w = oracle_ip_checksum(ih, f.l4_len);
+                memcpy(ih + 2, &l4w, 2);
                 st |= 2;
             }
         }

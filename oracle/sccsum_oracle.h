@@ -64,13 +64,18 @@ void oracle_pseudo_header(oracle_checksummer* c, uint32_t src_host, uint32_t dst
 void oracle_batch_spans(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                         const uint32_t* seed, uint16_t* out, uint64_t n, int nthreads);
 
-/* IPv4 frames starting at bytes+off[i] with len[i] bytes:
+/* IPv4 frames starting at bytes+off[i] with len[i] bytes, as the rx path
+ * src/net/ip.cc:114-229 takes them:
  *   out[2i]   = IPv4 header checksum over exactly 20 B (ip.cc:121-127, 271-277)
- *   out[2i+1] = L4 checksum of [4*ihl, ip_len) seeded with the pseudo-header
- *               (tcp.hh:876-883 verify / udp.cc:184-195 generate)
- *   status[i] bit0 = IP sum verifies (== 0), bit1 = L4 sum verifies,
- *             bit2 = malformed (len < 20, len < ip_len, 4*ihl > ip_len)
- *   (ip.cc:114-140 drop rules). status may be NULL. */
+ *   out[2i+1] = L4 checksum of [4*ihl, min(ip_len, len)): TCP / UDP seeded with
+ *               the pseudo-header (tcp.hh:876-883 verify / udp.cc:184-195
+ *               generate), any other protocol without (ICMP, ip.cc:471-474);
+ *               0 for an IP fragment (reassembly first, ip.cc:164-220)
+ *   status[i] bit0 = IP sum verifies (== 0), bit1 = L4 sum verifies (never for
+ *             a fragment), bit2 = malformed (len < 20, len < ip_len, 4*ihl >
+ *             ip_len, fragment offset + ip_len > 65535: ip.cc:115-144),
+ *             bit4 = IP fragment (MF set or offset != 0, ip.cc:165-166).
+ *   status may be NULL. */
 void oracle_batch_ipv4(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                        uint16_t* out2, uint8_t* status, uint64_t n, int nthreads);
 
@@ -82,14 +87,20 @@ void oracle_batch_fragments(const uint8_t* bytes, const uint64_t* frag_off, cons
 
 /* Tx generate, in place, for IPv4 frames (the writers the reference runs on
  * fresh, zero-checksum headers):
- *   mode & 1: iph->csum = 0; csum.sum(iph, 20); iph->csum = get()      ip.cc:270-276
- *   mode & 2: L4 field = 0; pseudo-header + csum.sum(segment); get()    udp.cc:186,192-193 / tcp.hh:1683,1691-1694
- *   mode & 4: L4 field = ~get() of the pseudo-header alone (tx offload) udp.cc:188-189 / tcp.hh:1688-1689
- *   mode & 8: with 4, TCP pseudo-header length 0 (TSO)                  tcp.hh:1674-1676
- * L4 field: UDP +6, TCP +16 after 4*ihl; written only for proto 17/6, when
- * the frame is not malformed (as oracle_batch_ipv4) and the segment holds the
- * field.  out2 (may be NULL) gets the values stored (0 = none); status bit0 =
- * IP stored, bit1 = L4 stored, bit2 malformed, bit3 never (no range checks). */
+ *   mode & 1:  iph->csum = 0; csum.sum(iph, 20); iph->csum = get()      ip.cc:270-276
+ *              (every frame, fragments included: ip.cc:256-278 runs per fragment)
+ *   mode & 2:  L4 field = 0; pseudo-header + csum.sum(segment); get()    udp.cc:186,192-193 / tcp.hh:1683,1691-1694
+ *   mode & 4:  L4 field = ~get() of the pseudo-header alone (tx offload) udp.cc:188-189 / tcp.hh:1688-1689
+ *   mode & 8:  with 4, TCP pseudo-header length 0 (TSO)                  tcp.hh:1674-1676
+ *   mode & 16: ICMP echo request -> echo reply: type 0, code 0, checksum
+ *              over the message, no pseudo-header                        ip.cc:464-474
+ * L4 field: UDP +6, TCP +16, ICMP +2 after 4*ihl; written only for proto
+ * 17/6 (modes 2, 4) or an ICMP echo request of >= 8 B (mode 16), never into
+ * an IP fragment (the reference sums the datagram before ipv4::send cuts it,
+ * ip.cc:283-294), only when the frame is not malformed (as oracle_batch_ipv4)
+ * and the segment holds the field.  out2 (may be NULL) gets the values stored
+ * (0 = none); status bit0 = IP stored, bit1 = L4 stored, bit2 malformed,
+ * bit4 fragment, bit3 never (no range checks). */
 void oracle_batch_ipv4_fill(uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                             uint16_t* out2, uint8_t* status, uint64_t n, uint32_t mode);
 

@@ -97,13 +97,25 @@ def _stream(stream) -> int | None:
     return s.cuda_stream
 
 
+def _scratch(numel: int, device, stream, dtype=torch.uint8) -> torch.Tensor:
+    """A buffer the library allocates for kernels queued on `stream`
+    (scratch, or an output the caller did not pass): the caching allocator
+    must not hand the block to another stream's allocation before that
+    stream's work is done with it, so the block is recorded on `stream` (the
+    allocation itself is made on torch's current stream)."""
+    t = torch.empty(numel, dtype=dtype, device=device)
+    if stream is not None and t.is_cuda:  # (None: torch's current stream, the one it was allocated on)
+        t.record_stream(stream)
+    return t
+
+
 def spans(batch: PacketBatch, seeds: torch.Tensor | None = None, out: torch.Tensor | None = None,
           status: torch.Tensor | None = None, stream=None) -> torch.Tensor:
     """sccsum_spans: one network-order uint16 checksum per span (int16 tensor)."""
     lib = native.load()
     n = batch.n
     if out is None:
-        out = torch.empty(max(n, 1), dtype=torch.int16, device=batch.device)
+        out = _scratch(max(n, 1), batch.device, stream, torch.int16)
     _need(out, n, torch.int16, "out", batch.device)
     _need(seeds, n, torch.int32, "seeds", batch.device)
     _need(status, n, torch.uint8, "status", batch.device)
@@ -121,7 +133,7 @@ def ipv4_frames(batch: PacketBatch, out2: torch.Tensor | None = None, status: to
     lib = native.load()
     n = batch.n
     if out2 is None:
-        out2 = torch.empty(max(2 * n, 2), dtype=torch.int16, device=batch.device)
+        out2 = _scratch(max(2 * n, 2), batch.device, stream, torch.int16)
     _need(out2, 2 * n, torch.int16, "out2", batch.device)
     _need(status, n, torch.uint8, "status", batch.device)
     code = lib.sccsum_ipv4_frames(
@@ -166,7 +178,7 @@ def _multi(fn, name, items, max_len, stream, width, with_seed):
         rows.append((b, out, status, seeds))
     for i, (b, out, status, seeds) in enumerate(rows):
         if out is None:
-            out = torch.empty(max(width * b.n, width), dtype=torch.int16, device=b.device)
+            out = _scratch(max(width * b.n, width), b.device, stream, torch.int16)
         arr[i] = native.Batch(ctypes_ptr(b.data), b.bytes_len, ctypes_ptr(b.off), ctypes_ptr(b.length), _ptr(seeds),
                               ctypes_ptr(out), _ptr(status), b.n)
         outs.append(out)
@@ -241,8 +253,9 @@ def ipv4_fill(batch: PacketBatch, mode: int = native.FILL_IP | native.FILL_L4, o
     lib = native.load()
     n = batch.n
     given = out2
-    if out2 is None and mode & native.FILL_L4:  # the generate and store passes hand the values over in out2
-        out2 = torch.empty(max(2 * n, 2), dtype=torch.int16, device=batch.device)
+    if out2 is None and mode & (native.FILL_L4 | native.FILL_ICMP_ECHO):
+        # the generate and store passes hand the values over in out2 (scratch kept alive for `stream`)
+        out2 = _scratch(4 * max(n, 1), batch.device, stream).view(torch.int16)
     _need(out2, 2 * n, torch.int16, "out2", batch.device)
     _need(status, n, torch.uint8, "status", batch.device)
     code = lib.sccsum_ipv4_fill(
@@ -269,7 +282,7 @@ def ipv4_rss(batch: PacketBatch, key: bytes = RSS_KEY_40, mode: int = native.RSS
     lib = native.load()
     n = batch.n
     if hash_out is None:
-        hash_out = torch.empty(max(n, 1), dtype=torch.int32, device=batch.device)
+        hash_out = _scratch(max(n, 1), batch.device, stream, torch.int32)
     _need(hash_out, n, torch.int32, "hash_out", batch.device)
     _need(status, n, torch.uint8, "status", batch.device)
     kb, kl = _key(key)
@@ -287,9 +300,9 @@ def ipv4_frames_rss(batch: PacketBatch, key: bytes = RSS_KEY_40, mode: int = nat
     lib = native.load()
     n = batch.n
     if out2 is None:
-        out2 = torch.empty(max(2 * n, 2), dtype=torch.int16, device=batch.device)
+        out2 = _scratch(max(2 * n, 2), batch.device, stream, torch.int16)
     if hash_out is None:
-        hash_out = torch.empty(max(n, 1), dtype=torch.int32, device=batch.device)
+        hash_out = _scratch(max(n, 1), batch.device, stream, torch.int32)
     _need(out2, 2 * n, torch.int16, "out2", batch.device)
     _need(hash_out, n, torch.int32, "hash_out", batch.device)
     _need(status, n, torch.uint8, "status", batch.device)
@@ -309,7 +322,7 @@ def fragments(data: torch.Tensor, bytes_len: int, frag_off: torch.Tensor, frag_l
     n = int(pkt_first.numel()) - 1
     nfrag = int(frag_off.numel())
     if out is None:
-        out = torch.empty(max(n, 1), dtype=torch.int16, device=data.device)
+        out = _scratch(max(n, 1), data.device, stream, torch.int16)
     dev = data.device
     if n < 0:
         raise ValueError("pkt_first needs n + 1 entries")
@@ -319,7 +332,7 @@ def fragments(data: torch.Tensor, bytes_len: int, frag_off: torch.Tensor, frag_l
     _need(seeds, n, torch.int32, "seeds", dev)
     _need(out, n, torch.int16, "out", dev)
     _need(status, n, torch.uint8, "status", dev)
-    ws = torch.empty(int(lib.sccsum_fragments_workspace(nfrag)), dtype=torch.uint8, device=data.device)
+    ws = _scratch(int(lib.sccsum_fragments_workspace(nfrag)), data.device, stream)
     code = lib.sccsum_fragments(
         ctypes_ptr(data), bytes_len, ctypes_ptr(frag_off), ctypes_ptr(frag_len), nfrag, ctypes_ptr(pkt_first),
         _ptr(seeds), ctypes_ptr(out), _ptr(status), n, max_frag_len, ctypes_ptr(ws), _stream(stream))
@@ -348,7 +361,7 @@ def _desc_call(name, desc, first, off, length, max_len, width, seeds, stage, out
     if int(first.numel()) != n + 1 or first.dtype != torch.int32 or desc.dtype != torch.uint8:
         raise ValueError(f"{name}: first must be int32 [n + 1] and desc uint8 records")
     if out is None:
-        out = torch.empty(max(width * n, width), dtype=torch.int16, device=dev)
+        out = _scratch(max(width * n, width), dev, stream, torch.int16)
     _need(length, n, torch.int32, "length", dev)
     _need(seeds, n, torch.int32, "seeds", dev)
     _need(out, width * n, torch.int16, "out", dev)

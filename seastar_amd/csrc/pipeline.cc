@@ -163,6 +163,21 @@ namespace {
 bool device_readable(const void* p, uint64_t len) {
     if (len == 0) return true;
     const auto* b = static_cast<const uint8_t*>(p);
+    // one allocation must hold the whole range: two pinned blocks with pageable
+    // memory between them pass an ends-only check, and the zero-copy kernel
+    // would then read the pageable hole over PCIe
+    void* start = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                               reinterpret_cast<hipDeviceptr_t>(const_cast<uint8_t*>(b))) == hipSuccess &&
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
+                               reinterpret_cast<hipDeviceptr_t>(const_cast<uint8_t*>(b))) == hipSuccess &&
+        start != nullptr && size != 0) {
+        const auto* s0 = static_cast<const uint8_t*>(start);
+        if (b < s0 || len > size || static_cast<uint64_t>(b - s0) > size - len) return false;
+    } else {
+        (void)hipGetLastError();  // the range query is not answered for this memory: the two-end check below
+    }
     for (const uint8_t* q : {b, b + len - 1}) {
         hipPointerAttribute_t a{};
         if (hipPointerGetAttributes(&a, q) != hipSuccess) {

@@ -25,10 +25,13 @@ ST_OK = 0x01
 ST_L4_OK = 0x02
 ST_MALFORMED = 0x04
 ST_RANGE = 0x08
+ST_IPFRAG = 0x10
 FILL_IP = 0x01
 FILL_L4 = 0x02
 FILL_L4_PSEUDO = 0x04
 FILL_TSO = 0x08
+FILL_ICMP_ECHO = 0x10
+ABI_VERSION = 2
 
 
 class SccsumError(RuntimeError):
@@ -144,8 +147,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.sccsum_abi_version() != 1:
-        raise RuntimeError("libsccsum ABI version mismatch")
+    if lib.sccsum_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"libsccsum ABI version {lib.sccsum_abi_version()} != {ABI_VERSION}: rebuild it")
     _LIB = lib
     return lib
 

@@ -155,6 +155,50 @@ def store_ipv4_checksums(buf: np.ndarray, off: np.ndarray, out2: np.ndarray) -> 
         buf[pos:pos + 2] = np.frombuffer(np.uint16(out2[i, 1]).tobytes(), np.uint8)
 
 
+def frag_words(rng: np.random.Generator, n: int, frac: float = 0.3) -> np.ndarray:
+    """IPv4 flags + fragment-offset words (header bytes 6-7, ip.hh:388-391)
+    for n frames: atomic datagrams (0, or DF alone) and, with probability
+    `frac`, fragments as ipv4::send cuts a datagram (ip.cc:283-294): a first
+    fragment (MF, offset 0), a middle one (MF, offset k), a last one (offset
+    k, MF clear), and offsets near the top whose offset + length passes the
+    65 535-byte datagram limit (ip.cc:141-144)."""
+    w = np.where(rng.random(n) < 0.5, 0, 0x4000).astype(np.uint32)  # DF alone is still atomic
+    kind = rng.random(n)
+    frag = kind < frac
+    sub = rng.integers(0, 4, n)
+    k = rng.integers(1, 0x2000, n).astype(np.uint32)
+    fw = np.select([sub == 0, sub == 1, sub == 2], [0x2000 + 0 * k, 0x2000 | (k & 0x1ff), k & 0x1ff],
+                   default=0x1f00 | (k & 0xff))
+    w = np.where(frag, fw | (w & 0x4000 & np.where(sub == 2, 0xFFFF, 0)), w)
+    return w.astype(np.uint32)
+
+
+def ipv4_fragment(datagram_l4: np.ndarray, proto: int, src: int, dst: int, mtu: int = 1500,
+                  ident: int = 0) -> list[np.ndarray]:
+    """ipv4::send (src/net/ip.cc:244-299) of one L4 datagram (header +
+    payload, its checksum already in place): cut into pieces of at most
+    mtu - 20 bytes when it does not fit (needs_frag, ip.cc:100-111), each
+    prepended with its own IPv4 header (ihl 5, id `ident`, MF on all but the
+    last, offset in 8-byte units, ttl 64; header checksum 0).  Returns the
+    frames.  (With mtu - 20 a multiple of 8, every offset is exact.)"""
+    data = np.asarray(datagram_l4, dtype=np.uint8)
+    room = mtu - IPV4_HDR
+    if data.size + IPV4_HDR <= mtu:
+        cuts = [(0, data.size)]
+    else:
+        cuts = [(o, min(room, data.size - o)) for o in range(0, data.size, room)]
+    frames = []
+    for k, (o, L) in enumerate(cuts):
+        f = np.zeros((1, IPV4_HDR + L), np.uint8)
+        write_ipv4_header(f, [IPV4_HDR + L], proto, [src], [dst])
+        _put_be16(f, 4, [ident])
+        more = k + 1 < len(cuts)
+        _put_be16(f, 6, [(0x2000 if more else 0) | ((o // 8) if len(cuts) > 1 else 0)])
+        f[0, IPV4_HDR:] = data[o:o + L]
+        frames.append(f.reshape(-1))
+    return frames
+
+
 def rss_frames(n: int, seed: int = 0x55):
     """A varied IPv4 batch for RSS hashing (forward_hash edge cases): UDP, TCP,
     ICMP and other protocols; fragments (MF set / nonzero offset); IP options

@@ -2,16 +2,22 @@
 // include/sccsum_diag.h) without a device: each bad call must return its
 // error code and touch nothing.  Built by tests/test_sanitize.py with host
 // AddressSanitizer + UndefinedBehaviorSanitizer (the reference's `sanitize`
-// build mode, cmake/FindSanitizers.cmake:37-43) over the library sources.
-// Exit status 0 = every check held.
+// build mode, cmake/FindSanitizers.cmake:37-43) over the library sources, and
+// with ThreadSanitizer, the checks run from several threads at once (Seastar
+// calls from one reactor thread per shard: src/core/reactor.cc:3437-3438).
+// Usage: abi_validate [threads].  Exit status 0 = every check held.
 #include "sccsum.h"
 #include "sccsum_diag.h"
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
+#include <vector>
 
-static int failures = 0;
+static std::atomic<int> failures{0};
 #define EXPECT(cond)                                                       \
     do {                                                                   \
         if (!(cond)) {                                                     \
@@ -22,7 +28,7 @@ static int failures = 0;
 
 static void noop(void*, uint64_t, uint32_t, const uint16_t*, const uint8_t*) {}
 
-int main() {
+static void checks() {
     void* const d16 = reinterpret_cast<void*>(uintptr_t(0x10000));  // aligned non-null stand-ins, never dereferenced
     void* const odd = reinterpret_cast<void*>(uintptr_t(0x10002));
     // n == 0 is a no-op whatever the pointers
@@ -66,9 +72,13 @@ int main() {
            SCCSUM_EINVAL);
     EXPECT(sccsum_ipv4_fill(nullptr, 64, nullptr, nullptr, nullptr, nullptr, 3, 0, SCCSUM_FILL_IP, nullptr) ==
            SCCSUM_EINVAL);
-    // FILL_L4 needs d_out2 (the generate pass hands its values to the store pass there)
+    // FILL_L4 / FILL_ICMP_ECHO need d_out2 (the generate pass hands its values to the store pass there)
     EXPECT(sccsum_ipv4_fill(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr,
                             nullptr, 3, 0, SCCSUM_FILL_IP | SCCSUM_FILL_L4, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_ipv4_fill(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr,
+                            nullptr, 3, 0, SCCSUM_FILL_ICMP_ECHO, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_ipv4_fill(nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, 0,
+                            SCCSUM_FILL_ICMP_ECHO | SCCSUM_FILL_L4_PSEUDO, nullptr) == SCCSUM_EINVAL);
     // RSS
     const uint8_t key3[3] = {1, 2, 3};
     EXPECT(sccsum_ipv4_rss(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), key3, 3, 0,
@@ -129,10 +139,24 @@ int main() {
     EXPECT(std::strcmp(sccsum_strerror(SCCSUM_EBUSY), "every batch slot is in flight") == 0);
     EXPECT(std::strcmp(sccsum_strerror(-99), "unknown sccsum error") == 0);
     EXPECT(sccsum_abi_version() == SCCSUM_ABI_VERSION);
-    if (failures) {
-        std::printf("abi_validate: %d FAILED\n", failures);
+}
+
+int main(int argc, char** argv) {
+    const int threads = argc > 1 ? std::atoi(argv[1]) : 1;
+    checks();
+    if (threads > 1) {
+        std::vector<std::thread> ts;
+        for (int t = 0; t < threads; ++t) {
+            ts.emplace_back([] {
+                for (int rep = 0; rep < 20; ++rep) checks();
+            });
+        }
+        for (auto& t : ts) t.join();
+    }
+    if (failures.load()) {
+        std::printf("abi_validate: %d FAILED\n", failures.load());
         return 1;
     }
-    std::printf("abi_validate: OK\n");
+    std::printf("abi_validate: OK (%d thread%s)\n", threads, threads > 1 ? "s" : "");
     return 0;
 }

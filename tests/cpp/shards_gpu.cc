@@ -1,0 +1,278 @@
+// Seastar's threading model against one device: one reactor thread per shard
+// (src/core/reactor.cc:3437-3438), each binding itself with sccsum_init,
+// owning its streams, its batches and a burst queue, and launching at the
+// same time as every other shard: frames (verify), seeded spans, a multi
+// launch, the in-place fill, a burst queue fed one frame at a time, and a
+// loop that creates a stream, launches on it and destroys it without waiting
+// (a new stream may get the old one's address while that launch still runs).
+// Every result is checked against the oracle (test infrastructure, linked
+// into this test program only).  Usage: shards_gpu [threads] [rounds].
+#include <hip/hip_runtime.h>
+
+#include "sccsum.h"
+#include "sccsum_diag.h"
+#include "sccsum_oracle.h"
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <thread>
+#include <vector>
+
+namespace {
+
+std::atomic<int> g_bad{0};
+std::mutex g_print;
+
+void fail(int shard, const char* what, long i) {
+    if (g_bad.fetch_add(1) < 20) {
+        std::lock_guard<std::mutex> l(g_print);
+        std::printf("shard %d: %s mismatch at %ld\n", shard, what, i);
+    }
+}
+
+bool hip_ok(hipError_t e, int shard, const char* what) {
+    if (e == hipSuccess) return true;
+    std::lock_guard<std::mutex> l(g_print);
+    std::printf("shard %d: %s: %s\n", shard, what, hipGetErrorString(e));
+    g_bad.fetch_add(1);
+    return false;
+}
+
+bool ok(int rc, int shard, const char* what) {
+    if (rc == SCCSUM_OK) return true;
+    std::lock_guard<std::mutex> l(g_print);
+    std::printf("shard %d: %s: %s\n", shard, what, sccsum_strerror(rc));
+    g_bad.fetch_add(1);
+    return false;
+}
+
+// IPv4 frames as the native stack sees them: UDP / TCP / ICMP (echo requests
+// among them), IP fragments, options, padding, runts, odd offsets.
+struct Frames {
+    std::vector<uint8_t> bytes;
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len;
+};
+
+Frames make_frames(std::mt19937_64& rng, uint32_t n) {
+    Frames F;
+    F.off.resize(n);
+    F.len.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t L = 20 + static_cast<uint32_t>(rng() % 3000);
+        if (rng() % 64 == 0) L = static_cast<uint32_t>(rng() % 20);
+        F.off[i] = F.bytes.size() + rng() % 4;
+        F.len[i] = L;
+        F.bytes.resize(F.off[i] + L);
+        uint8_t* f = F.bytes.data() + F.off[i];
+        for (uint32_t k = 0; k < L; ++k) f[k] = static_cast<uint8_t>(rng());
+        if (L < 20) continue;
+        const uint32_t ihl = rng() % 8 == 0 ? 6 + rng() % 4 : 5;
+        const uint32_t ip_len = rng() % 10 == 0 ? L - static_cast<uint32_t>(rng() % 8) : L;
+        f[0] = static_cast<uint8_t>(0x40 | ihl);
+        f[2] = static_cast<uint8_t>(ip_len >> 8);
+        f[3] = static_cast<uint8_t>(ip_len);
+        const uint32_t r = rng() % 10;
+        const uint32_t fragw = r == 0 ? 0x2000 : (r == 1 ? 0x2000 | (rng() % 0x100) : (r == 2 ? rng() % 0x100 : 0));
+        f[6] = static_cast<uint8_t>(fragw >> 8);
+        f[7] = static_cast<uint8_t>(fragw);
+        const uint8_t protos[3] = {17, 6, 1};
+        f[9] = protos[rng() % 3];
+        if (f[9] == 1 && ip_len > 4 * ihl && rng() % 4 != 0) f[4 * ihl] = 8;  // echo request
+    }
+    F.bytes.resize(F.bytes.size() + 16);
+    return F;
+}
+
+struct DevBatch {
+    uint8_t* bytes = nullptr;
+    uint64_t* off = nullptr;
+    uint32_t* len = nullptr;
+    uint64_t n = 0, bytes_len = 0;
+};
+
+bool upload(const Frames& F, DevBatch& D, int shard) {
+    D.n = F.off.size();
+    D.bytes_len = F.bytes.size();
+    return hip_ok(hipMalloc(&D.bytes, (D.bytes_len + 15) & ~uint64_t(15)), shard, "malloc") &&
+           hip_ok(hipMalloc(&D.off, D.n * 8), shard, "malloc") && hip_ok(hipMalloc(&D.len, D.n * 4), shard, "malloc") &&
+           hip_ok(hipMemcpy(D.bytes, F.bytes.data(), D.bytes_len, hipMemcpyHostToDevice), shard, "copy") &&
+           hip_ok(hipMemcpy(D.off, F.off.data(), D.n * 8, hipMemcpyHostToDevice), shard, "copy") &&
+           hip_ok(hipMemcpy(D.len, F.len.data(), D.n * 4, hipMemcpyHostToDevice), shard, "copy");
+}
+
+void release(DevBatch& D) {
+    (void)hipFree(D.bytes);
+    (void)hipFree(D.off);
+    (void)hipFree(D.len);
+}
+
+template <typename T>
+std::vector<T> fetch(const T* d, size_t count, int shard) {
+    std::vector<T> h(count);
+    hip_ok(hipMemcpy(h.data(), d, count * sizeof(T), hipMemcpyDeviceToHost), shard, "fetch");
+    return h;
+}
+
+struct BurstSink {
+    std::vector<uint16_t> out;
+    std::vector<uint8_t> st;
+};
+
+void burst_done(void* user, uint64_t first, uint32_t count, const uint16_t* results, const uint8_t* status) {
+    auto* S = static_cast<BurstSink*>(user);
+    for (uint32_t k = 0; k < count; ++k) {
+        S->out[2 * (first + k)] = results[2 * k];
+        S->out[2 * (first + k) + 1] = results[2 * k + 1];
+        S->st[first + k] = status[k];
+    }
+}
+
+void shard_main(int shard, int rounds) {
+    if (!ok(sccsum_init(0), shard, "sccsum_init")) return;
+    // per-thread knobs: each shard runs another kernel form; none leaks into another shard
+    const int forms[6] = {0, 16, 15, 14, 1, 2};
+    if (!ok(sccsum_set_kernel_variant(forms[shard % 6]), shard, "variant")) return;
+    std::mt19937_64 rng(0x5EA57A2Cull + 7919ull * shard);
+    const uint32_t n = 6000 + 1000 * (shard % 3);
+    Frames A = make_frames(rng, n), B = make_frames(rng, n / 2);
+    // oracle results
+    std::vector<uint16_t> wantA(2 * A.off.size()), wantB(2 * B.off.size());
+    std::vector<uint8_t> wstA(A.off.size()), wstB(B.off.size());
+    oracle_batch_ipv4(A.bytes.data(), A.off.data(), A.len.data(), wantA.data(), wstA.data(), A.off.size(), 1);
+    oracle_batch_ipv4(B.bytes.data(), B.off.data(), B.len.data(), wantB.data(), wstB.data(), B.off.size(), 1);
+    std::vector<uint32_t> seeds(n);
+    for (auto& s : seeds) s = static_cast<uint32_t>(rng() & 0xffff);
+    std::vector<uint16_t> want_sp(n);
+    oracle_batch_spans(A.bytes.data(), A.off.data(), A.len.data(), seeds.data(), want_sp.data(), n, 1);
+    const uint32_t fmode = SCCSUM_FILL_IP | SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO;
+    std::vector<uint8_t> want_fill = A.bytes;
+    std::vector<uint16_t> want_fout(2 * n);
+    std::vector<uint8_t> want_fst(n);
+    oracle_batch_ipv4_fill(want_fill.data(), A.off.data(), A.len.data(), want_fout.data(), want_fst.data(), n, fmode);
+
+    DevBatch dA, dB;
+    if (!upload(A, dA, shard) || !upload(B, dB, shard)) return;
+    uint8_t* fill_bytes = nullptr;
+    uint16_t *o1 = nullptr, *o2 = nullptr, *o3 = nullptr, *osp = nullptr, *ofill = nullptr;
+    uint8_t *s1 = nullptr, *s2 = nullptr, *ssp = nullptr, *sfill = nullptr;
+    uint32_t* d_seed = nullptr;
+    const int kTemp = 8;  // launches on streams destroyed without a sync, per round
+    uint16_t* otemp = nullptr;
+    if (!hip_ok(hipMalloc(&fill_bytes, (dA.bytes_len + 15) & ~uint64_t(15)), shard, "malloc") ||
+        !hip_ok(hipMalloc(&o1, 4 * n), shard, "malloc") || !hip_ok(hipMalloc(&o2, 4 * n), shard, "malloc") ||
+        !hip_ok(hipMalloc(&o3, 4 * n), shard, "malloc") || !hip_ok(hipMalloc(&osp, 2 * n), shard, "malloc") ||
+        !hip_ok(hipMalloc(&ofill, 4 * n), shard, "malloc") || !hip_ok(hipMalloc(&s1, n), shard, "malloc") ||
+        !hip_ok(hipMalloc(&s2, n), shard, "malloc") || !hip_ok(hipMalloc(&ssp, n), shard, "malloc") ||
+        !hip_ok(hipMalloc(&sfill, n), shard, "malloc") || !hip_ok(hipMalloc(&d_seed, 4 * n), shard, "malloc") ||
+        !hip_ok(hipMalloc(&otemp, size_t(4) * n * kTemp), shard, "malloc") ||
+        !hip_ok(hipMemcpy(d_seed, seeds.data(), 4 * n, hipMemcpyHostToDevice), shard, "copy")) {
+        return;
+    }
+    hipStream_t s0, sx;
+    if (!hip_ok(hipStreamCreate(&s0), shard, "stream") || !hip_ok(hipStreamCreate(&sx), shard, "stream")) return;
+    auto check2 = [&](const std::vector<uint16_t>& got, const std::vector<uint16_t>& want, const char* what) {
+        for (size_t i = 0; i < want.size(); ++i) {
+            if (got[i] != want[i]) {
+                fail(shard, what, static_cast<long>(i));
+                return;
+            }
+        }
+    };
+    for (int round = 0; round < rounds; ++round) {
+        // frames + status on s0; seeded spans on sx; a multi launch over A and B on s0
+        ok(sccsum_ipv4_frames(dA.bytes, dA.bytes_len, dA.off, dA.len, o1, s1, n, 3100, s0), shard, "frames");
+        ok(sccsum_spans(dA.bytes, dA.bytes_len, dA.off, dA.len, d_seed, osp, ssp, n, 3100, sx), shard, "spans");
+        sccsum_batch mb[2] = {{dA.bytes, dA.bytes_len, dA.off, dA.len, nullptr, o2, nullptr, n},
+                              {dB.bytes, dB.bytes_len, dB.off, dB.len, nullptr, o3, s2, dB.n}};
+        ok(sccsum_ipv4_frames_multi(mb, 2, 3100, s0), shard, "multi");
+        // in place, on a fresh copy of A
+        hip_ok(hipMemcpyAsync(fill_bytes, dA.bytes, dA.bytes_len, hipMemcpyDeviceToDevice, sx), shard, "copy");
+        ok(sccsum_ipv4_fill(fill_bytes, dA.bytes_len, dA.off, dA.len, ofill, sfill, n, 3100, fmode, sx), shard, "fill");
+        // streams created, launched on and destroyed without waiting
+        hipEvent_t ev[kTemp];
+        for (int k = 0; k < kTemp; ++k) {
+            hipStream_t t;
+            hip_ok(hipStreamCreateWithFlags(&t, hipStreamNonBlocking), shard, "stream");
+            ok(sccsum_ipv4_frames(dA.bytes, dA.bytes_len, dA.off, dA.len, otemp + size_t(2) * n * k, nullptr, n, 3100,
+                                  t),
+               shard, "frames (temp stream)");
+            hip_ok(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), shard, "event");
+            hip_ok(hipEventRecord(ev[k], t), shard, "event");
+            hip_ok(hipStreamDestroy(t), shard, "stream destroy");
+        }
+        hip_ok(hipStreamSynchronize(s0), shard, "sync");
+        hip_ok(hipStreamSynchronize(sx), shard, "sync");
+        for (int k = 0; k < kTemp; ++k) {
+            hip_ok(hipEventSynchronize(ev[k]), shard, "event sync");
+            (void)hipEventDestroy(ev[k]);
+        }
+        check2(fetch(o1, 2 * n, shard), wantA, "frames");
+        if (fetch(s1, n, shard) != wstA) fail(shard, "frames status", round);
+        check2(fetch(osp, n, shard), want_sp, "spans");
+        check2(fetch(o2, 2 * n, shard), wantA, "multi batch 0");
+        check2(fetch(o3, 2 * dB.n, shard), wantB, "multi batch 1");
+        if (fetch(s2, dB.n, shard) != wstB) fail(shard, "multi status", round);
+        check2(fetch(ofill, 2 * n, shard), want_fout, "fill values");
+        if (fetch(sfill, n, shard) != want_fst) fail(shard, "fill status", round);
+        const std::vector<uint8_t> fb = fetch(fill_bytes, dA.bytes_len, shard);
+        if (std::memcmp(fb.data(), want_fill.data(), dA.bytes_len) != 0) fail(shard, "fill bytes", round);
+        const std::vector<uint16_t> ot = fetch(otemp, size_t(2) * n * kTemp, shard);
+        for (int k = 0; k < kTemp; ++k) {
+            if (std::memcmp(ot.data() + size_t(2) * n * k, wantA.data(), 4 * size_t(n)) != 0) {
+                fail(shard, "frames on a destroyed stream", k);
+            }
+        }
+    }
+    // the shard's burst queue: frames handed over one at a time (host memory)
+    BurstSink sink;
+    sink.out.assign(2 * n, 0xEEEE);
+    sink.st.assign(n, 0xEE);
+    sccsum_burst* q = nullptr;
+    if (ok(sccsum_burst_create(0, SCCSUM_PIPE_IPV4, 1u << 20, 256, 20000, 4, burst_done, &sink, &q), shard,
+           "burst create")) {
+        for (uint32_t i = 0; i < n; ++i) {
+            sccsum_fragment fr{A.bytes.data() + A.off[i], A.len[i]};
+            int rc;
+            while ((rc = sccsum_burst_submit(q, &fr, 1, 0, nullptr)) == SCCSUM_EBUSY) ok(sccsum_burst_poll(q, nullptr), shard, "poll");
+            ok(rc, shard, "burst submit");
+            if (i % 32 == 31) ok(sccsum_burst_poll(q, nullptr), shard, "poll");
+        }
+        ok(sccsum_burst_drain(q), shard, "drain");
+        ok(sccsum_burst_destroy(q), shard, "burst destroy");
+        check2(sink.out, wantA, "burst");
+        if (sink.st != wstA) fail(shard, "burst status", 0);
+    }
+    (void)hipStreamDestroy(s0);
+    (void)hipStreamDestroy(sx);
+    for (void* p : {static_cast<void*>(fill_bytes), static_cast<void*>(o1), static_cast<void*>(o2),
+                    static_cast<void*>(o3), static_cast<void*>(osp), static_cast<void*>(ofill), static_cast<void*>(s1),
+                    static_cast<void*>(s2), static_cast<void*>(ssp), static_cast<void*>(sfill),
+                    static_cast<void*>(d_seed), static_cast<void*>(otemp)}) {
+        (void)hipFree(p);
+    }
+    release(dA);
+    release(dB);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const int threads = argc > 1 ? std::atoi(argv[1]) : 8;
+    const int rounds = argc > 2 ? std::atoi(argv[2]) : 6;
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t) ts.emplace_back(shard_main, t, rounds);
+    for (auto& t : ts) t.join();
+    if (g_bad.load()) {
+        std::printf("shards_gpu: FAILED (%d)\n", g_bad.load());
+        return 1;
+    }
+    std::printf("shards_gpu: OK (%d shards x %d rounds: frames, spans, multi, fill, %d launches on destroyed "
+                "streams per round, burst queue)\n",
+                threads, rounds, 8);
+    return 0;
+}

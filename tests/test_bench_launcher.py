@@ -29,6 +29,10 @@ def test_launcher_starts_n_ranks_without_device(n):
     assert [r["rank"] for r in d["ranks"]] == list(range(n))
     assert [r["local"] for r in d["ranks"]] == [str(i) for i in range(n)]
     assert len({r["pid"] for r in d["ranks"]}) == n  # one process per rank
+    # the per_rank block a real N > 1 line carries: one entry per rank, in rank order
+    assert [r["rank"] for r in d["per_rank"]] == list(range(n))
+    assert all({"device", "pci_bus_id", "host", "wall_s", "GiBps", "avg_launch_us", "read_ceiling_GBps"} <= set(r)
+               for r in d["per_rank"])
 
 
 def test_launcher_reports_a_failed_rank_and_stops_the_others():
@@ -54,6 +58,12 @@ def test_launcher_two_ranks_on_the_gpu():
                timeout=300)
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["config"]["global_batch"] == 2 * 65536
+    pr = d["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1]
+    for r in pr:  # real figures per rank: the device it ran on, its own rate, launch time and read ceiling
+        assert r["pci_bus_id"] and r["GiBps"] > 0 and r["avg_launch_us"] > 0 and r["read_ceiling_GBps"] > 0
+        assert 0 < r["frac"] < 1
+    print(json.dumps(pr))
 
 
 def test_torchrun_launch_as_the_driver_runs_it():
@@ -93,3 +103,4 @@ def test_torchrun_two_ranks_on_the_gpu():
     assert r.returncode == 0, r.stdout + r.stderr
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and lines[0]["value"] > 0
+    assert [x["rank"] for x in lines[0]["per_rank"]] == [0, 1]

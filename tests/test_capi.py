@@ -38,7 +38,7 @@ def test_library_loads_and_binds_every_symbol():
     lib = native.load()
     for s in native.header_symbols():
         assert hasattr(lib, s)
-    assert lib.sccsum_abi_version() == 1
+    assert lib.sccsum_abi_version() == native.ABI_VERSION == 2
     assert lib.sccsum_strerror(0) == b"success"
     assert lib.sccsum_strerror(native.SCCSUM_EINVAL) == b"invalid argument"
 
@@ -80,7 +80,11 @@ def test_argument_validation_without_device():
         == native.SCCSUM_EINVAL
     assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, F.FILL_IP | F.FILL_TSO, None) \
         == native.SCCSUM_EINVAL
-    assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, 0x10, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, 0x20, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, F.FILL_ICMP_ECHO | F.FILL_L4_PSEUDO,
+                                None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, F.FILL_ICMP_ECHO, None) == 0
+    assert lib.sccsum_ipv4_fill(None, 64, None, None, None, None, 3, 0, F.FILL_ICMP_ECHO, None) == native.SCCSUM_EINVAL
     assert lib.sccsum_ipv4_fill(None, 0, None, None, None, None, 0, 0, F.FILL_IP | F.FILL_L4, None) == 0
     assert lib.sccsum_ipv4_fill(None, 64, None, None, None, None, 3, 0, F.FILL_IP, None) == native.SCCSUM_EINVAL
     assert lib.sccsum_ipv4_fill(None, 64, None, None, None, None, 3, 0, F.FILL_L4, None) == native.SCCSUM_EINVAL

@@ -117,3 +117,35 @@ def test_burst_cpp_program_on_gpu(tmp_path):
         assert r.returncode == 0, r.stdout + r.stderr
         assert "OK" in r.stdout
         print(r.stdout)
+
+
+def _shards_exe(tmp_path):
+    obj = str(tmp_path / "oracle.o")
+    subprocess.run(["gcc", "-O2", "-fPIC", "-c", os.path.join(REPO, "oracle", "sccsum_oracle.c"), "-o", obj],
+                   check=True)
+    exe = str(tmp_path / "shards_gpu")
+    cmd = ["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"),
+           "-I", os.path.join(REPO, "oracle"), os.path.join(REPO, "tests", "cpp", "shards_gpu.cc"), "-x", "none", obj,
+           "-L", os.path.join(REPO, "seastar_amd", "lib"), "-lsccsum", "-lpthread",
+           "-Wl,-rpath," + os.path.join(REPO, "seastar_amd", "lib"), "-o", exe]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def test_shards_cpp_program_builds(tmp_path):
+    assert os.path.exists(_shards_exe(tmp_path))
+
+
+@pytest.mark.gpu
+def test_shards_cpp_program_on_gpu(tmp_path):
+    """Seastar's threading model (one reactor thread per shard,
+    reactor.cc:3437): 8 host threads on one device, each with its own
+    sccsum_init, streams, batches, kernel form and burst queue, launching
+    frames / spans / multi / fill concurrently, plus launches on streams
+    destroyed without a sync; every result against the oracle."""
+    exe = _shards_exe(tmp_path)
+    r = subprocess.run([exe, "8", "4"], capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout
+    print(r.stdout)

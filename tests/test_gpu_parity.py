@@ -410,8 +410,12 @@ def _tx_frames(rng, n):
     """IPv4 frames for the tx generate path: UDP / TCP / ICMP, IHL 5..15,
     Ethernet-padded (len > ip_len), truncated (malformed), runts (< 20 B),
     segments too short for their checksum field, GARBAGE in every checksum
-    field (a generate must not depend on it); random odd offsets."""
+    field (a generate must not depend on it); IP fragments (first, middle,
+    last, past the 65 535-byte limit: synth.frag_words) among atomic
+    datagrams; ICMP echo requests (some with all-zero messages, whose reply
+    checksum is 0xffff) among other ICMP types; random odd offsets."""
     frames = []
+    fw = synth.frag_words(rng, n)
     for i in range(n):
         proto = int(rng.choice([17, 6, 1, 17, 6]))
         ihl = 5 if rng.random() < 0.8 else int(rng.integers(6, 16))
@@ -420,7 +424,12 @@ def _tx_frames(rng, n):
         f = rng.integers(0, 256, size=ip_len, dtype=np.uint8)
         f[0] = 0x40 | ihl
         f[2], f[3] = ip_len >> 8, ip_len & 0xFF
+        f[6], f[7] = int(fw[i]) >> 8, int(fw[i]) & 0xFF
         f[9] = proto
+        if proto == 1 and pay >= 1:
+            f[4 * ihl] = 8 if rng.random() < 0.7 else int(rng.choice([0, 3, 11, 13, 9]))
+            if rng.random() < 0.1:  # all-zero message after type / code / checksum
+                f[4 * ihl + 4:] = 0
         kind = rng.random()
         if kind < 0.08:  # Ethernet padding past ip_len
             f = np.concatenate([f, rng.integers(0, 256, size=int(rng.integers(1, 40)), dtype=np.uint8)])
@@ -448,6 +457,8 @@ FILL_MODES = {
     "ip": native.FILL_IP,
     "pseudo": native.FILL_L4_PSEUDO,
     "ip_pseudo_tso": native.FILL_IP | native.FILL_L4_PSEUDO | native.FILL_TSO,
+    "icmp_echo": native.FILL_ICMP_ECHO,
+    "ip_l4_icmp_echo": native.FILL_IP | native.FILL_L4 | native.FILL_ICMP_ECHO,
 }
 
 
@@ -467,7 +478,27 @@ def test_ipv4_fill_in_place(dev, mode):
     assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want_out2)
     assert np.array_equal(st.cpu().numpy(), want_st)
     assert np.array_equal(got_buf, want_buf)
-    if m & native.FILL_L4:
+    # an IP fragment's bytes past its IP header are byte-identical after any
+    # fill (ip.cc:244-299: L4 is summed before ipv4::send cuts the datagram)
+    stn = st.cpu().numpy()
+    frag = np.nonzero(stn & native.ST_IPFRAG)[0]
+    assert frag.size > 50
+    for i in frag:
+        o, L = int(off[i]), int(length[i])
+        assert np.array_equal(got_buf[o + 20:o + L], buf[o + 20:o + L]), f"fragment {i} payload written"
+    assert not np.any(stn[frag] & native.ST_L4_OK)
+    if m & native.FILL_ICMP_ECHO:  # echo requests became replies; every other ICMP frame is untouched
+        icmp = [i for i in range(off.size) if length[i] >= 20 and buf[int(off[i]) + 9] == 1]
+        replies = [i for i in icmp if stn[i] & native.ST_L4_OK]
+        assert len(replies) > 20
+        for i in icmp:
+            o, L = int(off[i]), int(length[i])
+            ihl4 = 4 * (buf[o] & 0xF)
+            if i in replies:
+                assert buf[o + ihl4] == 8 and got_buf[o + ihl4] == 0 and got_buf[o + ihl4 + 1] == 0
+            else:
+                assert np.array_equal(got_buf[o + 20:o + L], buf[o + 20:o + L])
+    if m & (native.FILL_L4 | native.FILL_ICMP_ECHO):
         # the filled frames verify: receive path (ip.cc:121-127, udp/tcp verify) accepts them
         got, vst = _frames(dev, got_buf, off, length)
         stored = want_st & 2 != 0
@@ -493,12 +524,14 @@ def _packed_tx_frames(rng, n, gaps=(0,)):
     every start alignment: neighbours share the 16-byte units holding fields."""
     choices = [20, 21, 27, 28, 29, 37, 38, 39, 40, 47, 48, 63, 64, 65, 79, 80, 95, 96, 97, 100, 128, 576, 1500]
     frames = []
+    fw = synth.frag_words(rng, n, frac=0.15)
     for i in range(n):
         L = int(rng.choice(choices))
         proto = int(rng.choice([17, 6]))
         f = rng.integers(0, 256, size=L, dtype=np.uint8)
         f[0] = 0x45
         f[2], f[3] = L >> 8, L & 0xFF
+        f[6], f[7] = int(fw[i]) >> 8, int(fw[i]) & 0xFF
         f[9] = proto
         frames.append(f)
     length = np.array([f.size for f in frames], np.uint32)
@@ -818,9 +851,11 @@ def test_slot_layout_one_run_per_packet(dev, kernel_variant, short):
         assert np.array_equal(_spans(dev, buf, off, lens, seeds), oracle.batch_spans(buf, off, lens, seeds))
         fl = np.maximum(lens, 20).astype(np.uint32)
         fbuf = buf.copy()
-        for i in range(fl.size):  # IPv4/UDP headers, ip_len = frame length
+        fw = synth.frag_words(rng, fl.size, frac=0.1)
+        for i in range(fl.size):  # IPv4/UDP headers, ip_len = frame length, some fragments
             o, L = int(off[i]), int(fl[i])
             fbuf[o], fbuf[o + 2], fbuf[o + 3], fbuf[o + 9] = 0x45, L >> 8, L & 0xFF, 17
+            fbuf[o + 6], fbuf[o + 7] = int(fw[i]) >> 8, int(fw[i]) & 0xFF
         got, st = _frames(dev, fbuf, off, fl)
         want, want_st = oracle.batch_ipv4(fbuf, off, fl)
         assert np.array_equal(got, want) and np.array_equal(st, want_st)
@@ -958,12 +993,14 @@ def test_random_layouts_shuffled_overlapping(dev, kernel_variant, seed):
     assert np.array_equal(_spans(dev, buf, off, lens, seeds), oracle.batch_spans(buf, off, lens, seeds))
     # frames: the same layout with IPv4 headers written at each start (later writes win, as on the host)
     fb = buf.copy()
+    fw = synth.frag_words(rng, n, frac=0.1)
     for i in range(n):
         L = int(lens[i])
         if L >= 20:
             o = int(off[i])
             fb[o] = 0x45
             fb[o + 2], fb[o + 3] = (L >> 8) & 0xFF, L & 0xFF
+            fb[o + 6], fb[o + 7] = int(fw[i]) >> 8, int(fw[i]) & 0xFF
             fb[o + 9] = 17 if i % 2 else 6
     got, st = _frames(dev, fb, off, lens)
     want, want_st = oracle.batch_ipv4(fb, off, lens)
@@ -1075,3 +1112,135 @@ def test_run_align_matches_oracle(dev, kernel_variant, units):
         assert np.array_equal(batch.as_u16(o1), want) and np.array_equal(st1.cpu().numpy(), want_st)
     finally:
         native.check(lib.sccsum_set_run_align(8), "run_align")
+
+
+def _fragmented_datagrams(rng, sizes, mtu=1500):
+    """UDP / TCP datagrams of the given L4 sizes, checksummed whole by the
+    oracle (udp.cc:184-195 / tcp.hh:1656-1694 run before ipv4::send) and cut
+    into frames by synth.ipv4_fragment (ip.cc:283-294); the frames are packed
+    at odd offsets.  Returns (buf, off, lens, dgrams) with dgrams[d] =
+    (proto, src, dst, l4 bytes, [frame indices in offset order])."""
+    frames, dgrams = [], []
+    for d, size in enumerate(sizes):
+        proto = 17 if d % 2 == 0 else 6
+        src, dst = int(rng.integers(1, 2**32)), int(rng.integers(1, 2**32))
+        l4 = rng.integers(0, 256, size=size, dtype=np.uint8)
+        fo = 6 if proto == 17 else 16
+        if proto == 17:
+            l4[4], l4[5] = size >> 8, size & 0xFF
+        else:
+            l4[12] = 0x50
+        l4[fo:fo + 2] = 0
+        seed = oracle.pseudo_seed(src, dst, proto, size)
+        c = oracle.batch_spans(l4, np.zeros(1, np.uint64), np.array([size], np.uint32), np.array([seed], np.uint32))
+        l4[fo:fo + 2] = np.frombuffer(np.uint16(c[0]).tobytes(), np.uint8)
+        idx = []
+        for f in synth.ipv4_fragment(l4, proto, src, dst, mtu=mtu, ident=d):
+            idx.append(len(frames))
+            frames.append(f)
+        dgrams.append((proto, src, dst, l4, idx))
+    lens = np.array([f.size for f in frames], np.uint32)
+    off = np.empty(lens.size, np.uint64)
+    pos = 3
+    for i in range(lens.size):
+        pos += int(rng.integers(0, 4))
+        off[i] = pos
+        pos += int(lens[i])
+    buf = rng.integers(0, 256, size=pos + 5, dtype=np.uint8)
+    for i, f in enumerate(frames):
+        buf[int(off[i]):int(off[i]) + f.size] = f
+    return buf, off, lens, dgrams
+
+
+DGRAM_SIZES = [8, 100, 1480, 1481, 2960, 2961, 4000, 9000, 30001, 65515, 65515, 12345]
+
+
+def test_ip_fragments_rx_and_reassembled_l4(dev, kernel_variant):
+    """rx (ip.cc:114-229): every fragment's IPv4 header is verified; a
+    fragment claims no L4 value (SCCSUM_ST_IPFRAG, L4 word 0, never L4_OK);
+    the L4 checksum of the reassembled datagram — its fragments' payloads in
+    offset order, pseudo-header seed, no IP check (ip.cc:120-121) — verifies
+    through sccsum_spans_desc, and a corrupted fragment fails its datagram."""
+    rng = np.random.default_rng(0xF4A6)
+    buf, off, lens, dgrams = _fragmented_datagrams(rng, DGRAM_SIZES)
+    b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+    # the IP header checksums, as ipv4::send writes them per fragment
+    batch.ipv4_fill(b, native.FILL_IP)
+    torch.cuda.synchronize()
+    rx = b.data.cpu().numpy()[: buf.size]
+    got, st = _frames(dev, rx, off, lens)
+    want, want_st = oracle.batch_ipv4(rx, off, lens)
+    assert np.array_equal(got, want) and np.array_equal(st, want_st)
+    for proto, src, dst, l4, idx in dgrams:
+        if len(idx) == 1:
+            assert st[idx[0]] == native.ST_OK | native.ST_L4_OK
+        else:
+            assert np.all(st[idx] == native.ST_OK | native.ST_IPFRAG) and np.all(got[idx, 1] == 0)
+    # the reassembled datagrams: fragments summed where they lie (payload = frame + 20)
+    base = b.data.data_ptr()
+    src_a, dst_off, flen, first, doff, dlen, seeds = [], [], [], [0], [], [], []
+    pos = 0
+    for proto, s_ip, d_ip, l4, idx in dgrams:
+        doff.append(pos)
+        at = 0
+        for i in idx:
+            src_a.append(base + int(off[i]) + 20)
+            dst_off.append(pos + at)
+            flen.append(int(lens[i]) - 20)
+            at += int(lens[i]) - 20
+        first.append(len(src_a))
+        dlen.append(at)
+        seeds.append(oracle.pseudo_seed(s_ip, d_ip, proto, at))
+        pos += at
+    desc = torch.from_numpy(batch.make_desc(np.array(src_a, np.uint64), np.array(dst_off, np.uint32),
+                                            np.array(flen, np.uint32)).view(np.uint8)).to(dev)
+    args = (desc, torch.from_numpy(np.array(first, np.int32)).to(dev),
+            torch.from_numpy(np.array(doff, np.int64)).to(dev), torch.from_numpy(np.array(dlen, np.int32)).to(dev),
+            max(dlen))
+    dst_t = torch.empty(len(dgrams), dtype=torch.uint8, device=dev)
+    r = batch.spans_desc(*args, seeds=torch.from_numpy(np.array(seeds, np.uint32).view(np.int32)).to(dev),
+                         status=dst_t)
+    torch.cuda.synchronize()
+    assert np.all(batch.as_u16(r) == 0) and np.all(dst_t.cpu().numpy() == native.ST_OK)
+    # one payload byte of datagram 7's second fragment flipped: only that datagram fails
+    j = dgrams[7][4][1]
+    b.data[int(off[j]) + 100] ^= 0x41
+    r = batch.as_u16(batch.spans_desc(*args, seeds=torch.from_numpy(np.array(seeds, np.uint32).view(np.int32)).to(dev)))
+    torch.cuda.synchronize()
+    assert r[7] != 0 and np.all(np.delete(r, 7) == 0)
+
+
+def test_ip_fragments_fill(dev, kernel_variant):
+    """tx (ip.cc:244-299): ipv4_fill over the frames of fragmented datagrams
+    writes each fragment's IPv4 header checksum and nothing past its header —
+    the first fragment's L4 checksum (computed over the whole datagram before
+    the cut) and the later fragments' payload are byte-identical — while an
+    unfragmented datagram gets both checksums; byte-exact against the oracle."""
+    rng = np.random.default_rng(0xF4A7)
+    buf, off, lens, dgrams = _fragmented_datagrams(rng, DGRAM_SIZES)
+    for i in range(off.size):  # garbage in every checksum field a fill could write
+        o = int(off[i])
+        buf[o + 10:o + 12] = rng.integers(0, 256, 2)
+    for proto, src, dst, l4, idx in dgrams:
+        if len(idx) == 1:
+            o = int(off[idx[0]]) + 20 + (6 if proto == 17 else 16)
+            buf[o:o + 2] = rng.integers(0, 256, 2)
+    m = native.FILL_IP | native.FILL_L4 | native.FILL_ICMP_ECHO
+    b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+    out2 = torch.empty(2 * b.n, dtype=torch.int16, device=dev)
+    st = torch.empty(b.n, dtype=torch.uint8, device=dev)
+    batch.ipv4_fill(b, m, out2=out2, status=st)
+    torch.cuda.synchronize()
+    want_buf, want_out2, want_st = oracle.batch_ipv4_fill(buf, off, lens, m)
+    got_buf = b.data.cpu().numpy()[: buf.size]
+    assert np.array_equal(got_buf, want_buf)
+    assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want_out2)
+    assert np.array_equal(st.cpu().numpy(), want_st)
+    for proto, src, dst, l4, idx in dgrams:
+        for k, i in enumerate(idx):
+            o, L = int(off[i]), int(lens[i])
+            if len(idx) > 1:
+                assert np.array_equal(got_buf[o + 12:o + L], buf[o + 12:o + L])
+        # the wire bytes after the fill are the datagram the L4 writer produced
+        l4_wire = np.concatenate([got_buf[int(off[i]) + 20:int(off[i]) + int(lens[i])] for i in idx])
+        assert np.array_equal(l4_wire, l4)

@@ -230,3 +230,96 @@ def test_rss_forward_hash_construction(mode):
     # the batch really exercises the branches
     kinds = {len(_fwd_hash(bytes(buf[int(o):int(o) + int(L)]), mode) or b"") for o, L in zip(off, lens)}
     assert {0, 8, 12} <= kinds
+
+
+# ---- rx / tx semantics of the frames drivers (ip.cc:114-299, 464-474) -------
+
+
+def _py_rx(frame: bytes):
+    """(out2 pair, status) of one received frame, restated in Python from
+    ipv4::handle_received_packet (ip.cc:114-229) and the L4 receivers."""
+    if len(frame) < 20:
+        return (0, 0), 4
+    ipc = closed_form(frame[:20])
+    ihl, ip_len, proto = frame[0] & 0xF, (frame[2] << 8) | frame[3], frame[9]
+    fragw = (frame[6] << 8) | frame[7]
+    l4_end = min(ip_len, len(frame))
+    st = 0
+    if len(frame) < ip_len or (fragw & 0x1FFF) * 8 + l4_end > 65535 or 4 * ihl > l4_end:
+        st |= 4
+    if ipc == 0:
+        st |= 1
+    if fragw & 0x3FFF:  # reassembly first: no L4 on a fragment
+        return (ipc, 0), st | 16
+    l4 = frame[4 * ihl:l4_end] if 4 * ihl <= l4_end else b""
+    seed = 0
+    if proto in (6, 17):
+        seed = int.from_bytes(frame[12:16], "big") + int.from_bytes(frame[16:20], "big") + proto + (len(l4) & 0xFFFF)
+    l4c = closed_form(l4, seed)
+    return (ipc, l4c), st | (2 if l4c == 0 else 0)
+
+
+def test_frames_driver_fragments_and_protocols():
+    """oracle_batch_ipv4 on fragments (first / middle / last / past 65 535),
+    ICMP and other protocols (no pseudo-header), TCP / UDP, malformed frames:
+    each frame against the Python restatement of the rx path."""
+    from seastar_amd import synth
+
+    rng = np.random.default_rng(0xF7)
+    n = 3000
+    lens = rng.integers(0, 2200, n).astype(np.uint32)
+    off, total = synth.pack(lens, seed=5, max_gap=3)
+    buf = rng.integers(0, 256, size=int(total) + 8, dtype=np.uint8)
+    fw = synth.frag_words(rng, n)
+    for i in range(n):
+        o, L = int(off[i]), int(lens[i])
+        if L >= 20:
+            ihl = 5 if rng.random() < 0.8 else int(rng.integers(0, 16))
+            ip_len = L if rng.random() < 0.8 else int(rng.integers(0, L + 30))
+            buf[o] = 0x40 | ihl
+            buf[o + 2], buf[o + 3] = ip_len >> 8, ip_len & 0xFF
+            buf[o + 6], buf[o + 7] = int(fw[i]) >> 8, int(fw[i]) & 0xFF
+            buf[o + 9] = int(rng.choice([6, 17, 1, 47]))
+    out2, st = oracle.batch_ipv4(buf, off, lens)
+    seen = set()
+    for i in range(n):
+        fr = bytes(buf[int(off[i]):int(off[i]) + int(lens[i])])
+        want, wst = _py_rx(fr)
+        assert tuple(out2[i]) == want and st[i] == wst, (i, fr[:20].hex())
+        seen.add(wst & 0x1C)
+    assert {0, 4, 16, 20} <= seen
+
+
+def test_fill_driver_icmp_echo_and_fragments():
+    """oracle_batch_ipv4_fill: an ICMP echo request becomes the reply
+    (icmp::received, ip.cc:464-474: type 0, code 0, checksum over the message
+    with the field 0); other ICMP types, fragments and short messages are
+    left alone; an all-zero message gets 0xffff; fragments get the IP
+    checksum only (ip.cc:256-278)."""
+    frames = []
+    msgs = [bytes([8, 5, 0xAA, 0xBB]) + bytes(range(40)), bytes([8, 0, 1, 2]) + bytes(60),
+            bytes([0, 0, 1, 2]) + bytes(range(12)), bytes([8, 0, 1, 2, 3, 4, 5]), bytes([8, 9, 9, 9]) + b"\x01" * 33]
+    for k, m in enumerate(msgs + [msgs[0]]):
+        f = bytearray(20) + m
+        f[0], f[2], f[3], f[9] = 0x45, len(f) >> 8, len(f) & 0xFF, 1
+        if k == len(msgs):  # the same echo request as a first fragment
+            f[6] = 0x20
+        frames.append(bytes(f))
+    lens = np.array([len(f) for f in frames], np.uint32)
+    off = np.concatenate([[1], 1 + np.cumsum(lens)[:-1]]).astype(np.uint64)
+    buf = np.zeros(int(off[-1] + lens[-1]) + 3, np.uint8)
+    for o, f in zip(off, frames):
+        buf[int(o):int(o) + len(f)] = np.frombuffer(f, np.uint8)
+    got, out2, st = oracle.batch_ipv4_fill(buf, off, lens, 0x11)
+    for i, f in enumerate(frames):
+        g = bytes(got[int(off[i]):int(off[i]) + len(f)])
+        assert g[10:12] == closed_form(f[:10] + b"\0\0" + f[12:20]).to_bytes(2, "little")
+        m = f[20:]
+        echo = m[0] == 8 and len(m) >= 8 and i != len(msgs)
+        if echo:
+            r = closed_form(b"\0\0\0\0" + m[4:])
+            assert g[20:] == b"\0\0" + r.to_bytes(2, "little") + m[4:] and out2[i, 1] == r and st[i] & 2
+        else:
+            assert g[20:] == m and not st[i] & 2
+    assert out2[1, 1] == 0xFFFF  # all-zero message
+    assert st[len(msgs)] & 16

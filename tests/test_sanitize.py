@@ -10,7 +10,9 @@ CMakeLists.txt:140-145), applied to the host side of this path:
    (sccsum.hip host side, burst.cc, pipeline.cc, checksummer.cc) built with
    hipcc and the sanitizers on the host compilation only
    (`-Xarch_host -fsanitize=...`; device code is not instrumented), run
-   without a device (tests/cpp/abi_validate.cc).
+   without a device (tests/cpp/abi_validate.cc);
+4. the same program under ThreadSanitizer, its checks run from 8 threads at
+   once (one reactor thread per shard calls the library, reactor.cc:3437).
 """
 import os
 import subprocess
@@ -34,8 +36,8 @@ def _oracle_obj(tmp_path):
     return obj
 
 
-def _exec(exe, tmp_path):
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=ENV, cwd=tmp_path)
+def _exec(exe, tmp_path, args=()):
+    r = subprocess.run([exe, *args], capture_output=True, text=True, timeout=300, env=ENV, cwd=tmp_path)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert "OK" in r.stdout and "runtime error" not in r.stderr
     return r
@@ -71,3 +73,22 @@ def test_abi_validation_sanitized(tmp_path):
           os.path.join(csrc, "pipeline.cc"), os.path.join(csrc, "burst.cc"),
           os.path.join(REPO, "tests", "cpp", "abi_validate.cc"), "-o", exe], tmp_path)
     _exec(exe, tmp_path)
+
+
+def test_abi_validation_threads_tsan(tmp_path):
+    """The C-ABI's host side (thread-local knobs, argument checks, the
+    burst / pipeline constructors' failure paths) driven from 8 threads under
+    ThreadSanitizer, host code only: no data race may be reported."""
+    exe = str(tmp_path / "abi_validate_tsan")
+    host_san = []
+    for f in ("-fsanitize=thread", "-fno-omit-frame-pointer"):
+        host_san += ["-Xarch_host", f]
+    csrc = os.path.join(REPO, "seastar_amd", "csrc")
+    _run(["/opt/rocm/bin/hipcc", "-O1", "-g", "--offload-arch=gfx950", "-std=c++17", *host_san,
+          "-I", os.path.join(REPO, "include"), os.path.join(csrc, "sccsum.hip"), os.path.join(csrc, "checksummer.cc"),
+          os.path.join(csrc, "pipeline.cc"), os.path.join(csrc, "burst.cc"),
+          os.path.join(REPO, "tests", "cpp", "abi_validate.cc"), "-o", exe], tmp_path)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    r = subprocess.run([exe, "8"], capture_output=True, text=True, timeout=300, env=env, cwd=tmp_path)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert "OK (8 threads)" in r.stdout and "ThreadSanitizer" not in r.stderr

@@ -1,0 +1,92 @@
+#!/bin/bash
+# One parametrised GPU session (replaces round 2's one-off runners, which are in
+# git history): run on the GPU box through gpurun, e.g.
+#   gpurun --timeout 1200 -- 'bash tools/gpu_session.sh r03a pytest bench:udp1500 prof:fill'
+# Steps (in order; each GPU step has its own time limit and the steps chain:
+# the first failure, time limit or fault ends the session):
+#   pytest                 the GPU test suite (-m gpu), one process
+#   smoke                  __graft_entry__.smoke()
+#   headline               bench.py as the driver runs it (N=1, CPU baseline included)
+#   bench:CFG[+ARG...]     bench.py --config CFG --steps 20 --no-cpu ARG...   (ARGs joined by '+')
+#   trace:CFG[+ARG...]     rocprofv3 --kernel-trace --stats of the bench command
+#   prof:CFG[+ARG...]      trace + separate FETCH_SIZE and WRITE_SIZE passes of the bench command,
+#                          cut to the timed dispatches by tools/prof_timed.py ($TAG_pmc_CFG.json)
+#   py:SCRIPT[+ARG...]     python SCRIPT ARG... (a tools/ probe)
+# Outputs go to gpurun_out/TAG/; steps.log records each step's outcome.
+set -o pipefail
+TAG=${1:?usage: gpu_session.sh TAG STEP...}
+shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$R" || exit 1
+export TMPDIR=/tmp
+PROF_STEPS="--steps 10 --warmup 2 --no-cpu"
+
+split() {  # split CFG+A+B -> CFG and args array ARGS
+    local IFS='+'
+    read -r -a parts <<< "$1"
+    CFG=${parts[0]}
+    ARGS=("${parts[@]:1}")
+}
+
+name_of() {  # file-name form of a step's config + args
+    echo "$1" | tr '+' '_' | tr -d '-'
+}
+
+run_step() {
+    local step=$1 kind=${1%%:*} rest=${1#*:}
+    local n
+    n=$(name_of "$rest")
+    case $kind in
+        pytest)
+            timeout -k 10 900 python -u -m pytest tests -m gpu ${PYTEST_X--x} -v --timeout 120 --timeout-method thread \
+                > "$O/pytest_gpu.log" 2>&1 ;;
+        smoke)
+            timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > "$O/smoke.log" 2>&1 ;;
+        headline)
+            timeout -k 10 400 python bench.py > "$O/bench_headline.log" 2>&1 ;;
+        bench)
+            split "$rest"
+            timeout -k 10 400 python bench.py --config "$CFG" --steps 20 --no-cpu "${ARGS[@]}" \
+                >> "$O/bench_$n.log" 2>&1 ;;
+        trace)
+            split "$rest"
+            (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/trace_$n" -o run \
+                --output-format csv -- python3 "$R/bench.py" --config "$CFG" $PROF_STEPS "${ARGS[@]}") \
+                > "$O/trace_$n.log" 2>&1 ;;
+        prof)
+            split "$rest"
+            (cd /tmp && \
+             timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$n/trace" -o run --output-format csv \
+                -- python3 "$R/bench.py" --config "$CFG" $PROF_STEPS "${ARGS[@]}" > "$O/prof_${n}_trace.log" 2>&1 && \
+             timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$O/prof_$n/fetch" -o run --output-format csv \
+                -- python3 "$R/bench.py" --config "$CFG" $PROF_STEPS "${ARGS[@]}" > "$O/prof_${n}_fetch.log" 2>&1 && \
+             timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$O/prof_$n/write" -o run --output-format csv \
+                -- python3 "$R/bench.py" --config "$CFG" $PROF_STEPS "${ARGS[@]}" > "$O/prof_${n}_write.log" 2>&1) && \
+            python tools/prof_timed.py --bench-log "$O/prof_${n}_trace.log" --trace "$O/prof_$n/trace" \
+                --fetch "$O/prof_$n/fetch" --write "$O/prof_$n/write" --probe-bytes "${PROBE_BYTES:-0}" \
+                --config "$CFG" --label "$TAG bench.py --config $CFG $PROF_STEPS ${ARGS[*]}" \
+                --out "$O/${TAG}_pmc_$n.json" --trace-out "$O/${TAG}_trace_$n.csv" > "$O/prof_${n}_summary.log" 2>&1 ;;
+        py)
+            split "$rest"
+            timeout -k 10 400 python "$CFG" "${ARGS[@]}" >> "$O/py_$(basename "$CFG" .py).log" 2>&1 ;;
+        *)
+            echo "unknown step $step" >> "$O/steps.log"
+            return 2 ;;
+    esac
+}
+
+echo "start $(date)" >> "$O/steps.log"
+rc=0
+for step in "$@"; do
+    run_step "$step"
+    rc=$?
+    echo "$step rc=$rc $(date +%T)" >> "$O/steps.log"
+    [ $rc -eq 0 ] || break
+done
+echo "exit=$rc $(date)" >> "$O/steps.log"
+grep -h '^{' "$O"/bench*.log 2>/dev/null | cut -c1-600
+tail -3 "$O/pytest_gpu.log" 2>/dev/null
+cat "$O/steps.log"
+exit $rc
