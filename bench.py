@@ -56,6 +56,17 @@ def flat_kernel(ipv4: bool, fill: bool, n: int, nbytes: int) -> str:
     return f"csum_flat_kernel<{u}, {str(ipv4).lower()}, {str(fill).lower()}, {pipe}>"
 
 
+def sparse_kernel(args, ipv4: bool, max_len: int) -> str:
+    """The kernel a sparse layout gets (sccsum.hip pick_variant / launch_rows),
+    as rocprofv3 names it: the row kernel (V units per lane from max_len), or
+    the row-pair form with --variant 3."""
+    if args.variant == 3:
+        return f"csum_wrow_kernel<4, {str(ipv4).lower()}>"
+    units = (max_len + 30) // 16
+    v = 2 if units <= 32 else 4 if units <= 64 else 6 if units <= 96 else 8
+    return f"csum_row_kernel<{v}, {str(ipv4).lower()}>"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -685,7 +696,7 @@ def run_slots(args, world, rank, dev):
         batch.verify_frames(b, st)
         torch.cuda.synchronize()
         assert int((st != 3).sum()) == 0, "slot frames do not verify"
-    kern = "csum_row_kernel<6, true>"
+    kern = sparse_kernel(args, True, FRAME)
     LAUNCHES.add(kern, R)
     stream = torch.cuda.current_stream()
     warm = max(args.warmup, R)
@@ -746,7 +757,7 @@ def run_frags(args, world, rank, dev):
         torch.cuda.synchronize()
         assert torch.equal(got[:k], ref), "fragment lists differ from the contiguous packets"
         want.append(got.clone())
-    kern = "csum_row_kernel<8, false>"  # the raw pass over the fragments (a sparse layout)
+    kern = sparse_kernel(args, False, 2048)  # the raw pass over the fragments (a sparse layout)
     LAUNCHES.add(kern, R)
     stream = torch.cuda.current_stream()
     pre = [batch.prepare_call("sccsum_fragments", pools[r], n * nf * slot, frag_off, frag_len, n * nf, first, seeds,

@@ -44,7 +44,8 @@ int sccsum_set_tile_packets(int packets);
 /* Flat kernel: target bytes per tile (default 49152; 0 = only the 64-packet cap). */
 int sccsum_set_tile_bytes(int bytes);
 
-/* Flat kernel: tiles dequeued from per-stream counters (1, the default) or
+/* Flat kernel: tiles dequeued from a counter slot of the device's pool (1, the
+ * default; a launch that finds no free slot deals them round robin anyway) or
  * dealt round robin (0). */
 int sccsum_set_dynamic_tiles(int on);
 

@@ -686,6 +686,134 @@ __device__ __forceinline__ void tile_store(T* t, uint32_t lane, T v, uint32_t po
     }
 }
 
+// One packet per 64-lane ROW PAIR, K packets per round trip (variant 3, a
+// sparse-layout form): packet k's units 0..63 and 64..127 are two rows whose
+// base address is wave-uniform, so each load instruction reads 1 KiB of one
+// packet (the row kernel's read 4 x 256 B of four packets), and a wave keeps
+// K packets' bytes in flight together.  Longer packets continue with further
+// row pairs, one packet at a time.  Per-lane byte masks select the summed
+// range (frame mode: [4*ihl, min(ip_len, len)), from the header in the first
+// row's lanes 0..3), as csum_kernel does, so no packet needs a slow path.
+// A block takes 64 consecutive packets at a time (as csum_row_kernel: the
+// chunk's results leave one block, as whole lines).
+template <int K, bool IPV4>
+__global__ __launch_bounds__(kBlock) void csum_wrow_kernel(
+    const uint8_t* __restrict__ bytes, uint64_t bytes_len,
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
+    const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
+    uint8_t* __restrict__ status, uint64_t n, uint32_t flags) {
+    constexpr uint32_t kChunk = 64;
+    constexpr uint32_t kPerWave = kChunk / kWavesPerBlock;  // 16 packets of the chunk per wave
+    static_assert(kPerWave % K == 0, "a wave's share is whole groups of K");
+    const bool raw = !IPV4 && (flags & kFlagRaw);
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
+    auto rl = [](uint32_t v, uint32_t k) {
+        return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(k)));
+    };
+    for (uint64_t ch = xcd_block_id(); ch < nchunks; ch += gridDim.x) {
+        for (uint32_t grp = 0; grp < kPerWave / K; ++grp) {
+            const uint64_t p0 = ch * kChunk + wv * kPerWave + grp * K;
+            if (p0 >= n) break;
+            // lanes 0..K-1: the group's metadata, one round trip
+            uint64_t mo = 0;
+            uint32_t mL = 0, msd = 0;
+            if (lane < K && p0 + lane < n) {
+                mo = off[p0 + lane];
+                mL = len[p0 + lane];
+                if (!IPV4 && seed) msd = seed[p0 + lane];
+            }
+            uint64_t a0[K];
+            uint32_t L[K], head[K], nun[K], stbad[K];
+            bool bad[K];
+            u32x4 v[2 * K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint64_t o = (static_cast<uint64_t>(rl(static_cast<uint32_t>(mo >> 32), k)) << 32) |
+                                   rl(static_cast<uint32_t>(mo), k);
+                L[k] = rl(mL, k);
+                const bool in = p0 + k < n;
+                const bool rbad = in && (o > bytes_len || L[k] > bytes_len - o);
+                bad[k] = !in || rbad || (IPV4 && L[k] < 20);
+                stbad[k] = rbad ? SCCSUM_ST_RANGE : SCCSUM_ST_MALFORMED;
+                const uint64_t ptr = reinterpret_cast<uint64_t>(bytes) + (bad[k] ? 0 : o);
+                head[k] = static_cast<uint32_t>(ptr & 15u);
+                a0[k] = ptr - head[k];
+                nun[k] = (!bad[k] && L[k]) ? (head[k] + L[k] + 15u) >> 4 : 0u;
+                const u32x4* a = reinterpret_cast<const u32x4*>(a0[k]);
+                v[2 * k] = lane < nun[k] ? load_unit(reinterpret_cast<const uint8_t*>(a + lane)) : u32x4{0, 0, 0, 0};
+                v[2 * k + 1] =
+                    64u + lane < nun[k] ? load_unit(reinterpret_cast<const uint8_t*>(a + 64 + lane)) : u32x4{0, 0, 0, 0};
+            }
+            uint32_t word_mine = 0, st_mine = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                int rs = static_cast<int>(head[k]), re = static_cast<int>(head[k] + L[k]);
+                uint32_t ipc = 0, pseudo = 0, st = 0;
+                if (IPV4 && !bad[k]) {
+                    const u32x4 hu[4] = {
+                        u32x4{rl(v[2 * k].x, 0), rl(v[2 * k].y, 0), rl(v[2 * k].z, 0), rl(v[2 * k].w, 0)},
+                        u32x4{rl(v[2 * k].x, 1), rl(v[2 * k].y, 1), rl(v[2 * k].z, 1), rl(v[2 * k].w, 1)},
+                        u32x4{rl(v[2 * k].x, 2), rl(v[2 * k].y, 2), rl(v[2 * k].z, 2), rl(v[2 * k].w, 2)},
+                        u32x4{0, 0, 0, 0}};
+                    const FrameHeader F = frame_header(header_dword(hu, head[k], 0), header_dword(hu, head[k], 1),
+                                                       header_dword(hu, head[k], 2), header_dword(hu, head[k], 3),
+                                                       header_dword(hu, head[k], 4), L[k]);
+                    ipc = F.ipc;
+                    pseudo = F.pseudo;
+                    st = F.st;
+                    rs = static_cast<int>(head[k] + F.l4_off);
+                    re = rs + static_cast<int>(F.l4_len);
+                }
+                uint64_t acc = unit_sum(v[2 * k], rs - static_cast<int>(16 * lane), re - static_cast<int>(16 * lane)) +
+                               unit_sum(v[2 * k + 1], rs - static_cast<int>(16 * (64 + lane)),
+                                        re - static_cast<int>(16 * (64 + lane)));
+                // the rest of a packet longer than 128 units, two rows at a time
+                for (uint32_t g = 128; g < nun[k]; g += 128) {
+                    const u32x4* a = reinterpret_cast<const u32x4*>(a0[k]) + g;
+                    const u32x4 w0 = g + lane < nun[k] ? load_unit(reinterpret_cast<const uint8_t*>(a + lane))
+                                                       : u32x4{0, 0, 0, 0};
+                    const u32x4 w1 = g + 64u + lane < nun[k]
+                                         ? load_unit(reinterpret_cast<const uint8_t*>(a + 64 + lane))
+                                         : u32x4{0, 0, 0, 0};
+                    const int c0 = static_cast<int>(16 * (g + lane)), c1 = static_cast<int>(16 * (g + 64 + lane));
+                    acc += unit_sum(w0, rs - c0, re - c0) + unit_sum(w1, rs - c1, re - c1);
+                }
+                uint32_t S = fold16(wave_sum(fold16(acc)));
+                if (head[k] & 1u) S = swap16(S);
+                uint32_t word, stw;
+                if (IPV4) {
+                    const uint32_t r = ~fold16(static_cast<uint64_t>(S) + pseudo) & 0xffffu;
+                    word = frame_word(ipc, r, st);
+                    stw = frame_status(ipc, r, st);
+                } else {
+                    const uint32_t sd = rl(msd, k);
+                    const uint32_t r = raw ? S : ~fold16(static_cast<uint64_t>(S) + swap16(fold16(sd))) & 0xffffu;
+                    word = r;
+                    stw = (!raw && r == 0) ? SCCSUM_ST_OK : 0u;
+                }
+                if (bad[k]) {
+                    word = 0;
+                    stw = stbad[k];
+                }
+                if (lane == static_cast<uint32_t>(k)) {
+                    word_mine = word;
+                    st_mine = stw;
+                }
+            }
+            if (lane < K && p0 + lane < n) {
+                if (IPV4) {
+                    if (out) reinterpret_cast<uint32_t*>(out)[p0 + lane] = word_mine;
+                } else {
+                    out[p0 + lane] = static_cast<uint16_t>(word_mine);
+                }
+                if (status) status[p0 + lane] = static_cast<uint8_t>(st_mine);
+            }
+        }
+    }
+}
+
 constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B) between packets
 
 // The batches one flat-kernel launch works through: up to kMaxQueues
@@ -1607,6 +1735,20 @@ void launch_simple(int uc, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
 }
 
 template <bool IPV4>
+void launch_wrows(hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
+                  const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n, uint32_t flags) {
+    auto kern = csum_wrow_kernel<4, IPV4>;
+    const int occ = kernel_occupancy(reinterpret_cast<const void*>(kern));
+    const uint64_t bpc = static_cast<uint64_t>(occ < t_knobs.blocks_per_cu ? occ : t_knobs.blocks_per_cu);
+    const uint64_t cap = static_cast<uint64_t>(cu_count()) * bpc;
+    uint64_t blocks = (n + 63u) / 64u;  // a block takes 64-packet chunks
+    blocks = blocks < cap ? blocks : cap;
+    blocks = (blocks + 7u) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
+    kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out,
+                                                                     d_status, n, flags);
+}
+
+template <bool IPV4>
 void launch_rows(uint32_t max_len, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
                  const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
                  uint32_t flags) {
@@ -1700,7 +1842,7 @@ int pick_variant(uint64_t n_total, uint64_t bytes_total, uint32_t flags, uint32_
     const bool fill = (flags & kFillFlags) != 0;
     const bool sparse = max_len != 0 && n_total != 0 && bytes_total / n_total >= uint64_t(max_len) + 64u;
     if (variant == 0 && sparse && !fill) return 2;
-    if (variant == 0 || ((variant == 1 || variant == 2) && fill)) variant = dflt;  // in-place write-back: flat only
+    if (variant == 0 || ((variant == 1 || variant == 2 || variant == 3) && fill)) variant = dflt;  // in place: flat only
     return variant;
 }
 
@@ -1713,10 +1855,12 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
     const int variant = pick_variant(n, bytes_len, flags, max_len);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
-    if (variant == 1 || variant == 2) {
+    if (variant == 1 || variant == 2 || variant == 3) {
         if (variant == 1) {
             launch_simple<IPV4>(units_class(max_len), s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n,
                                 flags);
+        } else if (variant == 3) {
+            launch_wrows<IPV4>(s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
         } else {
             launch_rows<IPV4>(max_len, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
         }
@@ -1757,13 +1901,16 @@ int launch_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
     if (n_total == 0) return SCCSUM_OK;
     const int variant = pick_variant(n_total, bytes_total, 0, max_len);
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    if (variant == 1 || variant == 2) {  // the per-packet kernels take one batch per launch
+    if (variant == 1 || variant == 2 || variant == 3) {  // the per-packet kernels take one batch per launch
         for (uint32_t i = 0; i < nbatch; ++i) {
             const sccsum_batch& x = batches[i];
             if (!x.n) continue;
             if (variant == 1) {
                 launch_simple<IPV4>(units_class(max_len), s, static_cast<const uint8_t*>(x.d_bytes), x.bytes_len,
                                     x.d_off, x.d_len, x.d_seed, static_cast<uint16_t*>(x.d_out), x.d_status, x.n, 0);
+            } else if (variant == 3) {
+                launch_wrows<IPV4>(s, static_cast<const uint8_t*>(x.d_bytes), x.bytes_len, x.d_off, x.d_len,
+                                   x.d_seed, static_cast<uint16_t*>(x.d_out), x.d_status, x.n, 0);
             } else {
                 launch_rows<IPV4>(max_len, s, static_cast<const uint8_t*>(x.d_bytes), x.bytes_len, x.d_off, x.d_len,
                                   x.d_seed, static_cast<uint16_t*>(x.d_out), x.d_status, x.n, 0);
@@ -2208,7 +2355,9 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
 }
 
 int sccsum_set_kernel_variant(int variant) {
-    if (!(variant == 0 || variant == 1 || variant == 2 || (variant >= 14 && variant <= 16))) return SCCSUM_EINVAL;
+    if (!(variant == 0 || variant == 1 || variant == 2 || variant == 3 || (variant >= 14 && variant <= 16))) {
+        return SCCSUM_EINVAL;
+    }
     sccsum::t_knobs.variant = variant;
     return SCCSUM_OK;
 }

@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(params=[1, 2, 14, 15, 16], ids=["simple", "rows", "flat8", "flat8_pipe", "flat16"], autouse=True)
+@pytest.fixture(params=[1, 2, 3, 14, 15, 16], ids=["simple", "rows", "wrows", "flat8", "flat8_pipe", "flat16"],
+                autouse=True)
 def kernel_variant(request, dev):
     """Every parity test runs against both kernel families."""
     lib = native.load()
@@ -300,10 +301,16 @@ def test_host_pipeline_zero_copy_refuses_pageable_memory(dev):
                                            off64.ctypes.data, l32.ctypes.data, None, lens.size, 1500,
                                            out.ctypes.data, None)
     assert rc == native.SCCSUM_EINVAL
-    pinned = pipeline.pinned_empty(buf.size)
-    pinned[:] = buf
-    got = pl.run(native.PIPE_IPV4, pinned, off, lens, gather=native.GATHER_ZERO_COPY, max_len=1500)
+    pinned = pipeline.pinned_empty(buf.size + 64)
+    pinned[64:] = buf
+    got = pl.run(native.PIPE_IPV4, pinned[64:], off, lens, gather=native.GATHER_ZERO_COPY, max_len=1500)
     assert np.array_equal(got, oracle.batch_ipv4(buf, off, lens)[0])
+    # the whole range must lie in ONE pinned allocation: a host_len that runs past the block is refused
+    # (an ends-only check would pass two pinned blocks with pageable memory between them: ADVICE r02)
+    rc = native.load().sccsum_pipeline_run(pl._h, native.PIPE_IPV4, native.GATHER_ZERO_COPY, pinned.ctypes.data,
+                                           pinned.size + (1 << 20), off64.ctypes.data, l32.ctypes.data, None,
+                                           lens.size, 1500, out.ctypes.data, None)
+    assert rc == native.SCCSUM_EINVAL
     pl.close()
     assert ctypes.sizeof(ctypes.c_void_p) == 8
 
@@ -1244,3 +1251,33 @@ def test_ip_fragments_fill(dev, kernel_variant):
         # the wire bytes after the fill are the datagram the L4 writer produced
         l4_wire = np.concatenate([got_buf[int(off[i]) + 20:int(off[i]) + int(lens[i])] for i in idx])
         assert np.array_equal(l4_wire, l4)
+
+
+def test_scratch_on_a_side_stream(dev, kernel_variant):
+    """ipv4_fill(FILL_L4) and fragments() on a stream that is not torch's
+    current one, with library-allocated scratch (out2 / workspace): the
+    scratch is recorded on the launch stream, so allocations churned on the
+    current stream meanwhile cannot take its block while the kernels still
+    use it.  Results byte-exact against the oracle."""
+    if kernel_variant not in (1, 16):
+        pytest.skip("scratch lifetime is kernel independent")
+    rng = np.random.default_rng(0x5C1)
+    buf, off, length = _tx_frames(rng, 4000)
+    b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+    fb, fo, fl, first = _frag_batch(rng, 3000, lambda i: [int(x) for x in rng.integers(1, 700, int(rng.integers(1, 6)))])
+    d = torch.from_numpy(np.concatenate([fb, np.zeros(16, np.uint8)])).to(dev)
+    args = (d, fb.size, torch.from_numpy(fo.view(np.int64)).to(dev), torch.from_numpy(fl.view(np.int32)).to(dev),
+            torch.from_numpy(first.view(np.int32)).to(dev))
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream(device=dev)
+    m = native.FILL_IP | native.FILL_L4 | native.FILL_ICMP_ECHO
+    for _ in range(3):
+        batch.ipv4_fill(b, m, stream=side)  # out2 scratch allocated by the wrapper
+        got = batch.fragments(*args, stream=side)  # workspace allocated by the wrapper
+        junk = [torch.full((1 << 20,), 7, dtype=torch.uint8, device=dev) for _ in range(8)]  # churn, current stream
+        del junk
+        side.synchronize()
+    torch.cuda.synchronize()
+    want_buf, _, _ = oracle.batch_ipv4_fill(buf, off, length, m)
+    assert np.array_equal(b.data.cpu().numpy()[: buf.size], want_buf)
+    assert np.array_equal(batch.as_u16(got), oracle.batch_fragments(fb, fo, fl, first))

@@ -45,3 +45,46 @@ def test_mixed_frames_and_packing():
     assert np.any(off % 2 == 1)
     out, st = oracle.batch_ipv4(buf, off, lens)
     assert np.all((st & 4) == 0)
+
+
+def test_ipv4_fragment_cuts_like_ipv4_send():
+    """synth.ipv4_fragment follows ipv4::send (ip.cc:244-299): pieces of
+    mtu - 20 bytes, MF on all but the last, offsets in 8-byte units, one
+    header per piece; a datagram that fits goes out whole with frag = 0."""
+    import numpy as np
+
+    from seastar_amd import synth
+
+    rng = np.random.default_rng(3)
+    for size in (8, 1480, 1481, 2960, 9000, 65515):
+        l4 = rng.integers(0, 256, size, dtype=np.uint8)
+        frames = synth.ipv4_fragment(l4, 17, 0x0A000001, 0x0A000002, mtu=1500, ident=77)
+        assert len(frames) == max(1, -(-size // 1480))
+        at = 0
+        for k, f in enumerate(frames):
+            ip_len = (int(f[2]) << 8) | int(f[3])
+            fw = (int(f[6]) << 8) | int(f[7])
+            assert ip_len == f.size and f[0] == 0x45 and f[9] == 17 and (int(f[4]) << 8 | int(f[5])) == 77
+            if len(frames) == 1:
+                assert fw == 0
+            else:
+                assert (fw & 0x1FFF) * 8 == at and bool(fw & 0x2000) == (k + 1 < len(frames))
+            assert np.array_equal(f[20:], l4[at:at + f.size - 20])
+            at += f.size - 20
+        assert at == size
+
+
+def test_frag_words_mix():
+    import numpy as np
+
+    from seastar_amd import synth
+
+    w = synth.frag_words(np.random.default_rng(5), 20000)
+    frag = (w & 0x3FFF) != 0
+    assert 0.2 < frag.mean() < 0.4
+    mf, off = (w & 0x2000) != 0, (w & 0x1FFF) != 0
+    assert np.any(mf & ~off)  # first fragments
+    assert np.any(mf & off)   # middle fragments
+    assert np.any(~mf & off)  # last fragments
+    assert np.any((w & 0x1FFF) * 8 > 62000)                   # offsets near the 65 535-byte limit
+    assert np.any(w == 0x4000)                                # DF alone: atomic

@@ -12,6 +12,7 @@
 #   prof:CFG[+ARG...]      trace + separate FETCH_SIZE and WRITE_SIZE passes of the bench command,
 #                          cut to the timed dispatches by tools/prof_timed.py ($TAG_pmc_CFG.json)
 #   py:SCRIPT[+ARG...]     python SCRIPT ARG... (a tools/ probe)
+#   bin:PROGRAM[+ARG...]   a probe program built here beforehand (tools/dev/*.hip)
 # Outputs go to gpurun_out/TAG/; steps.log records each step's outcome.
 set -o pipefail
 TAG=${1:?usage: gpu_session.sh TAG STEP...}
@@ -71,6 +72,9 @@ run_step() {
         py)
             split "$rest"
             timeout -k 10 400 python "$CFG" "${ARGS[@]}" >> "$O/py_$(basename "$CFG" .py).log" 2>&1 ;;
+        bin)
+            split "$rest"
+            timeout -k 10 400 "./$CFG" "${ARGS[@]}" >> "$O/bin_$(basename "$CFG").log" 2>&1 ;;
         *)
             echo "unknown step $step" >> "$O/steps.log"
             return 2 ;;
