@@ -500,7 +500,7 @@ def test_ipv4_fill_in_place(dev, mode):
         assert len(replies) > 20
         for i in icmp:
             o, L = int(off[i]), int(length[i])
-            ihl4 = 4 * (buf[o] & 0xF)
+            ihl4 = 4 * (int(buf[o]) & 0xF)
             if i in replies:
                 assert buf[o + ihl4] == 8 and got_buf[o + ihl4] == 0 and got_buf[o + ihl4 + 1] == 0
             else:
