@@ -307,6 +307,41 @@ __global__ __launch_bounds__(kBlock) void csum_kernel(
     }
 }
 
+// Keep bytes [lo, hi) of a 64-bit half unit (half-relative byte indices).
+__device__ __forceinline__ uint64_t keep_half(uint64_t q, int lo, int hi) {
+    const int a = min(max(lo, 0), 8);
+    const int b = min(max(hi, 0), 8);
+    const int w = b - a;
+    const int sh = w > 0 ? 64 - 8 * w : 0;
+    const uint64_t m = (~0ull >> sh) << (8 * (w > 0 ? a : 0));
+    return w > 0 ? (q & m) : 0ull;
+}
+
+// Sum the four dwords of a unit as 16-bit halves into a 32-bit accumulator
+// (v_sad_u16 with a zero operand: lo16 + hi16 + acc, one instruction per dword).
+__device__ __forceinline__ uint32_t sad4(const u32x4& v, uint32_t acc) {
+    acc = __builtin_amdgcn_sad_u16(v.x, 0u, acc);
+    acc = __builtin_amdgcn_sad_u16(v.y, 0u, acc);
+    acc = __builtin_amdgcn_sad_u16(v.z, 0u, acc);
+    return __builtin_amdgcn_sad_u16(v.w, 0u, acc);
+}
+
+// Masked unit (bytes [lo, hi) kept, unit-relative) summed like sad4.
+__device__ __forceinline__ uint32_t sad4_masked(const u32x4& v, int lo, int hi, uint32_t acc) {
+    const uint64_t k0 = keep_half(static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32), lo, hi);
+    const uint64_t k1 = keep_half(static_cast<uint64_t>(v.z) | (static_cast<uint64_t>(v.w) << 32), lo - 8, hi - 8);
+    acc = __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k0), 0u, acc);
+    acc = __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k0 >> 32), 0u, acc);
+    acc = __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k1), 0u, acc);
+    return __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k1 >> 32), 0u, acc);
+}
+
+// Sum of the bytes [lo, hi) of a 16-byte unit as little-endian 16-bit words
+// at their unit-relative positions (sad4 of the masked unit).
+__device__ __forceinline__ uint32_t unit_part(const u32x4& v, int lo, int hi) {
+    return sad4_masked(v, lo, hi, 0u);
+}
+
 // Sum of v over each 16-lane row, in every lane of the row (the first four
 // steps of wave_sum).  All lanes of a row must be active.
 __device__ __forceinline__ uint32_t row_sum(uint32_t v) {
@@ -398,23 +433,39 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
             rs = head + static_cast<int>(F.l4_off);
             re = rs + static_cast<int>(F.l4_len);
         }
+        // Whole units summed with v_sad_u16 (one instruction per dword, exact in
+        // 32 bits per group), then the bytes outside [rs, re) taken off once:
+        // units wholly past re are dropped, the head part [0, rs) comes from
+        // the first row of units (the IPv4 header and options end within unit
+        // 4), and the tail part from the one unit per packet holding re - 1 —
+        // selected first, then masked once, so the byte masks cost one unit per
+        // lane instead of V (profiles/r03_ab_rows.log).
         uint64_t acc = 0;
+        auto group = [&](uint32_t g) {
+            uint32_t sum = 0;
+            u32x4 tv = u32x4{0, 0, 0, 0};
+            int tc16 = 0;
 #pragma unroll
-        for (int u = 0; u < V; ++u) {
-            const int c16 = 16 * static_cast<int>(static_cast<uint32_t>(u) * kRow + r);
-            acc += unit_sum(v[u], rs - c16, re - c16);
-        }
+            for (int u = 0; u < V; ++u) {
+                const int c16 = 16 * static_cast<int>(g + static_cast<uint32_t>(u) * kRow + r);
+                const uint32_t full = sad4(v[u], 0u);
+                sum += c16 < re ? full : 0u;
+                const bool tail = c16 < re && c16 + 16 > re;
+                tv = tail ? v[u] : tv;
+                tc16 = tail ? c16 : tc16;
+            }
+            sum -= unit_part(tv, re - tc16, 16);
+            if (g == 0) sum -= unit_part(v[0], 0, rs - 16 * static_cast<int>(r));
+            acc += sum;
+        };
+        group(0);
         for (uint32_t g = V * kRow; g < nunits; g += V * kRow) {
 #pragma unroll
             for (int u = 0; u < V; ++u) {
                 const uint32_t c = g + static_cast<uint32_t>(u) * kRow + r;
                 v[u] = c < nunits ? load_unit(a0 + 16u * c) : u32x4{0, 0, 0, 0};
             }
-#pragma unroll
-            for (int u = 0; u < V; ++u) {
-                const int c16 = 16 * static_cast<int>(g + static_cast<uint32_t>(u) * kRow + r);
-                acc += unit_sum(v[u], rs - c16, re - c16);
-            }
+            group(g);
         }
         uint32_t S = fold16(row_sum(fold16(acc)));
         if (addr & 1u) S = swap16(S);
@@ -438,35 +489,6 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
 
 // ---------------------------------------------------------------- flat-kernel helpers
 
-// Keep bytes [lo, hi) of a 64-bit half unit (half-relative byte indices).
-__device__ __forceinline__ uint64_t keep_half(uint64_t q, int lo, int hi) {
-    const int a = min(max(lo, 0), 8);
-    const int b = min(max(hi, 0), 8);
-    const int w = b - a;
-    const int sh = w > 0 ? 64 - 8 * w : 0;
-    const uint64_t m = (~0ull >> sh) << (8 * (w > 0 ? a : 0));
-    return w > 0 ? (q & m) : 0ull;
-}
-
-// Sum the four dwords of a unit as 16-bit halves into a 32-bit accumulator
-// (v_sad_u16 with a zero operand: lo16 + hi16 + acc, one instruction per dword).
-__device__ __forceinline__ uint32_t sad4(const u32x4& v, uint32_t acc) {
-    acc = __builtin_amdgcn_sad_u16(v.x, 0u, acc);
-    acc = __builtin_amdgcn_sad_u16(v.y, 0u, acc);
-    acc = __builtin_amdgcn_sad_u16(v.z, 0u, acc);
-    return __builtin_amdgcn_sad_u16(v.w, 0u, acc);
-}
-
-// Masked unit (bytes [lo, hi) kept, unit-relative) summed like sad4.
-__device__ __forceinline__ uint32_t sad4_masked(const u32x4& v, int lo, int hi, uint32_t acc) {
-    const uint64_t k0 = keep_half(static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32), lo, hi);
-    const uint64_t k1 = keep_half(static_cast<uint64_t>(v.z) | (static_cast<uint64_t>(v.w) << 32), lo - 8, hi - 8);
-    acc = __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k0), 0u, acc);
-    acc = __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k0 >> 32), 0u, acc);
-    acc = __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k1), 0u, acc);
-    return __builtin_amdgcn_sad_u16(static_cast<uint32_t>(k1 >> 32), 0u, acc);
-}
-
 constexpr int kRsrcFlags = 0x00020000;  // raw buffer, 32-bit data format (gfx950)
 constexpr int kNT = 2;                  // nontemporal: streamed once
 
@@ -480,12 +502,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* base, uint
     const uint32_t nb = __builtin_amdgcn_readfirstlane(bytes);
     void* p = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
     return __builtin_amdgcn_make_buffer_rsrc(p, static_cast<short>(0), static_cast<int>(nb), kRsrcFlags);
-}
-
-// Sum of the bytes [lo, hi) of a 16-byte unit as little-endian 16-bit words
-// at their unit-relative positions (sad4 of the masked unit).
-__device__ __forceinline__ uint32_t unit_part(const u32x4& v, int lo, int hi) {
-    return sad4_masked(v, lo, hi, 0u);
 }
 
 constexpr uint32_t kExactMax = 131072;  // fast path keeps exact 32-bit sums up to this length
@@ -937,12 +953,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
             uint32_t* h = heads + grp * kHeadStride;
             d = __hip_atomic_fetch_add(h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (d == tiles_g + waves_g - 1) {
+                // The slot's words are only ever touched by agent-scope atomics,
+                // which are performed at the device's coherence point; waiting
+                // for each to complete (s_waitcnt) orders reset -> count ->
+                // report without the L2 write-backs a release fence costs
+                // (profiles/r03_ab_pool.log).
                 __hip_atomic_store(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 uint32_t* const groups_done = heads + kGroups * kHeadStride;
-                const uint32_t gd = __hip_atomic_fetch_add(groups_done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t gd = __hip_atomic_fetch_add(groups_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (gd == kGroups - 1) {  // every group has reset: the slot is free for another launch
                     __hip_atomic_store(groups_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(done, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(done, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
             }
         }

@@ -13,6 +13,8 @@
 #                          cut to the timed dispatches by tools/prof_timed.py ($TAG_pmc_CFG.json)
 #   py:SCRIPT[+ARG...]     python SCRIPT ARG... (a tools/ probe)
 #   bin:PROGRAM[+ARG...]   a probe program built here beforehand (tools/dev/*.hip)
+#   lib:PATH | lib:default the library later steps load (SCCSUM_LIB: an A/B build of the same ABI);
+#                          their bench logs are named after it
 # Outputs go to gpurun_out/TAG/; steps.log records each step's outcome.
 set -o pipefail
 TAG=${1:?usage: gpu_session.sh TAG STEP...}
@@ -23,6 +25,7 @@ mkdir -p "$O"
 cd "$R" || exit 1
 export TMPDIR=/tmp
 PROF_STEPS="--steps 10 --warmup 2 --no-cpu"
+LIBTAG=
 
 split() {  # split CFG+A+B -> CFG and args array ARGS
     local IFS='+'
@@ -50,7 +53,15 @@ run_step() {
         bench)
             split "$rest"
             timeout -k 10 400 python bench.py --config "$CFG" --steps 20 --no-cpu "${ARGS[@]}" \
-                >> "$O/bench_$n.log" 2>&1 ;;
+                >> "$O/bench_$n$LIBTAG.log" 2>&1 ;;
+        lib)
+            if [ "$rest" = default ]; then
+                unset SCCSUM_LIB
+                LIBTAG=
+            else
+                export SCCSUM_LIB=$R/$rest
+                LIBTAG=_$(basename "$rest" .so)
+            fi ;;
         trace)
             split "$rest"
             (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/trace_$n" -o run \
