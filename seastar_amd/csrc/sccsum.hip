@@ -412,12 +412,19 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
         uint32_t hv = 0;
         const int sh = static_cast<int>(addr & 3u);
         if (IPV4 && (r < 5 || (r == 5 && sh != 0))) hv = *reinterpret_cast<const uint32_t*>(ptr - sh + 4 * r);
-        u32x4 v[V];
+        // lane r's units are r, r + 16, ...: one base address per lane and
+        // immediate offsets of 256 u, with the bounds as one per-lane limit
+        // (no per-unit address or threshold registers: 94 -> 64 VGPRs at V = 6)
+        const uint8_t* lb = a0 + 16u * r;
+        auto load_group = [&](uint32_t g, u32x4 (&v)[V]) {
+            const int lim = static_cast<int>(nunits) - static_cast<int>(g + r);  // units of this lane left
 #pragma unroll
-        for (int u = 0; u < V; ++u) {
-            const uint32_t c = static_cast<uint32_t>(u) * kRow + r;
-            v[u] = c < nunits ? load_unit(a0 + 16u * c) : u32x4{0, 0, 0, 0};
-        }
+            for (int u = 0; u < V; ++u) {
+                v[u] = u * static_cast<int>(kRow) < lim ? load_unit(lb + 16u * g + 256u * u) : u32x4{0, 0, 0, 0};
+            }
+        };
+        u32x4 v[V];
+        load_group(0, v);
         int rs = head, re = head + static_cast<int>(L);
         uint32_t ipc = 0, pseudo = 0;
         uint8_t st = 0;
@@ -442,29 +449,25 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
         // lane instead of V (profiles/r03_ab_rows.log).
         uint64_t acc = 0;
         auto group = [&](uint32_t g) {
+            const int rel = re - 16 * static_cast<int>(g + r);  // re relative to this lane's unit u = 0
             uint32_t sum = 0;
             u32x4 tv = u32x4{0, 0, 0, 0};
-            int tc16 = 0;
+            int tlo = 0;
 #pragma unroll
             for (int u = 0; u < V; ++u) {
-                const int c16 = 16 * static_cast<int>(g + static_cast<uint32_t>(u) * kRow + r);
-                const uint32_t full = sad4(v[u], 0u);
-                sum += c16 < re ? full : 0u;
-                const bool tail = c16 < re && c16 + 16 > re;
+                const int lo = rel - 256 * u;  // re relative to unit u: the unit is kept whole if lo >= 16
+                sum += lo > 0 ? sad4(v[u], 0u) : 0u;
+                const bool tail = lo > 0 && lo < 16;
                 tv = tail ? v[u] : tv;
-                tc16 = tail ? c16 : tc16;
+                tlo = tail ? lo : tlo;
             }
-            sum -= unit_part(tv, re - tc16, 16);
+            sum -= unit_part(tv, tlo, 16);
             if (g == 0) sum -= unit_part(v[0], 0, rs - 16 * static_cast<int>(r));
             acc += sum;
         };
         group(0);
         for (uint32_t g = V * kRow; g < nunits; g += V * kRow) {
-#pragma unroll
-            for (int u = 0; u < V; ++u) {
-                const uint32_t c = g + static_cast<uint32_t>(u) * kRow + r;
-                v[u] = c < nunits ? load_unit(a0 + 16u * c) : u32x4{0, 0, 0, 0};
-            }
+            load_group(g, v);
             group(g);
         }
         uint32_t S = fold16(row_sum(fold16(acc)));
