@@ -58,10 +58,7 @@ def flat_kernel(ipv4: bool, fill: bool, n: int, nbytes: int) -> str:
 
 def sparse_kernel(args, ipv4: bool, max_len: int) -> str:
     """The kernel a sparse layout gets (sccsum.hip pick_variant / launch_rows),
-    as rocprofv3 names it: the row kernel (V units per lane from max_len), or
-    the row-pair form with --variant 3."""
-    if args.variant == 3:
-        return f"csum_wrow_kernel<4, {str(ipv4).lower()}>"
+    as rocprofv3 names it: the row kernel, V units per lane from max_len."""
     units = (max_len + 30) // 16
     v = 2 if units <= 32 else 4 if units <= 64 else 6 if units <= 96 else 8
     return f"csum_row_kernel<{v}, {str(ipv4).lower()}>"

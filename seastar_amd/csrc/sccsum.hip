@@ -352,143 +352,6 @@ __device__ __forceinline__ uint32_t row_sum(uint32_t v) {
     return v;
 }
 
-// Lane k of each 16-lane row, broadcast to the whole row (DPP row_newbcast).
-template <int K>
-__device__ __forceinline__ uint32_t row_bcast(uint32_t v) {
-    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x150 + K, 0xF, 0xF, false));
-}
-
-// One packet per 16-lane ROW (four packets per wave at a time): for sparse
-// layouts, where every packet is its own run (DPDK mbuf slots a NIC wrote
-// into HBM: 1500 B of every 2304).  Each lane loads V 16-byte units, so one
-// load instruction covers four packets and a wave keeps four packets' round
-// trips in flight together; the row's sum is four DPP steps.  Same arithmetic
-// and outputs as csum_kernel (frame mode: the IPv4 header from the row's first
-// dwords, broadcast with row_newbcast; L4 range and pseudo-header as
-// frame_header).  Packets longer than 16 V units loop over groups.
-template <int V, bool IPV4>
-__global__ __launch_bounds__(kBlock) void csum_row_kernel(
-    const uint8_t* __restrict__ bytes, uint64_t bytes_len,
-    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
-    const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
-    uint8_t* __restrict__ status, uint64_t n, uint32_t flags) {
-    constexpr uint32_t kRow = 16;
-    constexpr uint32_t kRowsPerBlock = kBlock / kRow;
-    constexpr uint32_t kChunk = 4 * kRowsPerBlock;  // packets a block takes at a time
-    const bool raw = !IPV4 && (flags & kFlagRaw);
-    const uint32_t r = threadIdx.x & (kRow - 1);
-    const uint32_t row = threadIdx.x / kRow;
-    // A block takes 64 consecutive packets at a time (4 steps of 16 rows), so
-    // the 64 status bytes (and 256 B of results) of a chunk are written by one
-    // block, into one XCD's L2, and leave as whole lines; a plain grid stride
-    // spread each line over four blocks on different XCDs (partial writes).
-    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
-    for (uint64_t ch = xcd_block_id(); ch < nchunks; ch += gridDim.x)
-    for (uint32_t step = 0; step < kChunk / kRowsPerBlock; ++step) {
-        const uint64_t p = ch * kChunk + step * kRowsPerBlock + row;
-        if (p >= n) break;
-        const uint64_t o = off[p];
-        const uint32_t L = len[p];
-        if (o > bytes_len || L > bytes_len - o || (IPV4 && L < 20)) {
-            if (r == 0) {
-                if (IPV4) {
-                    if (out) reinterpret_cast<uint32_t*>(out)[p] = 0;
-                } else {
-                    out[p] = 0;
-                }
-                if (status) {
-                    status[p] = (o > bytes_len || L > bytes_len - o) ? SCCSUM_ST_RANGE : SCCSUM_ST_MALFORMED;
-                }
-            }
-            continue;
-        }
-        const uint8_t* ptr = bytes + o;
-        const uintptr_t addr = reinterpret_cast<uintptr_t>(ptr);
-        const int head = static_cast<int>(addr & 15u);
-        const uint8_t* a0 = ptr - head;
-        const uint32_t nunits = L ? (static_cast<uint32_t>(head) + L + 15u) >> 4 : 0u;
-        // frame mode: header dwords re-aligned to the packet start (row lanes
-        // 0..5 load the covering dwords, as span_packet)
-        uint32_t hv = 0;
-        const int sh = static_cast<int>(addr & 3u);
-        if (IPV4 && (r < 5 || (r == 5 && sh != 0))) hv = *reinterpret_cast<const uint32_t*>(ptr - sh + 4 * r);
-        // lane r's units are r, r + 16, ...: one base address per lane and
-        // immediate offsets of 256 u, with the bounds as one per-lane limit
-        // (no per-unit address or threshold registers: 94 -> 64 VGPRs at V = 6)
-        const uint8_t* lb = a0 + 16u * r;
-        auto load_group = [&](uint32_t g, u32x4 (&v)[V]) {
-            const int lim = static_cast<int>(nunits) - static_cast<int>(g + r);  // units of this lane left
-#pragma unroll
-            for (int u = 0; u < V; ++u) {
-                v[u] = u * static_cast<int>(kRow) < lim ? load_unit(lb + 16u * g + 256u * u) : u32x4{0, 0, 0, 0};
-            }
-        };
-        u32x4 v[V];
-        load_group(0, v);
-        int rs = head, re = head + static_cast<int>(L);
-        uint32_t ipc = 0, pseudo = 0;
-        uint8_t st = 0;
-        if (IPV4) {
-            const uint32_t nxt = static_cast<uint32_t>(
-                __builtin_amdgcn_update_dpp(0, static_cast<int>(hv), 0x101, 0xF, 0xF, false));  // row_shl:1
-            const uint32_t al = __builtin_amdgcn_alignbyte(nxt, hv, static_cast<uint32_t>(sh));
-            const FrameHeader F = frame_header(row_bcast<0>(al), row_bcast<1>(al), row_bcast<2>(al),
-                                               row_bcast<3>(al), row_bcast<4>(al), L);
-            ipc = F.ipc;
-            st = F.st;
-            pseudo = F.pseudo;
-            rs = head + static_cast<int>(F.l4_off);
-            re = rs + static_cast<int>(F.l4_len);
-        }
-        // Whole units summed with v_sad_u16 (one instruction per dword, exact in
-        // 32 bits per group), then the bytes outside [rs, re) taken off once:
-        // units wholly past re are dropped, the head part [0, rs) comes from
-        // the first row of units (the IPv4 header and options end within unit
-        // 4), and the tail part from the one unit per packet holding re - 1 —
-        // selected first, then masked once, so the byte masks cost one unit per
-        // lane instead of V (profiles/r03_ab_rows.log).
-        uint64_t acc = 0;
-        auto group = [&](uint32_t g) {
-            const int rel = re - 16 * static_cast<int>(g + r);  // re relative to this lane's unit u = 0
-            uint32_t sum = 0;
-            u32x4 tv = u32x4{0, 0, 0, 0};
-            int tlo = 0;
-#pragma unroll
-            for (int u = 0; u < V; ++u) {
-                const int lo = rel - 256 * u;  // re relative to unit u: the unit is kept whole if lo >= 16
-                sum += lo > 0 ? sad4(v[u], 0u) : 0u;
-                const bool tail = lo > 0 && lo < 16;
-                tv = tail ? v[u] : tv;
-                tlo = tail ? lo : tlo;
-            }
-            sum -= unit_part(tv, tlo, 16);
-            if (g == 0) sum -= unit_part(v[0], 0, rs - 16 * static_cast<int>(r));
-            acc += sum;
-        };
-        group(0);
-        for (uint32_t g = V * kRow; g < nunits; g += V * kRow) {
-            load_group(g, v);
-            group(g);
-        }
-        uint32_t S = fold16(row_sum(fold16(acc)));
-        if (addr & 1u) S = swap16(S);
-        if (IPV4) {
-            S = fold16(static_cast<uint64_t>(S) + pseudo);
-        } else if (seed && !raw) {
-            S = fold16(static_cast<uint64_t>(S) + swap16(fold16(seed[p])));
-        }
-        const uint32_t res = raw ? S : ~S & 0xffffu;
-        if (r == 0) {
-            if (IPV4) {
-                if (out) reinterpret_cast<uint32_t*>(out)[p] = frame_word(ipc, res, st);
-                if (status) status[p] = static_cast<uint8_t>(frame_status(ipc, res, st));
-            } else {
-                out[p] = static_cast<uint16_t>(res);
-                if (status) status[p] = (!raw && res == 0) ? SCCSUM_ST_OK : 0u;
-            }
-        }
-    }
-}
 
 // ---------------------------------------------------------------- flat-kernel helpers
 
@@ -705,130 +568,183 @@ __device__ __forceinline__ void tile_store(T* t, uint32_t lane, T v, uint32_t po
     }
 }
 
-// One packet per 64-lane ROW PAIR, K packets per round trip (variant 3, a
-// sparse-layout form): packet k's units 0..63 and 64..127 are two rows whose
-// base address is wave-uniform, so each load instruction reads 1 KiB of one
-// packet (the row kernel's read 4 x 256 B of four packets), and a wave keeps
-// K packets' bytes in flight together.  Longer packets continue with further
-// row pairs, one packet at a time.  Per-lane byte masks select the summed
-// range (frame mode: [4*ihl, min(ip_len, len)), from the header in the first
-// row's lanes 0..3), as csum_kernel does, so no packet needs a slow path.
-// A block takes 64 consecutive packets at a time (as csum_row_kernel: the
-// chunk's results leave one block, as whole lines).
-template <int K, bool IPV4>
-__global__ __launch_bounds__(kBlock) void csum_wrow_kernel(
+// Sparse layouts (variant 2): a wave owns TILES of 64 consecutive packets, as
+// the flat kernel does, but loads them ROW by row — one packet per 16-lane
+// row, four packets per load instruction, V 16-byte units per lane — because
+// in a sparse layout (DPDK mbuf slots a NIC wrote into HBM: 1500 B of every
+// 2304) every packet is its own run and the flat kernel's wave would wait
+// out one memory round trip per packet.  The rows do only what the bytes
+// need: load, v_sad_u16 the whole units, a row sum (DPP), and hand the
+// packet's lane its sum plus the units its finish needs (the first three,
+// the last) through LDS.  Everything per packet — IPv4 header, the edge
+// bytes outside the summed range, pseudo-header, fold, result — then runs
+// lane-parallel once per tile for all 64 packets (the flat kernel's phase C),
+// instead of once per row step for four: round 2's row kernel spent ~350
+// vector instructions per four packets on it and ran at 74 % where its own
+// loads alone reach 81 % (profiles/r03_sparse_probe.log).  Frames the fast
+// path cannot take (IP options, a trimmed IP length, over 128 KiB) are redone
+// exactly, one wave each (the flat kernel's phase D); results leave as one
+// coalesced store per tile.
+template <int V, bool IPV4>
+__global__ __launch_bounds__(kBlock) void csum_row_kernel(
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
     const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
     uint8_t* __restrict__ status, uint64_t n, uint32_t flags) {
-    constexpr uint32_t kChunk = 64;
-    constexpr uint32_t kPerWave = kChunk / kWavesPerBlock;  // 16 packets of the chunk per wave
-    static_assert(kPerWave % K == 0, "a wave's share is whole groups of K");
+    constexpr uint32_t kRow = 16;
     const bool raw = !IPV4 && (flags & kFlagRaw);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
-    auto rl = [](uint32_t v, uint32_t k) {
-        return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(k)));
-    };
-    for (uint64_t ch = xcd_block_id(); ch < nchunks; ch += gridDim.x) {
-        for (uint32_t grp = 0; grp < kPerWave / K; ++grp) {
-            const uint64_t p0 = ch * kChunk + wv * kPerWave + grp * K;
-            if (p0 >= n) break;
-            // lanes 0..K-1: the group's metadata, one round trip
-            uint64_t mo = 0;
-            uint32_t mL = 0, msd = 0;
-            if (lane < K && p0 + lane < n) {
-                mo = off[p0 + lane];
-                mL = len[p0 + lane];
-                if (!IPV4 && seed) msd = seed[p0 + lane];
-            }
-            uint64_t a0[K];
-            uint32_t L[K], head[K], nun[K], stbad[K];
-            bool bad[K];
-            u32x4 v[2 * K];
+    const uint32_t r = lane & (kRow - 1), j = lane / kRow;  // lane r of row j
+    // per packet of the tile: units 0, 1, 2 and its last unit, for its finish
+    __shared__ u32x4 picks_all[kWavesPerBlock][kWave][4];
+    u32x4(*picks)[4] = picks_all[wv];
+    const uint64_t ntiles = (n + kWave - 1) / kWave;
+    const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+    for (uint64_t t = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv; t < ntiles; t += nwaves) {
+        // ---- A: lane k plans packet k of the tile (coalesced metadata loads)
+        const uint64_t p = t * kWave + lane;
+        const uint32_t cnt = static_cast<uint32_t>(n - t * kWave < kWave ? n - t * kWave : kWave);
+        const bool mine = lane < cnt;
+        const uint64_t o = mine ? off[p] : 0;
+        const uint32_t L = mine ? len[p] : 0u;
+        const uint32_t sd = (!IPV4 && seed && mine) ? seed[p] : 0u;
+        const bool range_bad = mine && (o > bytes_len || L > bytes_len - o);
+        const bool short_frame = IPV4 && mine && !range_bad && L < 20;
+        const bool huge = mine && !range_bad && L > kExactMax;
+        const bool fast = mine && !range_bad && !short_frame && !huge;
+        const uint64_t ptr = reinterpret_cast<uint64_t>(bytes) + (range_bad ? 0 : o);
+        const uint32_t head = static_cast<uint32_t>(ptr & 15u);
+        const uint64_t a0 = ptr - head;
+        const uint32_t nunits = (fast && L) ? (head + L + 15u) >> 4 : 0u;
+
+        // ---- B: rows load and sum; packet k's sum and picks go to lane k
+        uint32_t res = 0;
+        for (uint32_t s = 0; s * 4u < cnt; ++s) {
+            const uint32_t k = 4u * s + j;  // this row's packet
+            const uint32_t klo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(a0)), k));
+            const uint32_t khi = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(a0 >> 32)), k));
+            const uint32_t knu = static_cast<uint32_t>(__shfl(static_cast<int>(nunits), k));
+            const uint8_t* lb = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(khi) << 32) | klo) + 16u * r;
+            uint32_t sum = 0;
+            for (uint32_t g = 0; g < knu; g += V * kRow) {
+                const int lim = static_cast<int>(knu) - static_cast<int>(g + r);  // this lane's units left
+                u32x4 v[V];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const uint64_t o = (static_cast<uint64_t>(rl(static_cast<uint32_t>(mo >> 32), k)) << 32) |
-                                   rl(static_cast<uint32_t>(mo), k);
-                L[k] = rl(mL, k);
-                const bool in = p0 + k < n;
-                const bool rbad = in && (o > bytes_len || L[k] > bytes_len - o);
-                bad[k] = !in || rbad || (IPV4 && L[k] < 20);
-                stbad[k] = rbad ? SCCSUM_ST_RANGE : SCCSUM_ST_MALFORMED;
-                const uint64_t ptr = reinterpret_cast<uint64_t>(bytes) + (bad[k] ? 0 : o);
-                head[k] = static_cast<uint32_t>(ptr & 15u);
-                a0[k] = ptr - head[k];
-                nun[k] = (!bad[k] && L[k]) ? (head[k] + L[k] + 15u) >> 4 : 0u;
-                const u32x4* a = reinterpret_cast<const u32x4*>(a0[k]);
-                v[2 * k] = lane < nun[k] ? load_unit(reinterpret_cast<const uint8_t*>(a + lane)) : u32x4{0, 0, 0, 0};
-                v[2 * k + 1] =
-                    64u + lane < nun[k] ? load_unit(reinterpret_cast<const uint8_t*>(a + 64 + lane)) : u32x4{0, 0, 0, 0};
-            }
-            uint32_t word_mine = 0, st_mine = 0;
+                for (int u = 0; u < V; ++u) {
+                    v[u] = u * static_cast<int>(kRow) < lim ? load_unit(lb + 16u * g + 256u * u) : u32x4{0, 0, 0, 0};
+                }
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                int rs = static_cast<int>(head[k]), re = static_cast<int>(head[k] + L[k]);
-                uint32_t ipc = 0, pseudo = 0, st = 0;
-                if (IPV4 && !bad[k]) {
-                    const u32x4 hu[4] = {
-                        u32x4{rl(v[2 * k].x, 0), rl(v[2 * k].y, 0), rl(v[2 * k].z, 0), rl(v[2 * k].w, 0)},
-                        u32x4{rl(v[2 * k].x, 1), rl(v[2 * k].y, 1), rl(v[2 * k].z, 1), rl(v[2 * k].w, 1)},
-                        u32x4{rl(v[2 * k].x, 2), rl(v[2 * k].y, 2), rl(v[2 * k].z, 2), rl(v[2 * k].w, 2)},
-                        u32x4{0, 0, 0, 0}};
-                    const FrameHeader F = frame_header(header_dword(hu, head[k], 0), header_dword(hu, head[k], 1),
-                                                       header_dword(hu, head[k], 2), header_dword(hu, head[k], 3),
-                                                       header_dword(hu, head[k], 4), L[k]);
-                    ipc = F.ipc;
-                    pseudo = F.pseudo;
-                    st = F.st;
-                    rs = static_cast<int>(head[k] + F.l4_off);
-                    re = rs + static_cast<int>(F.l4_len);
-                }
-                uint64_t acc = unit_sum(v[2 * k], rs - static_cast<int>(16 * lane), re - static_cast<int>(16 * lane)) +
-                               unit_sum(v[2 * k + 1], rs - static_cast<int>(16 * (64 + lane)),
-                                        re - static_cast<int>(16 * (64 + lane)));
-                // the rest of a packet longer than 128 units, two rows at a time
-                for (uint32_t g = 128; g < nun[k]; g += 128) {
-                    const u32x4* a = reinterpret_cast<const u32x4*>(a0[k]) + g;
-                    const u32x4 w0 = g + lane < nun[k] ? load_unit(reinterpret_cast<const uint8_t*>(a + lane))
-                                                       : u32x4{0, 0, 0, 0};
-                    const u32x4 w1 = g + 64u + lane < nun[k]
-                                         ? load_unit(reinterpret_cast<const uint8_t*>(a + 64 + lane))
-                                         : u32x4{0, 0, 0, 0};
-                    const int c0 = static_cast<int>(16 * (g + lane)), c1 = static_cast<int>(16 * (g + 64 + lane));
-                    acc += unit_sum(w0, rs - c0, re - c0) + unit_sum(w1, rs - c1, re - c1);
-                }
-                uint32_t S = fold16(wave_sum(fold16(acc)));
-                if (head[k] & 1u) S = swap16(S);
-                uint32_t word, stw;
+                for (int u = 0; u < V; ++u) sum = sad4(v[u], sum);
+                if (g == 0 && r < 3) picks[k][r] = v[0];  // units 0..2 (zero past the packet)
+                // the lane holding the last unit (its unit u has lim - 1 == 16 u): select, then one store
+                u32x4 lastv = v[0];
+#pragma unroll
+                for (int u = 1; u < V; ++u) lastv = lim - 1 == 16 * u ? v[u] : lastv;
+                if (lim >= 1 && lim <= 16 * V && ((lim - 1) & 15) == 0) picks[k][3] = lastv;
+            }
+            // row sums (exact: < 2^32 up to kExactMax bytes), one per row, to the packets' lanes
+            const uint32_t rsum = row_sum(sum);
+#pragma unroll
+            for (uint32_t jj = 0; jj < 4; ++jj) {
+                const uint32_t sj = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rsum), 16 * jj));
+                res = lane == 4u * s + jj ? sj : res;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // the rows' LDS picks precede the lanes' reads
+
+        // ---- C: lane k finishes packet k
+        u32x4 hs[4] = {picks[lane][0], picks[lane][1], picks[lane][2], u32x4{0, 0, 0, 0}};
+        const u32x4 hl = picks[lane][3];
+        __builtin_amdgcn_wave_barrier();  // this tile's reads precede the next tile's writes
+        const int rs0 = static_cast<int>(head) + (IPV4 ? 20 : 0);
+        const int re0 = static_cast<int>(head + L);
+        const int lastu16 = 16 * (static_cast<int>(nunits) - 1);
+        uint32_t excl = unit_part(hs[0], 0, rs0);
+        if (IPV4) excl += unit_part(hs[1], 0, rs0 - 16) + unit_part(hs[2], 0, rs0 - 32);
+        excl += unit_part(hl, re0 - lastu16, 16);
+        const uint32_t kept = nunits ? res - excl : 0u;
+        uint32_t S = fold16(kept);
+        if (head & 1u) S = swap16(S);
+        uint32_t word = 0, st = 0, ipc = 0, pseudo = 0;
+        bool slow = huge;  // (not streamed: phase D decodes its header from the frame)
+        if (IPV4) {
+            const uint32_t h0 = header_dword(hs, head, 0), h1 = header_dword(hs, head, 1);
+            const uint32_t h2 = header_dword(hs, head, 2), h3 = header_dword(hs, head, 3);
+            const uint32_t h4 = header_dword(hs, head, 4);
+            const FrameDecode D = frame_decode(h0, h1, h2, h3, h4, L);
+            ipc = ~fold16(static_cast<uint64_t>(h0) + h1 + h2 + h3 + h4) & 0xffffu;
+            st = D.st;
+            pseudo = D.pseudo;
+            // options or a trimmed IP length: the exact redo (a fragment claims no L4 value)
+            if (fast && (D.ihl != 5u || D.ip_len != L) && (st & SCCSUM_ST_IPFRAG) == 0u) slow = true;
+            const uint32_t rr = ~fold16(static_cast<uint64_t>(S) + pseudo) & 0xffffu;
+            word = frame_word(ipc, rr, st);
+            st = frame_status(ipc, rr, st);
+        } else {
+            const uint32_t rr = raw ? S : ~fold16(static_cast<uint64_t>(S) + swap16(fold16(sd))) & 0xffffu;
+            word = rr;
+            st = (!raw && rr == 0) ? SCCSUM_ST_OK : 0u;
+        }
+        if (range_bad) {
+            word = 0;
+            st = SCCSUM_ST_RANGE;
+        } else if (short_frame) {
+            word = 0;
+            st = SCCSUM_ST_MALFORMED;
+        }
+
+        // ---- D: exact redo of the packets the fast path could not take (frame
+        // header from the packet itself when it was not streamed: over 128 KiB)
+        uint64_t todo = __ballot(slow);
+        while (todo) {
+            const uint32_t jl = static_cast<uint32_t>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            const uint32_t jlo = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0), jl);
+            const uint32_t jhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(a0 >> 32), jl);
+            const uint8_t* ja0 = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(jhi) << 32) | jlo);
+            const uint32_t jhead = __builtin_amdgcn_readlane(head, jl);
+            const uint32_t jL = __builtin_amdgcn_readlane(L, jl);
+            uint64_t rs = jhead, re = static_cast<uint64_t>(jhead) + jL;
+            uint32_t jipc = 0, jpseudo = 0, jst = 0;
+            if (IPV4) {
+                // over 128 KiB the header was not picked up: decode it from the frame (wave-uniform)
+                const uint32_t* hp = reinterpret_cast<const uint32_t*>(ja0 + jhead - (jhead & 3u));
+                const uint32_t sh = jhead & 3u;
+                uint32_t hd[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) hd[i] = hp[i];
+                uint32_t h[5];
+#pragma unroll
+                for (int i = 0; i < 5; ++i) h[i] = __builtin_amdgcn_alignbyte(hd[i + 1], hd[i], sh);
+                const FrameDecode D = frame_decode(h[0], h[1], h[2], h[3], h[4], jL);
+                jipc = ~fold16(static_cast<uint64_t>(h[0]) + h[1] + h[2] + h[3] + h[4]) & 0xffffu;
+                jpseudo = D.pseudo;
+                jst = D.st;
+                rs = jhead + D.l4_off;
+                re = rs + D.l4_len;
+            }
+            uint32_t SJ = exact_range_sum(ja0, rs, re, lane);
+            if (jhead & 1u) SJ = swap16(SJ);
+            if (lane == jl) {
                 if (IPV4) {
-                    const uint32_t r = ~fold16(static_cast<uint64_t>(S) + pseudo) & 0xffffu;
-                    word = frame_word(ipc, r, st);
-                    stw = frame_status(ipc, r, st);
+                    const uint32_t rr = ~fold16(static_cast<uint64_t>(SJ) + jpseudo) & 0xffffu;
+                    word = frame_word(jipc, rr, jst);
+                    st = frame_status(jipc, rr, jst);
                 } else {
-                    const uint32_t sd = rl(msd, k);
-                    const uint32_t r = raw ? S : ~fold16(static_cast<uint64_t>(S) + swap16(fold16(sd))) & 0xffffu;
-                    word = r;
-                    stw = (!raw && r == 0) ? SCCSUM_ST_OK : 0u;
-                }
-                if (bad[k]) {
-                    word = 0;
-                    stw = stbad[k];
-                }
-                if (lane == static_cast<uint32_t>(k)) {
-                    word_mine = word;
-                    st_mine = stw;
+                    const uint32_t rr = raw ? SJ : ~fold16(static_cast<uint64_t>(SJ) + swap16(fold16(sd))) & 0xffffu;
+                    word = rr;
+                    st = (!raw && rr == 0) ? SCCSUM_ST_OK : 0u;
                 }
             }
-            if (lane < K && p0 + lane < n) {
-                if (IPV4) {
-                    if (out) reinterpret_cast<uint32_t*>(out)[p0 + lane] = word_mine;
-                } else {
-                    out[p0 + lane] = static_cast<uint16_t>(word_mine);
-                }
-                if (status) status[p0 + lane] = static_cast<uint8_t>(st_mine);
+        }
+        if (mine) {
+            if (IPV4) {
+                if (out) reinterpret_cast<uint32_t*>(out)[p] = word;
+            } else {
+                out[p] = static_cast<uint16_t>(word);
             }
+            if (status) status[p] = static_cast<uint8_t>(st);
         }
     }
 }
@@ -960,7 +876,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
                 // which are performed at the device's coherence point; waiting
                 // for each to complete (s_waitcnt) orders reset -> count ->
                 // report without the L2 write-backs a release fence costs
-                // (profiles/r03_ab_pool.log).
+                // (profiles/r03_ab_pool_rows.log).
                 __hip_atomic_store(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 uint32_t* const groups_done = heads + kGroups * kHeadStride;
@@ -1761,20 +1677,6 @@ void launch_simple(int uc, hipStream_t s, const uint8_t* b, uint64_t bytes_len, 
 }
 
 template <bool IPV4>
-void launch_wrows(hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
-                  const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n, uint32_t flags) {
-    auto kern = csum_wrow_kernel<4, IPV4>;
-    const int occ = kernel_occupancy(reinterpret_cast<const void*>(kern));
-    const uint64_t bpc = static_cast<uint64_t>(occ < t_knobs.blocks_per_cu ? occ : t_knobs.blocks_per_cu);
-    const uint64_t cap = static_cast<uint64_t>(cu_count()) * bpc;
-    uint64_t blocks = (n + 63u) / 64u;  // a block takes 64-packet chunks
-    blocks = blocks < cap ? blocks : cap;
-    blocks = (blocks + 7u) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
-    kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out,
-                                                                     d_status, n, flags);
-}
-
-template <bool IPV4>
 void launch_rows(uint32_t max_len, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
                  const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
                  uint32_t flags) {
@@ -1785,7 +1687,7 @@ void launch_rows(uint32_t max_len, hipStream_t s, const uint8_t* b, uint64_t byt
         const int occ = kernel_occupancy(reinterpret_cast<const void*>(kern));
         const uint64_t bpc = static_cast<uint64_t>(occ < t_knobs.blocks_per_cu ? occ : t_knobs.blocks_per_cu);
         const uint64_t cap = static_cast<uint64_t>(cu_count()) * bpc;
-        uint64_t blocks = (n + 63u) / 64u;  // a block takes 64-packet chunks
+        uint64_t blocks = ((n + 63u) / 64u + kWavesPerBlock - 1) / kWavesPerBlock;  // a wave takes 64-packet tiles
         blocks = blocks < cap ? blocks : cap;
         blocks = (blocks + 7u) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
         kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out,
@@ -1868,7 +1770,7 @@ int pick_variant(uint64_t n_total, uint64_t bytes_total, uint32_t flags, uint32_
     const bool fill = (flags & kFillFlags) != 0;
     const bool sparse = max_len != 0 && n_total != 0 && bytes_total / n_total >= uint64_t(max_len) + 64u;
     if (variant == 0 && sparse && !fill) return 2;
-    if (variant == 0 || ((variant == 1 || variant == 2 || variant == 3) && fill)) variant = dflt;  // in place: flat only
+    if (variant == 0 || ((variant == 1 || variant == 2) && fill)) variant = dflt;  // in-place write-back: flat only
     return variant;
 }
 
@@ -1881,12 +1783,10 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
     const int variant = pick_variant(n, bytes_len, flags, max_len);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
-    if (variant == 1 || variant == 2 || variant == 3) {
+    if (variant == 1 || variant == 2) {
         if (variant == 1) {
             launch_simple<IPV4>(units_class(max_len), s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n,
                                 flags);
-        } else if (variant == 3) {
-            launch_wrows<IPV4>(s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
         } else {
             launch_rows<IPV4>(max_len, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
         }
@@ -1927,16 +1827,13 @@ int launch_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
     if (n_total == 0) return SCCSUM_OK;
     const int variant = pick_variant(n_total, bytes_total, 0, max_len);
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    if (variant == 1 || variant == 2 || variant == 3) {  // the per-packet kernels take one batch per launch
+    if (variant == 1 || variant == 2) {  // the per-packet kernels take one batch per launch
         for (uint32_t i = 0; i < nbatch; ++i) {
             const sccsum_batch& x = batches[i];
             if (!x.n) continue;
             if (variant == 1) {
                 launch_simple<IPV4>(units_class(max_len), s, static_cast<const uint8_t*>(x.d_bytes), x.bytes_len,
                                     x.d_off, x.d_len, x.d_seed, static_cast<uint16_t*>(x.d_out), x.d_status, x.n, 0);
-            } else if (variant == 3) {
-                launch_wrows<IPV4>(s, static_cast<const uint8_t*>(x.d_bytes), x.bytes_len, x.d_off, x.d_len,
-                                   x.d_seed, static_cast<uint16_t*>(x.d_out), x.d_status, x.n, 0);
             } else {
                 launch_rows<IPV4>(max_len, s, static_cast<const uint8_t*>(x.d_bytes), x.bytes_len, x.d_off, x.d_len,
                                   x.d_seed, static_cast<uint16_t*>(x.d_out), x.d_status, x.n, 0);
@@ -2381,9 +2278,7 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
 }
 
 int sccsum_set_kernel_variant(int variant) {
-    if (!(variant == 0 || variant == 1 || variant == 2 || variant == 3 || (variant >= 14 && variant <= 16))) {
-        return SCCSUM_EINVAL;
-    }
+    if (!(variant == 0 || variant == 1 || variant == 2 || (variant >= 14 && variant <= 16))) return SCCSUM_EINVAL;
     sccsum::t_knobs.variant = variant;
     return SCCSUM_OK;
 }

@@ -11,6 +11,8 @@
 //   wave     one packet per wave, 2 units per lane
 //   half     one packet per 32-lane half wave, 3 units per lane
 //   wrows<K> a wave takes K packets per round trip, two 64-lane rows each
+//   rows_m<M>[h] rows with the offsets and lengths loaded from arrays (per step, or 4 steps at once) and
+//            with the header dword loads
 //   virt<U>  a wave streams a tile of T packets as ONE virtual extent of units
 //            (packet k's 94 units follow packet k-1's): U units per lane per
 //            round trip, each lane's address from its virtual unit
@@ -80,6 +82,60 @@ __global__ __launch_bounds__(256) void k_rows(const uint8_t* __restrict__ buf, u
                 for (int u = 0; u < V; ++u) cur[u] = nxt[u];
             }
             p = q;
+        }
+    }
+}
+
+// rows with the product's metadata: each step's packet offset and length
+// loaded from arrays (M = 1: per step, a dependent round trip before the
+// data; M = 4: the chunk's four steps loaded at the chunk's start); HDR: the
+// row's lanes 0..5 also load the packet's first 24 bytes as dwords (the row
+// kernel's IPv4 header loads)
+template <int V, int M, bool HDR>
+__global__ __launch_bounds__(256) void k_rows_meta(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+                                                   const uint32_t* __restrict__ len, uint64_t n,
+                                                   uint8_t* __restrict__ st) {
+    const uint32_t r = threadIdx.x & 15, row = threadIdx.x >> 4;
+    const uint64_t nch = (n + 63) / 64;
+    for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+        uint64_t mo[4];
+        uint32_t ml[4];
+        if (M == 4) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t p = ch * 64 + k * 16 + row;
+                mo[k] = p < n ? off[p] : 0;
+                ml[k] = p < n ? len[p] : 0;
+            }
+        }
+#pragma unroll 1
+        for (int step = 0; step < 4; ++step) {
+            const uint64_t p = ch * 64 + step * 16 + row;
+            if (p >= n) break;
+            uint64_t o;
+            uint32_t L;
+            if (M == 4) {
+                o = step == 0 ? mo[0] : step == 1 ? mo[1] : step == 2 ? mo[2] : mo[3];
+                L = step == 0 ? ml[0] : step == 1 ? ml[1] : step == 2 ? ml[2] : ml[3];
+            } else {
+                o = off[p];
+                L = len[p];
+            }
+            const uint32_t nu = (L + 15) / 16;
+            const u32x4* a = reinterpret_cast<const u32x4*>(buf + o);
+            uint32_t hv = 0;
+            if (HDR && r < 6) hv = reinterpret_cast<const uint32_t*>(buf + o)[r];
+            u32x4 v[V];
+#pragma unroll
+            for (int u = 0; u < V; ++u) {
+                const uint32_t c = u * 16 + r;
+                v[u] = c < nu ? __builtin_nontemporal_load(a + c) : u32x4{0, 0, 0, 0};
+            }
+            uint32_t s = hv;
+#pragma unroll
+            for (int u = 0; u < V; ++u) s += s4(v[u]);
+            s += __shfl_xor(s, 1, 16) + __shfl_xor(s, 2, 16) + __shfl_xor(s, 4, 16) + __shfl_xor(s, 8, 16);
+            if (r == 0) st[p] = static_cast<uint8_t>(s);
         }
     }
 }
@@ -196,6 +252,22 @@ int main(int argc, char** argv) {
     run("slab", [&](uint8_t* b) { k_slab<<<g8, 256>>>(reinterpret_cast<const u32x4*>(b), kBytes / 16, st); });
     run("rows", [&](uint8_t* b) { k_rows<6, false><<<g8, 256>>>(b, kN, st); });
     run("rows_pf", [&](uint8_t* b) { k_rows<6, true><<<g8, 256>>>(b, kN, st); });
+    uint64_t* d_off;
+    uint32_t* d_len;
+    {
+        std::vector<uint64_t> ho(kN);
+        std::vector<uint32_t> hl(kN, kLen);
+        for (uint64_t i = 0; i < kN; ++i) ho[i] = i * kSlot + kData;
+        CK(hipMalloc(&d_off, kN * 8));
+        CK(hipMalloc(&d_len, kN * 4));
+        CK(hipMemcpy(d_off, ho.data(), kN * 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_len, hl.data(), kN * 4, hipMemcpyHostToDevice));
+    }
+    run("rows_m1", [&](uint8_t* b) { k_rows_meta<6, 1, false><<<g8, 256>>>(b, d_off, d_len, kN, st); });
+    run("rows_m4", [&](uint8_t* b) { k_rows_meta<6, 4, false><<<g8, 256>>>(b, d_off, d_len, kN, st); });
+    run("rows_m1h", [&](uint8_t* b) { k_rows_meta<6, 1, true><<<g8, 256>>>(b, d_off, d_len, kN, st); });
+    run("rows_m4h", [&](uint8_t* b) { k_rows_meta<6, 4, true><<<g8, 256>>>(b, d_off, d_len, kN, st); });
+    run("rows", [&](uint8_t* b) { k_rows<6, false><<<g8, 256>>>(b, kN, st); });
     run("wave", [&](uint8_t* b) { k_group<64, 2><<<g8, 256>>>(b, kN, st); });
     run("half", [&](uint8_t* b) { k_group<32, 3><<<g8, 256>>>(b, kN, st); });
     run("wrows4", [&](uint8_t* b) { k_wrows<4><<<g8, 256>>>(b, kN, st); });
