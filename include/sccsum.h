@@ -72,8 +72,7 @@ extern "C" {
 
 /* 2 (round 3): frames leave IP fragments' L4 alone (SCCSUM_ST_IPFRAG), L4
  * values of protocols other than TCP / UDP carry no pseudo-header, fill gained
- * SCCSUM_FILL_ICMP_ECHO and needs d_out2 with SCCSUM_FILL_L4 (INTEGRATION.md,
- * "Migration from ABI 1"). */
+ * SCCSUM_FILL_ICMP_ECHO ("Migration from ABI 1"). */
 #define SCCSUM_ABI_VERSION 2
 
 #define SCCSUM_OK 0
@@ -248,12 +247,12 @@ int sccsum_ipv4_frames_rss(const void* d_bytes, uint64_t bytes_len, const uint64
  * first fragment's L4 header, a later fragment's payload — are never written.
  *   mode: SCCSUM_FILL_IP and/or one of SCCSUM_FILL_L4 / SCCSUM_FILL_L4_PSEUDO
  *         (| SCCSUM_FILL_TSO), and/or SCCSUM_FILL_ICMP_ECHO (not with
- *         L4_PSEUDO).  FILL_L4 and FILL_ICMP_ECHO read every byte (the flat
- *         kernel generates into d_out2, then a second pass stores the
- *         fields); the others read only the 20-byte header.
+ *         L4_PSEUDO).  FILL_L4 and FILL_ICMP_ECHO read every byte in one
+ *         launch of the flat kernel, which stores the fields once the
+ *         launch's reads are done; the others read only the 20-byte header.
  *   d_out2[2i] / [2i+1] = the IP / L4 values stored (0 where nothing was
- *         stored); REQUIRED with SCCSUM_FILL_L4 or SCCSUM_FILL_ICMP_ECHO (the
- *         two passes hand the values over in it), else may be NULL.
+ *         stored); may be NULL (ABI 2 as first released in round 3 required
+ *         it with FILL_L4 / FILL_ICMP_ECHO; NULL is accepted again).
  *   d_status[i] = SCCSUM_ST_OK if the IP field was written, SCCSUM_ST_L4_OK
  *         if the L4 field was written, plus MALFORMED / RANGE / IPFRAG; may
  *         be NULL.

@@ -248,21 +248,17 @@ def spans_multi(items, stream=None) -> list:
 
 def ipv4_fill(batch: PacketBatch, mode: int = native.FILL_IP | native.FILL_L4, out2: torch.Tensor | None = None,
               status: torch.Tensor | None = None, stream=None) -> torch.Tensor | None:
-    """sccsum_ipv4_fill: generate checksums and store them in batch.data in place.
+    """sccsum_ipv4_fill: generate checksums and store them in batch.data in place
+    (one launch; out2 / status are optional reports of what was stored).
     Returns the [n, 2] values stored when out2 is given (else None)."""
     lib = native.load()
     n = batch.n
-    given = out2
-    if out2 is None and mode & (native.FILL_L4 | native.FILL_ICMP_ECHO):
-        # the generate and store passes hand the values over in out2 (scratch kept alive for `stream`)
-        out2 = _scratch(4 * max(n, 1), batch.device, stream).view(torch.int16)
     _need(out2, 2 * n, torch.int16, "out2", batch.device)
     _need(status, n, torch.uint8, "status", batch.device)
     code = lib.sccsum_ipv4_fill(
         ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length),
         _ptr(out2), _ptr(status), n, batch.max_len, mode, _stream(stream),
     )
-    out2 = given
     native.check(code, "sccsum_ipv4_fill")
     return None if out2 is None else out2[: 2 * n].view(n, 2)
 

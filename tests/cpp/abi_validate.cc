@@ -72,11 +72,13 @@ static void checks() {
            SCCSUM_EINVAL);
     EXPECT(sccsum_ipv4_fill(nullptr, 64, nullptr, nullptr, nullptr, nullptr, 3, 0, SCCSUM_FILL_IP, nullptr) ==
            SCCSUM_EINVAL);
-    // FILL_L4 / FILL_ICMP_ECHO need d_out2 (the generate pass hands its values to the store pass there)
-    EXPECT(sccsum_ipv4_fill(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr,
-                            nullptr, 3, 0, SCCSUM_FILL_IP | SCCSUM_FILL_L4, nullptr) == SCCSUM_EINVAL);
-    EXPECT(sccsum_ipv4_fill(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr,
-                            nullptr, 3, 0, SCCSUM_FILL_ICMP_ECHO, nullptr) == SCCSUM_EINVAL);
+    // FILL_L4 / FILL_ICMP_ECHO: d_out2 is optional, the batch is checked like a frames batch
+    EXPECT(sccsum_ipv4_fill(static_cast<uint8_t*>(d16) + 1, 64, static_cast<const uint64_t*>(d16),
+                            static_cast<const uint32_t*>(d16), nullptr, nullptr, 3, 0,
+                            SCCSUM_FILL_IP | SCCSUM_FILL_L4, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_ipv4_fill(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16),
+                            reinterpret_cast<uint16_t*>(static_cast<uint8_t*>(d16) + 2), nullptr, 3, 0,
+                            SCCSUM_FILL_ICMP_ECHO, nullptr) == SCCSUM_EINVAL);
     EXPECT(sccsum_ipv4_fill(nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, 0,
                             SCCSUM_FILL_ICMP_ECHO | SCCSUM_FILL_L4_PSEUDO, nullptr) == SCCSUM_EINVAL);
     // RSS

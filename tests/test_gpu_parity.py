@@ -576,6 +576,67 @@ def test_ipv4_fill_whole_unit_stores(dev, gaps):
     assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
 
 
+@pytest.mark.parametrize("shape", ["ring_overflow", "static_order", "one_wave_tiles"])
+def test_ipv4_fill_drain_shapes(dev, kernel_variant, shape):
+    """The in-place fill stores its fields after the grid's reads (round 3):
+    each wave keeps its tiles' values (24 in VGPRs for the U 16 form, a ring
+    of 6 in LDS for the U 8 forms) and stores a tile early when it took more.
+    Tiles of one packet on a 1-block-per-CU grid give every wave ~50 tiles
+    (the early path); the static tile order (no slot, no grid wait) and tiles
+    of 64 are the other shapes.  No out2 (the production call).  Byte-exact
+    against the oracle."""
+    if kernel_variant not in (14, 15, 16):
+        pytest.skip("the fill runs the flat kernel")
+    lib = native.load()
+    rng = np.random.default_rng(0xD2A1)
+    buf, off, length = _tx_frames(rng, 50000 if shape != "one_wave_tiles" else 8000)
+    b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+    m = native.FILL_IP | native.FILL_L4 | native.FILL_ICMP_ECHO
+    try:
+        if shape == "ring_overflow":
+            native.check(lib.sccsum_set_blocks_per_cu(1), "blocks")
+            native.check(lib.sccsum_set_tile_packets(1), "tile packets")
+        elif shape == "static_order":
+            native.check(lib.sccsum_set_dynamic_tiles(0), "static")
+        else:
+            native.check(lib.sccsum_set_tile_bytes(0), "tile bytes")
+        for _ in range(2):  # a repeated fill is idempotent
+            batch.ipv4_fill(b, m)
+        torch.cuda.synchronize()
+    finally:
+        lib.sccsum_set_blocks_per_cu(8)
+        lib.sccsum_set_tile_packets(64)
+        lib.sccsum_set_dynamic_tiles(1)
+        lib.sccsum_set_tile_bytes(49152)
+    want_buf, _, _ = oracle.batch_ipv4_fill(buf, off, length, m)
+    got_buf = b.data.cpu().numpy()[: buf.size]
+    bad = np.nonzero(got_buf != want_buf)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+
+
+def test_ipv4_fill_full_scale_no_out2(dev, kernel_variant):
+    """cfg 2 tx at full size in the production form (no out2, no status):
+    every frame verifies afterwards and the fields equal classic generate
+    (the U 8 forms keep ~11 tiles per wave here: their LDS ring overflows)."""
+    from seastar_amd import devsynth
+
+    if kernel_variant in (1, 2):
+        pytest.skip("the fill runs the flat kernel")
+
+    b = devsynth.udp_frames(1 << 20, 1500, seed=78, device=dev)
+    gen = batch.ipv4_frames(b).clone()  # fields are 0 here: classic generate
+    f = b.data[: b.n * 1500].view(b.n, 1500)
+    f[:, 10:12] = 0x5A
+    f[:, 26:28] = 0xC3
+    batch.ipv4_fill(b, native.FILL_IP | native.FILL_L4)
+    got = torch.stack([f[:, 10:12].contiguous().view(torch.int16).view(-1),
+                       f[:, 26:28].contiguous().view(torch.int16).view(-1)], dim=1)
+    assert torch.equal(got, gen)
+    st = torch.empty(b.n, dtype=torch.uint8, device=dev)
+    batch.ipv4_frames(b, status=st)
+    assert int((st == 3).sum()) == b.n
+
+
 def test_ipv4_fill_full_scale_udp1500(dev):
     """cfg 2 at full size: fill(IP|L4) on frames with garbage checksum fields
     stores exactly what generate-on-zeroed-fields computes, and every frame verifies."""
@@ -1255,10 +1316,11 @@ def test_ip_fragments_fill(dev, kernel_variant):
 
 def test_scratch_on_a_side_stream(dev, kernel_variant):
     """ipv4_fill(FILL_L4) and fragments() on a stream that is not torch's
-    current one, with library-allocated scratch (out2 / workspace): the
-    scratch is recorded on the launch stream, so allocations churned on the
-    current stream meanwhile cannot take its block while the kernels still
-    use it.  Results byte-exact against the oracle."""
+    current one: fragments() allocates its workspace, which is recorded on
+    the launch stream, so allocations churned on the current stream meanwhile
+    cannot take its block while the kernels still use it; the
+    fill needs no scratch (one launch since round 3).  Results byte-exact
+    against the oracle."""
     if kernel_variant not in (1, 16):
         pytest.skip("scratch lifetime is kernel independent")
     rng = np.random.default_rng(0x5C1)
@@ -1272,7 +1334,7 @@ def test_scratch_on_a_side_stream(dev, kernel_variant):
     side = torch.cuda.Stream(device=dev)
     m = native.FILL_IP | native.FILL_L4 | native.FILL_ICMP_ECHO
     for _ in range(3):
-        batch.ipv4_fill(b, m, stream=side)  # out2 scratch allocated by the wrapper
+        batch.ipv4_fill(b, m, stream=side)
         got = batch.fragments(*args, stream=side)  # workspace allocated by the wrapper
         junk = [torch.full((1 << 20,), 7, dtype=torch.uint8, device=dev) for _ in range(8)]  # churn, current stream
         del junk
