@@ -85,8 +85,6 @@ def parse():
                          "jumbo packets as 5-fragment mbuf chains in HBM (checksummer::sum(const packet&))")
     ap.add_argument("--tile-bytes", type=int, default=None, help="A/B: flat-kernel tile target (sccsum_diag.h)")
     ap.add_argument("--variant", type=int, default=None, help="A/B: kernel form (sccsum_set_kernel_variant)")
-    ap.add_argument("--fill-out2", action="store_true",
-                    help="A/B: fill also reports the stored values in out2 (the two-pass A/B library needs it)")
     ap.add_argument("--run-align", type=int, default=None, help="A/B: run-start alignment in units (sccsum_set_run_align)")
     ap.add_argument("--sync", default="auto", choices=["auto", "spin", "yield"],
                     help="how the host thread waits on the device (hipSetDeviceFlags schedule)")
@@ -810,7 +808,7 @@ def run_fill(args, world, rank, dev):
     mode = native.FILL_IP | native.FILL_L4
     st = torch.empty(n, dtype=torch.uint8, device=dev)
     for b in bs:
-        batch.ipv4_fill(b, mode, out2=torch.empty(2 * n, dtype=torch.int16, device=dev) if args.fill_out2 else None)
+        batch.ipv4_fill(b, mode)
         batch.ipv4_frames(b, status=st)
         torch.cuda.synchronize()
         assert args.no_check or int((st != 3).sum()) == 0, "filled frames do not verify"
@@ -823,21 +821,14 @@ def run_fill(args, world, rank, dev):
     warm = max(args.warmup, R)
     LAUNCHES.add(kern, warm)
     sel = LAUNCHES.select(kern, args.steps)
-    # prebuilt launches; out2 (the values stored) only for the two-pass A/B library, whose
-    # generate pass hands its words to the store pass there
-    outs2 = [torch.empty(2 * n, dtype=torch.int16, device=dev) if args.fill_out2 else None for _ in range(ns)]
+    # prebuilt launches; the caller's out2 (the values stored) carries the generate pass's
+    # words to the store pass, so no per-call scratch allocation is timed
+    outs2 = [torch.empty(2 * n, dtype=torch.int16, device=dev) for _ in range(ns)]
     pre = {(r, i): batch.prepare_call("sccsum_ipv4_fill", bs[r].data, bs[r].bytes_len, bs[r].off, bs[r].length,
                                       outs2[i], None, bs[r].n, bs[r].max_len, mode)
            for r in range(R) for i in range(ns)}
     wall, launch_s = timed(lambda k: pre[(k % R, k % ns)](streams[k % ns]), args.steps, warm, world, streams)
     alg = n * (FRAME + META_BYTES + 4)  # read every byte + metadata, write the two 2-byte fields
-    if native.load().sccsum_fill_passes() == 2:  # the two-pass A/B library
-        desc = " + fill_store_kernel (sccsum_ipv4_fill: generate pass, then the field-store pass)"
-        extra_sel = {"trace_select_extra": [{"kernel": "fill_store_kernel", "skip": sel["skip"],
-                                             "count": sel["count"]}]}
-    else:
-        desc = " (sccsum_ipv4_fill: one launch; the fields are stored after the grid's reads)"
-        extra_sel = {}
     ranks = per_rank(world, rank, dev, **rank_rate(n * FRAME, args.steps), avg_launch_us=launch_s * 1e6,
                      frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS)
     if rank == 0:
@@ -846,7 +837,10 @@ def run_fill(args, world, rank, dev):
              {"workload": "cfg2 tx: 1500 B IPv4/UDP frames, IP + UDP checksums generated and stored in place",
               "packets_per_gpu": n, "rotation": f"{R} distinct batches launched in turn",
               "streams": f"{ns} (step k on stream k % {ns})", "parallelism": f"{world} independent shards"},
-             roofline(alg, launch_s, "fill", kern + desc, sel, args, extra_sel), extra={"per_rank": ranks})
+             roofline(alg, launch_s, "fill", kern + " + fill_store_kernel (sccsum_ipv4_fill: generate pass, "
+                                                    "then the field-store pass)", sel, args,
+                      {"trace_select_extra": [{"kernel": "fill_store_kernel", "skip": sel["skip"],
+                                               "count": sel["count"]}]}), extra={"per_rank": ranks})
 
 
 def run_sweep(args, world, rank, dev):

@@ -247,12 +247,14 @@ int sccsum_ipv4_frames_rss(const void* d_bytes, uint64_t bytes_len, const uint64
  * first fragment's L4 header, a later fragment's payload — are never written.
  *   mode: SCCSUM_FILL_IP and/or one of SCCSUM_FILL_L4 / SCCSUM_FILL_L4_PSEUDO
  *         (| SCCSUM_FILL_TSO), and/or SCCSUM_FILL_ICMP_ECHO (not with
- *         L4_PSEUDO).  FILL_L4 and FILL_ICMP_ECHO read every byte in one
- *         launch of the flat kernel, which stores the fields once the
- *         launch's reads are done; the others read only the 20-byte header.
+ *         L4_PSEUDO).  FILL_L4 and FILL_ICMP_ECHO read every byte (the flat
+ *         kernel generates into d_out2, then a second pass stores the
+ *         fields); the others read only the 20-byte header.
  *   d_out2[2i] / [2i+1] = the IP / L4 values stored (0 where nothing was
- *         stored); may be NULL (ABI 2 as first released in round 3 required
- *         it with FILL_L4 / FILL_ICMP_ECHO; NULL is accepted again).
+ *         stored); may be NULL: FILL_L4 / FILL_ICMP_ECHO then hand the values
+ *         between the passes in a stream-ordered allocation (hipMallocAsync /
+ *         hipFreeAsync on `stream`; ABI 2 as first released in round 3
+ *         refused NULL here).
  *   d_status[i] = SCCSUM_ST_OK if the IP field was written, SCCSUM_ST_L4_OK
  *         if the L4 field was written, plus MALFORMED / RANGE / IPFRAG; may
  *         be NULL.

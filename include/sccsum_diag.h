@@ -77,11 +77,6 @@ int sccsum_set_run_align(int units);
 int sccsum_read_probe(const void* d_src, uint64_t bytes, uint64_t* d_sink, void* stream);
 int sccsum_read_probe_blocks(void);
 
-/* Launches sccsum_ipv4_fill makes with SCCSUM_FILL_L4 / SCCSUM_FILL_ICMP_ECHO:
- * 1 (the default build: the flat kernel stores the fields itself) or 2 (the
- * SCCSUM_FILL_TWO_PASS A/B build: generate pass, then fill_store_kernel). */
-int sccsum_fill_passes(void);
-
 /* Burst queues driven from this thread: how a batch holding zero-copy packets
  * (sccsum_burst_submit_mapped) runs.  2 (default) = one launch of the
  * fragment-list kernel that reads the pinned metadata, descriptors and

@@ -50,22 +50,6 @@ constexpr uint32_t kFlagFillIcmp = 8;  // frames: turn ICMP echo requests into r
 constexpr uint32_t kFillFlags = kFlagFillL4 | kFlagFillIcmp;  // the in-place (FILL) instantiation
 constexpr uint32_t kFlagFullChunks = 16;  // flat kernel: a run's last chunk loads all U rows (diagnostic A/B)
 constexpr uint32_t kRunAlignShift = 12;   // flat kernel, flags bits 12-13: run extents start on 1 / 4 / 8-unit boundaries
-#ifdef SCCSUM_FILL_TWO_PASS
-constexpr bool kFillDrain = false;  // (A/B form) generate pass into out2, then fill_store_kernel
-#else
-constexpr bool kFillDrain = true;   // the FILL kernel stores the fields itself, after the grid's reads
-#endif
-// in-place fill: a frame's field plan (bits 0-7: the L4 / ICMP checksum
-// field's offset from the frame start)
-constexpr uint32_t kFiIp = 1u << 8;     // store the IPv4 header checksum (+10)
-constexpr uint32_t kFiL4 = 1u << 9;     // store the L4 checksum at the offset
-constexpr uint32_t kFiIcmp = 1u << 10;  // echo reply: type and code (offset - 2) become 0
-constexpr uint64_t kDrainWaitTicks = 20000;  // s_memrealtime ticks (100 MHz): 200 us
-#ifdef SCCSUM_DRAIN_FORM
-constexpr int kDrainForm = SCCSUM_DRAIN_FORM;  // (A/B) store form of the fill drain
-#else
-constexpr int kDrainForm = 2;
-#endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -117,18 +101,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 
 __device__ __forceinline__ u32x4 load_unit(const uint8_t* p) {
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-}
-
-// A checksum field (2 bytes, the value as the little-endian word it sums as):
-// one 2-byte store, or two byte stores at an odd address.  Field bytes of
-// different frames never overlap, so stores need no coordination.
-__device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {
-    if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0u) {
-        *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(v);
-    } else {
-        p[0] = static_cast<uint8_t>(v);
-        p[1] = static_cast<uint8_t>(v >> 8);
-    }
 }
 
 // Logical block id with XCD affinity: blocks b, b+8, b+16 ... are dealt to one
@@ -912,9 +884,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
     // (acquire_heads).  Without `heads`: static round robin.
     const uint64_t wglob = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
     const uint32_t grp = static_cast<uint32_t>(wglob % kGroups);
-    // parts that must reset before the slot is released: the kGroups dequeue
-    // counters, plus (in-place fill) the drain's two counters
-    constexpr uint32_t kParts = kGroups + (FILL && kFillDrain ? 1u : 0u);
     const uint64_t rest = ntiles > nwaves ? ntiles - nwaves : 0;
     const uint32_t tiles_g = rest > grp ? static_cast<uint32_t>((rest - grp + kGroups - 1) / kGroups) : 0u;
     const uint32_t waves_g = static_cast<uint32_t>(nwaves / kGroups);
@@ -934,7 +903,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 uint32_t* const groups_done = heads + kGroups * kHeadStride;
                 const uint32_t gd = __hip_atomic_fetch_add(groups_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (gd == kParts - 1) {  // every group has reset: the slot is free for another launch
+                if (gd == kGroups - 1) {  // every group has reset: the slot is free for another launch
                     __hip_atomic_store(groups_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __hip_atomic_store(done, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1034,116 +1003,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
 #pragma unroll
         for (int u = 0; u < R; ++u)
             v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(16u * g + vo + 1024u * u), 0, kNT);
-    };
-
-    // ---- in-place fill: stores inside the read stream cost it ~100 us per
-    // 1 M frames, a pass of their own after it ~60-70.  So a
-    // wave keeps its tiles' field values and plans in registers (the tile
-    // number in an SGPR) and stores them once the whole grid has read its
-    // bytes: no out2 round trip, no header re-read, no second launch.  A wave
-    // that took more tiles than it keeps stores its oldest tile's fields
-    // early (the same stores, only sooner).
-    // The U = 16 form (big launches, 2 waves per SIMD) keeps 24 tiles in
-    // VGPRs as a shift register; the U = 8 forms have no VGPRs to spare (3
-    // waves per SIMD at 168) and keep 6 tiles in an LDS ring instead, which
-    // costs them no occupancy (3 blocks per CU either way).
-    constexpr bool kDrain = FILL && kFillDrain;
-    constexpr bool kLdsStash = kDrain && U < 16;
-    constexpr int kStash = kDrain ? (U >= 16 ? 24 : 6) : 1;
-    constexpr int kRegStash = kLdsStash ? 1 : kStash;
-    uint32_t stash_t[kRegStash], stash_w[kRegStash], stash_i[kRegStash];
-    __shared__ uint32_t lstash_all[kLdsStash ? kWavesPerBlock : 1][kLdsStash ? kStash : 1][2 * kWave];
-    __shared__ uint32_t ltile_all[kLdsStash ? kWavesPerBlock : 1][kLdsStash ? kStash : 1];
-    uint32_t nstash = 0;  // tiles taken so far (LDS ring) / tiles held (registers)
-    // A tile's fields, stored at once (a full ring / register stash): plain
-    // 2-byte stores.
-    auto field_stores = [&](uint32_t tt, uint32_t w, uint32_t info) {
-        const TileRef tr = tile_ref(tt);
-        if (lane < tr.cnt && info != 0u) {
-            uint8_t* const p = const_cast<uint8_t*>(Q.bytes[tr.q]) + Q.off[tr.q][tr.base + lane];
-            if (info & kFiIp) store_field(p + 10, w);
-            if (info & kFiL4) {
-                uint8_t* const f = p + (info & 0xffu);
-                if (info & kFiIcmp) store_field(f - 2, 0u);  // echo_reply, code 0 (ip.cc:469-470)
-                store_field(f, w >> 16);
-            }
-        }
-    };
-    // The drain: NB tiles' fields with every load of a step in flight (the
-    // frame offsets, then the dwords holding the fields), then the stores.
-    // kDrainForm 0: plain 2-byte stores; 1: the dwords are read first (their
-    // lines then sit whole in L2 when the stores land) and the 2-byte stores
-    // follow; 2: the dwords are rewritten with the field bytes merged in.  A
-    // dword never holds two frames' field bytes (frames are >= 20 B apart,
-    // the IP field is at +8..+11, L4 fields lie past +20), so no atomics.
-    auto drain_fields = [&](const auto& tt, const auto& w, const auto& info, uint32_t nv) {
-        constexpr int NB = std::extent<std::remove_reference_t<decltype(tt)>>::value;
-        uint8_t* fp[NB];
-#pragma unroll
-        for (int k = 0; k < NB; ++k) {
-            fp[k] = nullptr;
-            const TileRef tr = tile_ref(static_cast<uint32_t>(k) < nv ? tt[k] : 0u);
-            if (static_cast<uint32_t>(k) < nv && lane < tr.cnt && info[k] != 0u) {
-                fp[k] = const_cast<uint8_t*>(Q.bytes[tr.q]) + Q.off[tr.q][tr.base + lane];
-            }
-        }
-        // piece 0: the IP field (2 B at +10); piece 1: the L4 field (2 B), or
-        // for an ICMP echo reply type, code and checksum (4 B from offset - 2)
-        uint8_t* ps[NB][2];
-        uint32_t pl[NB][2], pv[NB][2], x0[NB][2], x1[NB][2];
-#pragma unroll
-        for (int k = 0; k < NB; ++k) {
-            const uint32_t fi = info[k];
-            const bool on = fp[k] != nullptr;
-            ps[k][0] = on && (fi & kFiIp) ? fp[k] + 10 : nullptr;
-            pl[k][0] = 2u;
-            pv[k][0] = w[k] & 0xffffu;
-            const bool icmp = (fi & kFiIcmp) != 0u;
-            ps[k][1] = on && (fi & kFiL4) ? fp[k] + (fi & 0xffu) - (icmp ? 2u : 0u) : nullptr;
-            pl[k][1] = icmp ? 4u : 2u;
-            pv[k][1] = icmp ? w[k] & 0xffff0000u : w[k] >> 16;
-        }
-        if constexpr (kDrainForm != 0) {
-#pragma unroll
-            for (int k = 0; k < NB; ++k) {
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    x0[k][j] = x1[k][j] = 0u;
-                    if (ps[k][j] != nullptr) {
-                        const uintptr_t a = reinterpret_cast<uintptr_t>(ps[k][j]);
-                        const uint32_t* d = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-                        x0[k][j] = d[0];
-                        if ((a & 3u) + pl[k][j] > 4u) x1[k][j] = d[1];
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NB; ++k) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                uint8_t* const q = ps[k][j];
-                if (q == nullptr) continue;
-                if constexpr (kDrainForm == 2) {
-                    const uintptr_t a = reinterpret_cast<uintptr_t>(q);
-                    uint32_t* d = reinterpret_cast<uint32_t*>(a & ~uintptr_t(3));
-                    const uint32_t sh = 8u * static_cast<uint32_t>(a & 3u);
-                    const uint64_t m = ((pl[k][j] == 4u ? 0xffffffffull : 0xffffull)) << sh;
-                    const uint64_t x = (static_cast<uint64_t>(x1[k][j]) << 32) | x0[k][j];
-                    const uint64_t y = (x & ~m) | (static_cast<uint64_t>(pv[k][j]) << sh);
-                    d[0] = static_cast<uint32_t>(y);
-                    if ((a & 3u) + pl[k][j] > 4u) d[1] = static_cast<uint32_t>(y >> 32);
-                } else {
-                    if constexpr (kDrainForm == 1) asm volatile("" ::"v"(x0[k][j]), "v"(x1[k][j]));
-                    if (pl[k][j] == 4u) {
-                        store_field(q, pv[k][j]);
-                        store_field(q + 2, pv[k][j] >> 16);
-                    } else {
-                        store_field(q, pv[k][j]);
-                    }
-                }
-            }
-        }
     };
 
     uint64_t o_n = 0;
@@ -1269,7 +1128,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
         uint32_t word = 0, st = 0;
         bool slow = huge && mine && !range_bad;
         uint32_t ipc = 0, pseudo = 0, fpos = 0;
-        uint32_t finfo = 0;  // in-place fill: which fields this lane's frame gets, and where (kFi*)
         int srs = 0, sre = 0;
         if (IPV4) {
             const uint32_t h0 = header_dword(hs, head, 0), h1 = header_dword(hs, head, 1);
@@ -1311,8 +1169,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
                 }
                 const bool has_field = fo != 0u && atomic && l4_len >= fo + 2u;
                 fpos = has_field ? head + l4_off + fo : 0u;
-                finfo = (fill_ip ? kFiIp : 0u) | (has_field ? kFiL4 | (l4_off + fo) : 0u) |
-                        (has_field && icmp_lane ? kFiIcmp : 0u);
                 uint32_t rr;
                 if (icmp_lane) {
                     rr = ~S & 0xffffu;
@@ -1344,7 +1200,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
             word = 0;
             st = SCCSUM_ST_MALFORMED;
         }
-        if (range_bad || short_frame || !mine) finfo = 0;
 
         // ---- D: exact redo of the packets the fast path could not take
         uint64_t todo = __ballot(slow);
@@ -1404,103 +1259,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
             }
             if (status) tile_store(status + base, lane, static_cast<uint8_t>(st), pol_st);
         }
-        if constexpr (kLdsStash) {
-            const uint32_t slot = nstash % kStash;
-            uint32_t* const ls = lstash_all[wv][slot];
-            if (nstash >= static_cast<uint32_t>(kStash)) {  // the ring is full: its oldest tile's stores leave now
-                field_stores(__builtin_amdgcn_readfirstlane(ltile_all[wv][slot]), ls[lane], ls[kWave + lane]);
-            }
-            ls[lane] = word;
-            ls[kWave + lane] = finfo;
-            if (lane == 0) ltile_all[wv][slot] = static_cast<uint32_t>(t);
-            ++nstash;
-        } else if constexpr (kDrain) {
-            if (nstash == kStash) field_stores(stash_t[kStash - 1], stash_w[kStash - 1], stash_i[kStash - 1]);
-#pragma unroll
-            for (int k = kStash - 1; k > 0; --k) {
-                stash_t[k] = stash_t[k - 1];
-                stash_w[k] = stash_w[k - 1];
-                stash_i[k] = stash_i[k - 1];
-            }
-            stash_t[0] = static_cast<uint32_t>(t);
-            stash_w[0] = word;
-            stash_i[0] = finfo;
-            nstash += nstash < static_cast<uint32_t>(kStash) ? 1u : 0u;
-        }
         t = t1;
         t1 = t2;
-    }
-
-    if constexpr (kDrain) {
-        // Wait until every block of the grid has left its tile loop, so the
-        // stores follow the read stream instead of cutting into it: one wave
-        // per block counts the block in and polls the count with
-        // system-scope loads (they miss this XCD's L2, which would keep a
-        // stale copy of the line), sleeping ~3 us between polls.  The wait
-        // is only an ordering for speed: a frame's fields depend on its own
-        // wave's reads alone, so a wait that times out (a grid not all
-        // resident, e.g. beside another kernel) still stores the right
-        // values.  The two counters live in the launch's slot and are reset
-        // by the last block out, which then counts as one more part for the
-        // slot's release (kParts).
-        uint32_t* const fin = heads ? heads + (kGroups + 1) * kHeadStride : nullptr;
-        uint32_t* const ext = heads ? heads + (kGroups + 2) * kHeadStride : nullptr;
-        const uint32_t nb = gridDim.x;
-        if (heads != nullptr) {
-            __syncthreads();
-            if (wv == 0 && lane == 0) {
-                __hip_atomic_fetch_add(fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-                while (__hip_atomic_load(fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < nb &&
-                       __builtin_amdgcn_s_memrealtime() - w0 < kDrainWaitTicks) {
-                    __builtin_amdgcn_s_sleep(127);
-                }
-            }
-            __syncthreads();
-            if (wv == 0 && lane == 0) {  // this block is past its wait
-                const uint32_t e = __hip_atomic_fetch_add(ext, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (e == nb - 1u) {  // the last block out: reset, then count as a part
-                    __hip_atomic_store(fin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(ext, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    uint32_t* const groups_done = heads + kGroups * kHeadStride;
-                    const uint32_t gd =
-                        __hip_atomic_fetch_add(groups_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (gd == kParts - 1) {
-                        __hip_atomic_store(groups_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        __hip_atomic_store(done, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
-                }
-            }
-        }
-        if constexpr (kLdsStash) {
-            const uint32_t c0 = nstash > static_cast<uint32_t>(kStash) ? nstash - kStash : 0u;
-            uint32_t tt[kStash], ww[kStash], ii[kStash];
-#pragma unroll
-            for (int k = 0; k < kStash; ++k) {
-                const uint32_t slot = (c0 + k) % kStash;
-                tt[k] = __builtin_amdgcn_readfirstlane(ltile_all[wv][slot]);
-                ww[k] = lstash_all[wv][slot][lane];
-                ii[k] = lstash_all[wv][slot][kWave + lane];
-            }
-            drain_fields(tt, ww, ii, nstash - c0);
-        } else {
-            constexpr int NB = 4;
-#pragma unroll
-            for (int k0 = 0; k0 < kStash; k0 += NB) {
-                if (static_cast<uint32_t>(k0) < nstash) {
-                    uint32_t tt[NB], ww[NB], ii[NB];
-#pragma unroll
-                    for (int k = 0; k < NB; ++k) {
-                        tt[k] = stash_t[k0 + k];
-                        ww[k] = stash_w[k0 + k];
-                        ii[k] = stash_i[k0 + k];
-                    }
-                    drain_fields(tt, ww, ii, nstash - k0);
-                }
-            }
-        }
     }
 }
 
@@ -1534,15 +1294,24 @@ __global__ __launch_bounds__(kBlock) void frag_combine_kernel(const uint32_t* __
     if (status) status[i] = bad ? SCCSUM_ST_RANGE : (r == 0 ? SCCSUM_ST_OK : 0u);
 }
 
-// In-place fill, second pass of the two-pass form (round 2; kept as the A/B
-// form SCCSUM_FILL_TWO_PASS): store the values the flat kernel generated
+// In-place fill, second pass: store the values the flat kernel generated
 // (FILL instantiation, words[i] = IP | L4 << 16) into the frames' fields.
 // One thread per frame; which fields it writes is decided from the frame's
 // own (unmodified) header exactly as the first pass decided it.  The stores
 // run as a pass of their own, after the read stream: interleaved with the
 // stream the same stores cost ~100 us per 1 M frames, as their own pass
 // ~70-90 us (HBM read/write turnarounds; tools/dev/store_probe.hip,
-// DESIGN.md §5.6).
+// DESIGN.md §5.6).  Field bytes of different frames never overlap, so the
+// 2-byte stores need no coordination.
+__device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {
+    if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0u) {
+        *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(v);
+    } else {
+        p[0] = static_cast<uint8_t>(v);
+        p[1] = static_cast<uint8_t>(v >> 8);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void fill_store_kernel(uint8_t* __restrict__ bytes, uint64_t bytes_len,
                                                             const uint64_t* __restrict__ off,
                                                             const uint32_t* __restrict__ len,
@@ -1752,7 +1521,7 @@ unsigned grid_for(uint64_t n) {
 // instead: the same results without the dynamic load balance.
 constexpr uint32_t kSlots = 2048;
 constexpr uint32_t kSlotProbe = 16;  // ring entries a launch checks before it falls back to the static order
-constexpr uint32_t kSlotWords = (kGroups + 3) * kHeadStride;  // + the completion counter, the fill drain's two
+constexpr uint32_t kSlotWords = (kGroups + 1) * kHeadStride;  // + the completion counter
 
 struct DevicePool {
     std::mutex mu;
@@ -2505,22 +2274,37 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
     }
     if (n == 0) return SCCSUM_OK;
     if (mode & (SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO)) {
-        // one launch: the flat kernel reads every frame and stores the fields
-        // once the grid's reads are done (d_out2 / d_status optional reports).
-        // A/B form (SCCSUM_FILL_TWO_PASS): pass 1 generates into d_out2
-        // (required), pass 2 stores the fields.
-        if (!sccsum::kFillDrain && !d_out2) return SCCSUM_EINVAL;
+        // pass 1 generates into d_out2, pass 2 stores the fields.  Without a
+        // caller's d_out2 the values go through a stream-ordered allocation
+        // (hipMallocAsync / hipFreeAsync on `stream`: no host sync, safe
+        // under graph capture, freed once pass 2 is done with it)
+        const hipStream_t s = static_cast<hipStream_t>(stream);
+        if (!sccsum::batch_ok<true>(d_bytes, d_off, d_len, nullptr, d_out2, d_status, sccsum::kFlagFillL4)) {
+            return SCCSUM_EINVAL;  // (before any allocation)
+        }
+        void* scratch = nullptr;
+        if (!d_out2) {
+            const hipError_t e = hipMallocAsync(&scratch, 4 * n, s);
+            if (e != hipSuccess) return static_cast<int>(e);
+        }
+        uint16_t* const vals = d_out2 ? d_out2 : static_cast<uint16_t*>(scratch);
         const uint32_t flags = ((mode & SCCSUM_FILL_L4) ? sccsum::kFlagFillL4 : 0u) |
                                ((mode & SCCSUM_FILL_ICMP_ECHO) ? sccsum::kFlagFillIcmp : 0u) |
                                ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u);
-        const int rc = sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len,
-                                            stream, flags);
-        if (rc != SCCSUM_OK || sccsum::kFillDrain) return rc;
-        const unsigned grid = static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock);
-        sccsum::fill_store_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, static_cast<hipStream_t>(stream)>>>(
-            static_cast<uint8_t*>(d_bytes), bytes_len, d_off, d_len, reinterpret_cast<const uint32_t*>(d_out2), n,
-            mode);
-        return static_cast<int>(hipGetLastError());
+        int rc = sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, vals, d_status, n, max_len,
+                                      stream, flags);
+        if (rc == SCCSUM_OK) {
+            const unsigned grid = static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock);
+            sccsum::fill_store_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, s>>>(
+                static_cast<uint8_t*>(d_bytes), bytes_len, d_off, d_len, reinterpret_cast<const uint32_t*>(vals), n,
+                mode);
+            rc = static_cast<int>(hipGetLastError());
+        }
+        if (scratch) {
+            const hipError_t e = hipFreeAsync(scratch, s);
+            if (rc == SCCSUM_OK && e != hipSuccess) rc = static_cast<int>(e);
+        }
+        return rc;
     }
     if (!d_bytes || !d_off || !d_len || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
         (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_out2) & 3u)) {
@@ -2595,8 +2379,6 @@ int sccsum_set_tail_split(int split, int quarters) {
 }
 
 int sccsum_sync(void* stream) { return static_cast<int>(hipStreamSynchronize(static_cast<hipStream_t>(stream))); }
-
-int sccsum_fill_passes(void) { return sccsum::kFillDrain ? 1 : 2; }
 
 int sccsum_read_probe_blocks(void) { return sccsum::cu_count() * sccsum::kBlocksPerCU; }
 

@@ -80,7 +80,6 @@ _PROTOS = {
     "sccsum_set_run_align": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_read_probe": (ctypes.c_int, [_vp, _u64, _vp, _vp]),
     "sccsum_read_probe_blocks": (ctypes.c_int, []),
-    "sccsum_fill_passes": (ctypes.c_int, []),
     "sccsum_pipeline_create": (ctypes.c_int, [ctypes.c_int, _u64, _u32, ctypes.c_int, ctypes.POINTER(_vp)]),
     "sccsum_pipeline_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, _u64, _vp, _vp, _vp, _u64, _u32,
                                            _vp, _vp]),

@@ -577,14 +577,12 @@ def test_ipv4_fill_whole_unit_stores(dev, gaps):
 
 
 @pytest.mark.parametrize("shape", ["ring_overflow", "static_order", "one_wave_tiles"])
-def test_ipv4_fill_drain_shapes(dev, kernel_variant, shape):
-    """The in-place fill stores its fields after the grid's reads (round 3):
-    each wave keeps its tiles' values (24 in VGPRs for the U 16 form, a ring
-    of 6 in LDS for the U 8 forms) and stores a tile early when it took more.
-    Tiles of one packet on a 1-block-per-CU grid give every wave ~50 tiles
-    (the early path); the static tile order (no slot, no grid wait) and tiles
-    of 64 are the other shapes.  No out2 (the production call).  Byte-exact
-    against the oracle."""
+def test_ipv4_fill_tile_shapes(dev, kernel_variant, shape):
+    """The in-place fill under other tile shapes: one-packet tiles on a
+    1-block-per-CU grid (~50 tiles per wave), the static tile order (no
+    counter slot), the plain 64-packet cap.  No out2: the generate pass hands
+    its values to the store pass through the library's stream-ordered
+    scratch (the production call).  Byte-exact against the oracle."""
     if kernel_variant not in (14, 15, 16):
         pytest.skip("the fill runs the flat kernel")
     lib = native.load()
@@ -617,7 +615,7 @@ def test_ipv4_fill_drain_shapes(dev, kernel_variant, shape):
 def test_ipv4_fill_full_scale_no_out2(dev, kernel_variant):
     """cfg 2 tx at full size in the production form (no out2, no status):
     every frame verifies afterwards and the fields equal classic generate
-    (the U 8 forms keep ~11 tiles per wave here: their LDS ring overflows)."""
+    (the values cross between the passes in the library's scratch)."""
     from seastar_amd import devsynth
 
     if kernel_variant in (1, 2):
@@ -1319,8 +1317,8 @@ def test_scratch_on_a_side_stream(dev, kernel_variant):
     current one: fragments() allocates its workspace, which is recorded on
     the launch stream, so allocations churned on the current stream meanwhile
     cannot take its block while the kernels still use it; the
-    fill needs no scratch (one launch since round 3).  Results byte-exact
-    against the oracle."""
+    fill's values cross between its passes in the library's stream-ordered
+    allocation on the launch stream.  Results byte-exact against the oracle."""
     if kernel_variant not in (1, 16):
         pytest.skip("scratch lifetime is kernel independent")
     rng = np.random.default_rng(0x5C1)
