@@ -143,11 +143,16 @@ def load():
         )
     # SCCSUM_LIB: diagnostic override (A/B builds of the same ABI); still a native library, never a fallback
     lib = ctypes.CDLL(os.environ.get("SCCSUM_LIB", LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+    # SCCSUM_ABI_ANY=1: diagnostic A/B against an older build (another ABI version; entry points it
+    # lacks stay unbound); only ever set together with SCCSUM_LIB by tools/gpu_session.sh's lib: step
+    any_abi = bool(os.environ.get("SCCSUM_ABI_ANY")) and "SCCSUM_LIB" in os.environ
     for name, (res, args) in _PROTOS.items():
+        if any_abi and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.sccsum_abi_version() != ABI_VERSION:
+    if lib.sccsum_abi_version() != ABI_VERSION and not any_abi:
         raise RuntimeError(f"libsccsum ABI version {lib.sccsum_abi_version()} != {ABI_VERSION}: rebuild it")
     _LIB = lib
     return lib

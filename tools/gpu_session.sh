@@ -13,8 +13,8 @@
 #                          cut to the timed dispatches by tools/prof_timed.py ($TAG_pmc_CFG.json)
 #   py:SCRIPT[+ARG...]     python SCRIPT ARG... (a tools/ probe)
 #   bin:PROGRAM[+ARG...]   a probe program built here beforehand (tools/dev/*.hip)
-#   lib:PATH | lib:default the library later steps load (SCCSUM_LIB: an A/B build of the same ABI);
-#                          their bench logs are named after it
+#   lib:PATH | lib:default the library later steps load (SCCSUM_LIB: an A/B build of the same ABI,
+#                          or libsccsum_at_<commit>.so, an older tree's build); bench logs are named after it
 # Outputs go to gpurun_out/TAG/; steps.log records each step's outcome.
 set -o pipefail
 TAG=${1:?usage: gpu_session.sh TAG STEP...}
@@ -56,11 +56,13 @@ run_step() {
                 >> "$O/bench_$n$LIBTAG.log" 2>&1 ;;
         lib)
             if [ "$rest" = default ]; then
-                unset SCCSUM_LIB
+                unset SCCSUM_LIB SCCSUM_ABI_ANY
                 LIBTAG=
             else
                 export SCCSUM_LIB=$R/$rest
                 LIBTAG=_$(basename "$rest" .so)
+                # libsccsum_at_<commit>.so: an older tree's build (maybe another ABI version)
+                case $rest in *libsccsum_at_*) export SCCSUM_ABI_ANY=1 ;; *) unset SCCSUM_ABI_ANY ;; esac
             fi ;;
         trace)
             split "$rest"
