@@ -1317,8 +1317,13 @@ __global__ __launch_bounds__(kBlock) void fill_store_kernel(uint8_t* __restrict_
                                                             const uint32_t* __restrict__ len,
                                                             const uint32_t* __restrict__ words, uint64_t n,
                                                             uint32_t mode) {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (i >= n) return;
+    const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i0 >= n) return;
+#ifdef SCCSUM_FILL_REV
+    const uint64_t i = n - 1 - i0;  // (A/B) last-read frames first
+#else
+    const uint64_t i = i0;
+#endif
     const uint64_t o = off[i];
     const uint32_t L = len[i];
     if (o > bytes_len || L > bytes_len - o || L < 20u) return;
