@@ -1281,11 +1281,17 @@ __global__ __launch_bounds__(kBlock) void frag_combine_kernel(const uint32_t* __
     if (i >= n) return;
     const uint64_t f0 = pkt_first[i], f1 = pkt_first[i + 1];
     bool bad = f1 < f0 || f1 > nfrag;
+    const uint64_t f_end = bad ? f0 : f1;
     uint64_t S = 0;
     uint32_t par = 0;
-    for (uint64_t j = f0; !bad && j < f1; ++j) {
+    // no exit on a bad fragment inside the loop: its trip count then depends
+    // on no loaded value, so the loads of all the packet's fragments issue
+    // back to back instead of one round trip per fragment (a 5-fragment
+    // packet's walk was ~5 us of latency)
+#pragma unroll 4
+    for (uint64_t j = f0; j < f_end; ++j) {
         const uint32_t t = raw[j];
-        bad = (raw_status[j] & SCCSUM_ST_RANGE) != 0;
+        bad = bad || (raw_status[j] & SCCSUM_ST_RANGE) != 0;
         S += par ? swap16(t) : t;
         par ^= frag_len[j] & 1u;
     }
