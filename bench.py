@@ -613,7 +613,7 @@ def run_mixed(args, world, rank, dev):
             for _ in range(ns)]
     sts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(R)]
     for rx, st in zip(rxs, sts):  # rx: checksums stored, so every frame verifies
-        batch.ipv4_fill(rx, native.FILL_IP | native.FILL_L4)
+        batch.ipv4_fill(rx, native.FILL_IP | native.FILL_L4, out2=outs[0][0])  # (out2: older A/B builds need it)
         if multi:
             batch.ipv4_frames(rx, out2=outs[0][1], status=st)
             LAUNCHES.add(flat_kernel(True, False, n, rx.bytes_len))

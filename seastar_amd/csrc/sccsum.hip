@@ -1687,6 +1687,10 @@ void launch_flat(FlatKernel kern, hipStream_t s, Queues& Q, uint64_t n_total, ui
     uint64_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     blocks = blocks < cap ? blocks : cap;
     blocks = (blocks + 15) & ~uint64_t(15);  // multiple of 16: XCD mapping, waves divide into kGroups
+    // A sticky error left by an earlier, unrelated HIP call on this thread
+    // would read as this launch failing below, and the slot would go back to
+    // the ring while the kernel runs on it: clear it first.
+    (void)hipGetLastError();
     const HeadSlot H = K.dynamic ? acquire_heads(s) : HeadSlot{};
     flags |= static_cast<uint32_t>(K.out_policy) << kOutPolicyShift;
     if (!K.short_chunks) flags |= kFlagFullChunks;
