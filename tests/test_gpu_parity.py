@@ -791,6 +791,33 @@ def test_many_launches_in_flight_streams_and_graphs(dev, kernel_variant):
     assert np.array_equal(gst.cpu().numpy(), want_st)
 
 
+def test_fill_without_out2_in_a_graph(dev, kernel_variant):
+    """sccsum_ipv4_fill with no d_out2, captured in a HIP graph: its scratch
+    is a stream-ordered allocation (a graph memory node), so the call stays
+    capturable; each replay over freshly restored frames stores exactly the
+    oracle's fields."""
+    if kernel_variant not in (15, 16):
+        pytest.skip("the fill runs the flat kernel")
+    rng = np.random.default_rng(0x6A1)
+    buf, off, length = _tx_frames(rng, 3000)
+    b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+    orig = b.data.clone()
+    m = native.FILL_IP | native.FILL_L4 | native.FILL_ICMP_ECHO
+    want_buf, _, _ = oracle.batch_ipv4_fill(buf, off, length, m)
+    g = torch.cuda.CUDAGraph()
+    cs = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=cs):
+        batch.ipv4_fill(b, m, stream=cs)
+    for _ in range(3):
+        b.data.copy_(orig)
+        g.replay()
+        torch.cuda.synchronize()
+        got = b.data.cpu().numpy()[: buf.size]
+        bad = np.nonzero(got != want_buf)[0]
+        assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+
+
 def test_multi_batch_launch(dev, kernel_variant):
     """sccsum_ipv4_frames_multi / sccsum_spans_multi: 16 independent batches in
     one launch (empty, 1 packet, 1500 B frames, Zipf frames at odd offsets,
