@@ -601,13 +601,6 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
     u32x4(*picks)[4] = picks_all[wv];
     const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
     const uint64_t wglob = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
-#ifdef SCCSUM_ROWS_RR
-    // (A/B form) 64-packet tiles dealt round robin to the end
-    const uint64_t ntiles = (n + kWave - 1) / kWave;
-    for (uint64_t t = wglob; t < ntiles; t += nwaves) {
-        const uint64_t t0 = t * kWave;
-        const uint32_t cnt = static_cast<uint32_t>(n - t0 < kWave ? n - t0 : kWave);
-#else
     // 64-packet tiles dealt round robin for as many whole rounds of the grid
     // as the batch holds (all waves sweep the buffer together, front to
     // back), then the packets left are split evenly over the waves as one
@@ -624,7 +617,6 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
         const uint64_t t0 = rr < R ? (rr * nwaves + wglob) * kWave : lo_last;
         const uint32_t cnt = rr < R ? static_cast<uint32_t>(kWave) : cnt_last;
         if (cnt == 0) break;
-#endif
         // ---- A: lane k plans packet k of the tile (coalesced metadata loads)
         const uint64_t p = t0 + lane;
         const bool mine = lane < cnt;
@@ -1323,13 +1315,8 @@ __global__ __launch_bounds__(kBlock) void fill_store_kernel(uint8_t* __restrict_
                                                             const uint32_t* __restrict__ len,
                                                             const uint32_t* __restrict__ words, uint64_t n,
                                                             uint32_t mode) {
-    const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (i0 >= n) return;
-#ifdef SCCSUM_FILL_REV
-    const uint64_t i = n - 1 - i0;  // (A/B) last-read frames first
-#else
-    const uint64_t i = i0;
-#endif
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= n) return;
     const uint64_t o = off[i];
     const uint32_t L = len[i];
     if (o > bytes_len || L > bytes_len - o || L < 20u) return;

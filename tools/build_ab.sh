@@ -1,8 +1,8 @@
 #!/bin/bash
 # Build A/B variants of libsccsum.so (same sources and ABI, one -D switch each)
 # into seastar_amd/lib/ab/, for tools/gpu_session.sh's lib:PATH step, e.g.
-#   bash tools/build_ab.sh fill2=SCCSUM_FILL_TWO_PASS rowsrr=SCCSUM_ROWS_RR
-# builds seastar_amd/lib/ab/libsccsum_fill2.so and libsccsum_rowsrr.so.
+#   bash tools/build_ab.sh nt0=SCCSUM_SOME_SWITCH b=SWITCH_A,SWITCH_B=2
+# builds seastar_amd/lib/ab/libsccsum_nt0.so (-DSCCSUM_SOME_SWITCH) and libsccsum_b.so.
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p seastar_amd/lib/ab
