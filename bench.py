@@ -85,6 +85,8 @@ def parse():
                          "jumbo packets as 5-fragment mbuf chains in HBM (checksummer::sum(const packet&))")
     ap.add_argument("--tile-bytes", type=int, default=None, help="A/B: flat-kernel tile target (sccsum_diag.h)")
     ap.add_argument("--variant", type=int, default=None, help="A/B: kernel form (sccsum_set_kernel_variant)")
+    ap.add_argument("--out-policy", type=int, default=None,
+                    help="A/B: cache policy of the flat kernel's result stores (sccsum_set_out_policy)")
     ap.add_argument("--run-align", type=int, default=None, help="A/B: run-start alignment in units (sccsum_set_run_align)")
     ap.add_argument("--sync", default="auto", choices=["auto", "spin", "yield"],
                     help="how the host thread waits on the device (hipSetDeviceFlags schedule)")
@@ -1022,6 +1024,8 @@ def main():
             native.check(native.load().sccsum_set_tile_bytes(args.tile_bytes), "sccsum_set_tile_bytes")
         if args.variant is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_kernel_variant(args.variant), "sccsum_set_kernel_variant")
+        if args.out_policy is not None:  # A/B only (sccsum_diag.h)
+            native.check(native.load().sccsum_set_out_policy(args.out_policy), "sccsum_set_out_policy")
         if args.run_align is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_run_align(args.run_align), "sccsum_set_run_align")
         {"udp1500": run_udp1500, "tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e, "fill": run_fill,
