@@ -67,7 +67,9 @@ def sparse_kernel(args, ipv4: bool, max_len: int) -> str:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # 200 timed steps (~0.1 s of cfg 2): the timed region's fixed cost (first launch, closing
+    # sync, ~100 us) is then 0.1 % of it instead of 1 % (profiles/r02_ab_steps.log)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--packets", type=int, default=1 << 20, help="frames per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (rank 0, N=1)")
