@@ -99,19 +99,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
            static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 48));
 }
 
-// Maximum of v over the wave (row DPP steps, then the four row results).
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-    v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xF, 0xF, false)));
-    v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4E, 0xF, 0xF, false)));
-    v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x124, 0xF, 0xF, false)));
-    v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x128, 0xF, 0xF, false)));
-    const uint32_t a = max(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 0)),
-                           static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 16)));
-    const uint32_t b = max(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 32)),
-                           static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 48)));
-    return max(a, b);
-}
-
 __device__ __forceinline__ u32x4 load_unit(const uint8_t* p) {
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
@@ -823,7 +810,7 @@ struct Queues {
 // (waves_per_eu: the U = 8 forms fit 168 VGPRs and keep 3 waves per SIMD —
 // the in-place form with a chunk in flight needed 172 without the bound; the
 // U = 16 forms are held to 2 by their LDS anyway)
-template <int U, bool IPV4, bool FILL, bool PIPE, bool VIRT = false>
+template <int U, bool IPV4, bool FILL, bool PIPE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 ? 2 : 3))) void csum_flat_kernel(const Queues Q, uint32_t B, uint32_t* __restrict__ heads,
                                                           uint32_t* __restrict__ done, uint32_t ticket,
                                                           uint32_t flags, const RssParams rss) {
@@ -941,9 +928,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
     // kGapUnits past j-1's end and ends no earlier (so a run's extent is
     // [fu of its first, lu of its last])
     struct Tile {
-        uint64_t base, o, a0, fu, lu, starts, streamed, magic;
-        uint32_t q, cnt, L, sd, head, nunits, M, arel;
-        bool mine, range_bad, short_frame, huge, fast, part, virt;
+        uint64_t base, o, a0, fu, lu, starts, streamed;
+        uint32_t q, cnt, L, sd, head, nunits;
+        bool mine, range_bad, short_frame, huge, fast, part;
     };
     auto derive = [&](uint64_t tt, uint64_t o_, uint32_t L_, uint32_t sd_) {
         Tile c;
@@ -978,35 +965,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
         const bool joins = lane != 0 && c.part && ppart && c.fu >= pfu && c.lu >= plu && c.fu <= plu + kGapUnits;
         c.starts = __ballot(c.mine && !joins) | (c.cnt < 64 ? (1ull << c.cnt) : 0ull);
         c.streamed = c.starts & __ballot(c.part);  // runs that stream bytes start at a lane that takes part
-        c.virt = false;
-        c.M = 0;
-        c.magic = 0;
-        c.arel = 0;
-        if constexpr (VIRT) {
-            // Sparse layouts (variant 3): a tile whose packets do not run
-            // forward densely (mbuf slots: 1500 B every 2304) streams as ONE
-            // virtual extent, packet k's units at [k M, k M + nunits_k) with M
-            // the tile's longest packet in units: lane l's unit x of a chunk
-            // loads packet x / M (a multiply by the tile's reciprocal), unit
-            // x % M, from that packet's own address (a bpermute), so each
-            // 1 KiB load row covers packet bytes only and the wave keeps U
-            // rows in flight over several packets.  Needs the tile's packets
-            // within 4 GiB of the batch start (32-bit buffer offsets) and M <=
-            // 1023 units (the reciprocal is exact below 2^16 virtual units).
-            const uint64_t base_u = reinterpret_cast<uint64_t>(Q.bytes[c.q]);
-            const uint32_t m = wave_max(c.part ? c.nunits : 0u);
-            const uint64_t rel = c.a0 - base_u;
-            const bool far = c.part && rel + 16ull * c.nunits > 0xFFFFFFF0ull;
-            const uint64_t inner = c.cnt >= 64 ? ~0ull : ((1ull << c.cnt) - 1ull);
-            if (m >= 1u && m <= 1023u && __ballot(far) == 0 && __popcll(c.starts & inner) > 1) {
-                c.virt = true;
-                c.M = m;
-                c.magic = ((1ull << 32) + m - 1u) / m;
-                c.arel = c.part ? static_cast<uint32_t>(rel) : 0u;
-                c.starts = 1ull | (c.cnt < 64 ? (1ull << c.cnt) : 0ull);
-                c.streamed = __ballot(c.part) ? 1ull : 0ull;
-            }
-        }
         return c;
     };
     // Run [k, k2) of tile c: its extent's first unit F and unit count.
@@ -1059,55 +1017,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
         uint32_t pst = 0, pend = 0;
         uint64_t rem = cur.streamed;
         while (rem != 0) {
-            Run rn{};
-            const bool virt = VIRT && cur.virt;
-            if (virt) {  // the tile's one virtual run: packet k's units from k M
-                rn.k = 0;
-                rn.k2 = cur.cnt;
-                rn.ext = cur.cnt * cur.M;
-                rn.F = reinterpret_cast<uint64_t>(Q.bytes[cur.q]) >> 4;
-            } else {
-                rn = run_of(cur, static_cast<uint32_t>(__builtin_ctzll(rem)));
-            }
+            const Run rn = run_of(cur, static_cast<uint32_t>(__builtin_ctzll(rem)));
             rem &= rem - 1;
             const uint32_t k = rn.k, k2 = rn.k2, ext = rn.ext;
             const uint64_t F = rn.F;
-            // (virtual: a descriptor over the batch, lanes address their packets by 32-bit offsets)
-            const auto r = virt ? rsrc(Q.bytes[cur.q], static_cast<uint32_t>(
-                                      Q.bytes_len[cur.q] + 15u > 0xFFFFFFF0ull ? 0xFFFFFFF0ull
-                                                                              : (Q.bytes_len[cur.q] + 15u) & ~15ull))
-                                : run_rsrc(rn);
+            const auto r = run_rsrc(rn);
             const bool cap = lane >= k && lane < k2;
-            const int vf = static_cast<int>(lane * cur.M);
-            const int rf = !cap ? -0x40000000 : (virt ? vf : static_cast<int>(static_cast<uint32_t>(cur.fu - F)));
-            const int rl = !cap ? -0x40000000
-                                : (virt ? vf + static_cast<int>(cur.nunits) - 1
-                                        : static_cast<int>(static_cast<uint32_t>(cur.lu - F)));
-            // a virtual chunk's loads: unit x of the extent is unit x % M of
-            // packet x / M (x < 2^16 + 2^10, M <= 1023: the reciprocal is exact)
-            auto vload = [&](uint32_t g, auto& v) {
-                constexpr int R = std::extent<std::remove_reference_t<decltype(v)>>::value;
-#pragma unroll
-                for (int u = 0; u < R; ++u) {
-                    const uint32_t x = g + lane + 64u * u;
-                    const uint32_t kk = static_cast<uint32_t>((static_cast<uint64_t>(x) * cur.magic) >> 32);
-                    const uint32_t cc = x - kk * cur.M;
-                    const uint32_t ak = static_cast<uint32_t>(__shfl(static_cast<int>(cur.arel), static_cast<int>(kk & 63u)));
-                    const uint32_t nk = static_cast<uint32_t>(__shfl(static_cast<int>(cur.nunits), static_cast<int>(kk & 63u)));
-                    v[u] = (kk < cur.cnt && cc < nk)
-                               ? __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(ak + 16u * cc), 0, kNT)
-                               : u32x4{0, 0, 0, 0};
-                }
-            };
-            auto ld = [&](uint32_t g, auto& v) {
-                if constexpr (VIRT) {
-                    if (virt) {
-                        vload(g, v);
-                        return;
-                    }
-                }
-                load(r, g, v);
-            };
+            const int rf = cap ? static_cast<int>(static_cast<uint32_t>(cur.fu - F)) : -0x40000000;
+            const int rl = cap ? static_cast<int>(static_cast<uint32_t>(cur.lu - F)) : -0x40000000;
             uint32_t carry = 0;
             // one chunk = R <= U rows of 64 units: unit sums, scanned, parked
             // in LDS with the units; packet lanes pick up what falls in it
@@ -1160,19 +1077,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
                     const uint32_t left = ext - g;
                     if (!short_chunks || left > C / 2) {
                         u32x4 v[U];
-                        ld(g, v);
+                        load(r, g, v);
                         chunk(g, v);
                     } else if (left > C / 4) {
                         u32x4 v[U / 2];
-                        ld(g, v);
+                        load(r, g, v);
                         chunk(g, v);
                     } else if (U < 8 || left > C / 8) {
                         u32x4 v[U / 4];
-                        ld(g, v);
+                        load(r, g, v);
                         chunk(g, v);
                     } else {
                         u32x4 v[U >= 8 ? U / 8 : 1];
-                        ld(g, v);
+                        load(r, g, v);
                         chunk(g, v);
                     }
                 }
@@ -1817,15 +1734,11 @@ void launch_rows(uint32_t max_len, hipStream_t s, const uint8_t* b, uint64_t byt
 // in place; spans never do.
 template <bool IPV4>
 void launch_flat_variant(int variant, hipStream_t s, Queues& Q, uint64_t n_total, uint64_t bytes_total,
-                         uint32_t flags, const RssParams& rss, uint32_t max_len) {
+                         uint32_t flags, const RssParams& rss) {
     auto go = [&](auto kern) { launch_flat(kern, s, Q, n_total, bytes_total, flags, rss); };
     constexpr bool F = IPV4;
     const bool fill = IPV4 && (flags & kFillFlags);
     switch (variant) {
-        case 3:  // sparse layouts as virtual runs: tiles sized by the packets' bytes, not the gaps'
-            if (max_len) bytes_total = n_total * max_len;
-            launch_flat(csum_flat_kernel<16, IPV4, false, false, true>, s, Q, n_total, bytes_total, flags, rss);
-            break;
         case 14: fill ? go(csum_flat_kernel<8, IPV4, F, false>) : go(csum_flat_kernel<8, IPV4, false, false>); break;
         case 15: fill ? go(csum_flat_kernel<8, IPV4, F, true>) : go(csum_flat_kernel<8, IPV4, false, true>); break;
         default: fill ? go(csum_flat_kernel<16, IPV4, F, false>) : go(csum_flat_kernel<16, IPV4, false, false>); break;
@@ -1881,7 +1794,7 @@ int pick_variant(uint64_t n_total, uint64_t bytes_total, uint32_t flags, uint32_
     const bool fill = (flags & kFillFlags) != 0;
     const bool sparse = max_len != 0 && n_total != 0 && bytes_total / n_total >= uint64_t(max_len) + 64u;
     if (variant == 0 && sparse && !fill) return 2;
-    if (variant == 0 || ((variant == 1 || variant == 2 || variant == 3) && fill)) variant = dflt;  // in-place: flat only
+    if (variant == 0 || ((variant == 1 || variant == 2) && fill)) variant = dflt;  // in-place write-back: flat only
     return variant;
 }
 
@@ -1916,7 +1829,7 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
         Q.out[0] = d_out;
         Q.status[0] = d_status;
         Q.n[0] = n;
-        launch_flat_variant<IPV4>(variant, s, Q, n, bytes_len, flags, rss, max_len);
+        launch_flat_variant<IPV4>(variant, s, Q, n, bytes_len, flags, rss);
     }
     return static_cast<int>(hipGetLastError());
 }
@@ -1966,7 +1879,7 @@ int launch_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
         Q.status[q] = x.d_status;
         Q.n[q] = x.n;
     }
-    launch_flat_variant<IPV4>(variant, s, Q, n_total, bytes_total, 0, kNoRss, max_len);
+    launch_flat_variant<IPV4>(variant, s, Q, n_total, bytes_total, 0, kNoRss);
     return static_cast<int>(hipGetLastError());
 }
 
@@ -2407,9 +2320,7 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
 }
 
 int sccsum_set_kernel_variant(int variant) {
-    if (!(variant == 0 || variant == 1 || variant == 2 || variant == 3 || (variant >= 14 && variant <= 16))) {
-        return SCCSUM_EINVAL;
-    }
+    if (!(variant == 0 || variant == 1 || variant == 2 || (variant >= 14 && variant <= 16))) return SCCSUM_EINVAL;
     sccsum::t_knobs.variant = variant;
     return SCCSUM_OK;
 }

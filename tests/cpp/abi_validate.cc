@@ -112,7 +112,7 @@ static void checks() {
     EXPECT(sccsum_pipeline_create(0, 1 << 20, 1024, 2, nullptr) == SCCSUM_EINVAL);
     EXPECT(sccsum_host_alloc(nullptr, 64) == SCCSUM_EINVAL);
     // diagnostics: thread-local knobs validate their ranges
-    EXPECT(sccsum_set_kernel_variant(4) == SCCSUM_EINVAL && sccsum_set_kernel_variant(5) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_kernel_variant(3) == SCCSUM_EINVAL && sccsum_set_kernel_variant(5) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_kernel_variant(20) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_kernel_variant(10) == SCCSUM_EINVAL && sccsum_set_kernel_variant(17) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_kernel_variant(16) == SCCSUM_OK && sccsum_set_kernel_variant(0) == SCCSUM_OK);

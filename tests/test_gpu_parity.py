@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.fixture(params=[1, 2, 3, 14, 15, 16], ids=["simple", "rows", "virt", "flat8", "flat8_pipe", "flat16"],
+@pytest.fixture(params=[1, 2, 14, 15, 16], ids=["simple", "rows", "flat8", "flat8_pipe", "flat16"],
                 autouse=True)
 def kernel_variant(request, dev):
     """Every parity test runs against both kernel families."""
