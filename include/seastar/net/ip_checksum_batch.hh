@@ -98,9 +98,9 @@ public:
 
     // Generate IPv4 header and/or TCP/UDP checksums (ICMP echo replies with
     // SCCSUM_FILL_ICMP_ECHO) and store them into the frames (mode:
-    // SCCSUM_FILL_*; d_status may be null; d_out2 may be null except with
-    // SCCSUM_FILL_L4 / SCCSUM_FILL_ICMP_ECHO, whose two passes hand the values
-    // over in it).  IP fragments get their IPv4 header checksum only.
+    // SCCSUM_FILL_*; d_status and d_out2 may be null: without d_out2 the
+    // two passes of SCCSUM_FILL_L4 / SCCSUM_FILL_ICMP_ECHO hand the values over
+    // in stream-ordered scratch).  IP fragments get their IPv4 header checksum only.
     void ipv4_fill(const device_packet_batch& b, uint32_t mode, uint16_t* d_out2, uint8_t* d_status,
                    void* stream) const {
         check(sccsum_ipv4_fill(const_cast<void*>(b.bytes), b.bytes_len, b.off, b.len, d_out2, d_status, b.n,
