@@ -44,7 +44,9 @@
  *     device's null stream), one kernel each (two for in-place fill and
  *     fragment lists).  No allocation, no memset and no host synchronisation
  *     on the launch path — sccsum_init allocates the device's pool of tile
- *     counters once — so the calls are safe inside hipStreamBeginCapture
+ *     counters once; the one exception is sccsum_ipv4_fill with a NULL
+ *     d_out2, whose scratch is a stream-ordered hipMallocAsync / hipFreeAsync
+ *     pair on `stream` — so the calls are safe inside hipStreamBeginCapture
  *     (global or relaxed mode) and never stall another stream.  Any number
  *     of launches may be in flight, on any streams: a launch takes a counter
  *     slot no unfinished launch holds, and the kernel itself reports when it
