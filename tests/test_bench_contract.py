@@ -1,0 +1,57 @@
+"""bench.py's JSON line carries every field the driver contract names
+(metric, value, unit, n_gpus, steps, warmup, ms_per_step, higher_is_better,
+scaling, vs_baseline, dtype, data, config), plus `roofline` (bound, achieved,
+peak, unit, frac, traffic) and `cpu_baseline` (value, unit, cores, kind,
+sample) — checked on the CPU with the bench's own builders, a small frame
+sample for the oracle leg and synthetic launch timings."""
+import argparse
+import importlib.util
+import io
+import json
+import os
+import sys
+from contextlib import redirect_stdout
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(REPO, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["bench_under_test"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_bench_line_has_the_contract_fields():
+    bench = _bench()
+    bench._imports()  # bench imports numpy / torch / the package lazily (the launcher parent never does)
+    frame = bench.FRAME
+    n = 512
+    rng = np.random.default_rng(5)
+    data = torch.from_numpy(rng.integers(0, 256, size=n * frame, dtype=np.uint8))
+    cpu = bench.cpu_baseline(SimpleNamespace(n=n, data=data), 0.2)
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in cpu, k
+    assert cpu["kind"] in ("port", "reference") and cpu["value"] > 0 and cpu["cores"] >= 1
+    args = argparse.Namespace(pmc=None, steps=200, warmup=5)
+    alg = 3_176_136_704
+    roof = bench.roofline(alg, 460e-6, "udp1500", "csum_flat_kernel<16, true, false, false>",
+                          {"kernel": "csum_flat_kernel<16, true, false, false>", "skip": 9, "count": 200}, args)
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in roof, k
+    assert roof["bound"] == "hbm" and roof["unit"] == "GB/s" and roof["peak"] == bench.HBM_PEAK_GBPS
+    assert abs(roof["frac"] - alg / 460e-6 / 1e9 / bench.HBM_PEAK_GBPS) < 1e-3
+    buf = io.StringIO()
+    with redirect_stdout(buf):
+        bench.emit("GiB/s test", 6300.0, "GiB/s", args, 1, 0.092, "u8", {"workload": "cfg2"}, roof, cpu)
+    line = json.loads(buf.getvalue().strip())
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert line["n_gpus"] == 1 and line["steps"] == 200 and line["scaling"] == "weak"
+    assert line["config"]["workload"] == "cfg2" and line["data"] == "synthetic"
