@@ -1,4 +1,4 @@
-"""Per-kernel SQ counter summary from tools/sq_profile.sh output (means over dispatches)."""
+"""Per-kernel SQ counter summary of rocprofv3 SQ_* / GRBM_* passes (means over dispatches; round 1-2, the sq_profile.sh runner is in git history)."""
 import collections
 import csv
 import re
