@@ -87,6 +87,8 @@ def parse():
                          "jumbo packets as 5-fragment mbuf chains in HBM (checksummer::sum(const packet&))")
     ap.add_argument("--tile-bytes", type=int, default=None, help="A/B: flat-kernel tile target (sccsum_diag.h)")
     ap.add_argument("--variant", type=int, default=None, help="A/B: kernel form (sccsum_set_kernel_variant)")
+    ap.add_argument("--blocks-per-cu", type=int, default=None,
+                    help="A/B: grid cap in workgroups per CU (sccsum_set_blocks_per_cu)")
     ap.add_argument("--out-policy", type=int, default=None,
                     help="A/B: cache policy of the flat kernel's result stores (sccsum_set_out_policy)")
     ap.add_argument("--run-align", type=int, default=None, help="A/B: run-start alignment in units (sccsum_set_run_align)")
@@ -1026,6 +1028,8 @@ def main():
             native.check(native.load().sccsum_set_tile_bytes(args.tile_bytes), "sccsum_set_tile_bytes")
         if args.variant is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_kernel_variant(args.variant), "sccsum_set_kernel_variant")
+        if args.blocks_per_cu is not None:  # A/B only (sccsum_diag.h)
+            native.check(native.load().sccsum_set_blocks_per_cu(args.blocks_per_cu), "sccsum_set_blocks_per_cu")
         if args.out_policy is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_out_policy(args.out_policy), "sccsum_set_out_policy")
         if args.run_align is not None:  # A/B only (sccsum_diag.h)
