@@ -111,6 +111,14 @@ def parse():
     ap.add_argument("--dry-run", action="store_true",
                     help="multi-rank plumbing only: launch, rendezvous, barrier, max-over-ranks, one line; "
                          "no device call (the CPU test of the launcher)")
+    ap.add_argument("--share-devices", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks then share devices: local %% ndev); "
+                         "refused without it")
+    ap.add_argument("--numa", default="bind", choices=["bind", "preferred", "none", "off"],
+                    help="rank locality, as Seastar pins shards and binds their memory (reactor.cc:4163, "
+                         "memory.cc:1898-1951): every thread onto the GPU's NUMA node's CPUs, and the host "
+                         "memory policy MPOL_BIND (bind) / MPOL_PREFERRED (preferred) to that node, or CPUs only "
+                         "(none); off = leave the rank where the OS put it")
     return ap.parse_args()
 
 
@@ -189,24 +197,61 @@ def set_sync_mode(dev: int, mode: str) -> None:
             raise RuntimeError(f"{what} failed ({rc})")
 
 
-def dist_setup(dry_run=False):
+NUMA = {}  # this rank's locality (seastar_amd.numa.bind), reported in per_rank
+
+
+def place_rank(bdf, mode: str) -> dict:
+    """Bind this rank to its GPU's NUMA node (every thread onto the node's
+    schedulable CPUs; host memory policy per --numa) before any host buffer
+    of the run is allocated: the pinned mbuf pool, burst staging and the CPU
+    baseline's sample then sit on the GPU's node, as Seastar binds a shard's
+    memory to its core's node (src/core/memory.cc:1898-1951)."""
+    from seastar_amd import numa
+
+    sysfs = os.environ.get("SCCSUM_SYSFS", numa.SYSFS)  # a fake tree in the launcher test
+    p = numa.plan(bdf, sysfs=sysfs)
+    if mode == "off":
+        return {"numa_node": p["numa_node"], "cpus": numa.format_cpulist(sorted(os.sched_getaffinity(0))),
+                "ncpus": len(os.sched_getaffinity(0)), "affinity": "unchanged (--numa off)", "mempolicy": "default",
+                "reason": "--numa off"}
+    return numa.bind(p, mem="none" if mode == "none" else mode)
+
+
+def check_devices(world_local: int, ndev: int, share: bool) -> None:
+    """More ranks on this node than visible GPUs would silently stack ranks on
+    one device (local % ndev): refuse unless --share-devices asks for it."""
+    if world_local > ndev and not share:
+        sys.exit(f"bench.py: {world_local} ranks on this node but {ndev} visible GPU(s); "
+                 "pass --share-devices to let ranks share devices")
+
+
+def dist_setup(dry_run=False, args=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    share = bool(args and args.share_devices)
+    numa_mode = args.numa if args else "bind"
     if world > 1 and os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
         # one node (the driver's torchrun uses --master-addr 127.0.0.1): keep gloo's control traffic on
         # loopback rather than on whatever interface the box's hostname resolves to
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
     if dry_run:
+        # the launcher test's stand-ins for the GPUs: PCI ids (one per local rank) and device count
+        bdfs = [b for b in os.environ.get("SCCSUM_DRY_RUN_BDFS", "").split(",") if b]
+        check_devices(local_world, int(os.environ.get("SCCSUM_DRY_RUN_NDEV", str(max(len(bdfs), local_world)))), share)
+        NUMA.update(place_rank(bdfs[local % len(bdfs)] if bdfs else None, numa_mode))
         if world > 1:
             import torch.distributed as dist
 
             dist.init_process_group("gloo")
         return world, rank, local
     ndev = torch.cuda.device_count()
+    check_devices(local_world, ndev, share)
     dev = local % max(ndev, 1)
     set_sync_mode(dev, SYNC_MODE)
     torch.cuda.set_device(dev)
+    NUMA.update(place_rank(device_id(torch.device("cuda", dev))["pci_bus_id"], numa_mode))
     if world > 1:
         import torch.distributed as dist
 
@@ -258,8 +303,18 @@ def cpu_model() -> str:
 
 def cpu_baseline(tx, budget_s: float):
     """Oracle (C restatement of src/net/ip_checksum.cc, -O2) on a bounded
-    sample of the same frames, on this host's cores (cpu_threads), plus the
-    1-thread rate."""
+    sample of the same frames, shard-per-core as Seastar runs it (SURVEY
+    §8(d)): one thread per PHYSICAL core, each pinned to its core (smp::pin,
+    src/core/reactor.cc:4163), on the rank's CPUs — the GPU's NUMA node after
+    place_rank — up to the box's CPU share (cpu_threads: OMP_NUM_THREADS).
+    The cores are taken round robin over the node's L3 domains (CCDs): a CCD's
+    link to memory caps what its cores stream together, so 16 threads packed
+    on 2 CCDs measure the links, not the cores.  Also measured: 1 thread, a
+    1/2/4/8 curve, and one CCD fully loaded (its link's ceiling), from which
+    the all-cores figure is projected.  The sample is allocated after
+    place_rank, so it sits on the GPU's node too."""
+    from seastar_amd import numa
+
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # cpu_baseline leg only
 
@@ -267,13 +322,19 @@ def cpu_baseline(tx, budget_s: float):
     host = tx.data[: n_sample * FRAME].cpu().numpy()
     off = np.arange(n_sample, dtype=np.uint64) * FRAME
     length = np.full(n_sample, FRAME, dtype=np.uint32)
-    threads, why = cpu_threads()
+    share, why = cpu_threads()
+    cores = numa.physical_cores(sorted(os.sched_getaffinity(0)))  # one hardware thread per physical core
+    spread = numa.spread_over_l3(cores)
+    pinned = spread[:share]
+    threads = len(pinned)
+    doms = numa.l3_domains(cores)
+    one_ccd = max(doms.values(), key=len)[:share] if doms else pinned
 
-    def rate(nt, seconds):
-        oracle.batch_ipv4(host, off, length, nthreads=nt)  # warm
+    def rate(cpus, seconds):
+        oracle.batch_ipv4(host, off, length, cpus=cpus)  # warm
         reps, t0 = 0, time.perf_counter()
         while True:
-            oracle.batch_ipv4(host, off, length, nthreads=nt)
+            oracle.batch_ipv4(host, off, length, cpus=cpus)
             reps += 1
             dt = time.perf_counter() - t0
             if dt >= seconds:
@@ -282,18 +343,43 @@ def cpu_baseline(tx, budget_s: float):
         # side; the CPU rate is bytes checksummed per second either way.
         return reps * n_sample * FRAME / dt / 2**30, reps
 
-    v1, r1 = rate(1, budget_s / 2)
-    vn, rn = rate(threads, budget_s / 2)
+    v1, r1 = rate(pinned[:1], budget_s * 0.25)
+    curve = {}
+    for k in (2, 4, 8):
+        if k < threads:
+            curve[str(k)] = round(rate(pinned[:k], budget_s * 0.07)[0], 3)
+    vccd = rate(one_ccd, budget_s * 0.1)[0] if len(one_ccd) > 1 else None
+    vn, rn = rate(pinned, budget_s * 0.4)
+    host_cores, host_ccds = numa.host_physical_cores(), numa.host_l3_domains()
+    node = NUMA.get("numa_node", -1)
+    per_core = vn / max(threads, 1)
+    per_ccd = vccd if vccd else per_core * max(len(one_ccd), 1)
+    cands = [per_core * host_cores] + ([per_ccd * host_ccds] if host_ccds else [])
+    all_cores = min(cands) if host_cores else None
     return {
         "value": round(vn, 3),
         "unit": "GiB/s",
         "cores": threads,
-        "cores_source": why,
+        "cores_source": f"one thread per physical core, pinned, spread over the L3 domains of the rank's CPUs "
+                        f"({NUMA.get('cpus')}, NUMA node {node}), up to the box's CPU share: {why}",
         "kind": "port",
-        "sample": f"{n_sample} x {FRAME} B IPv4/UDP frames ({n_sample * FRAME / 1e6:.0f} MB) from the same batch, "
-                  f"IPv4 header + UDP checksum per frame, {rn} passes on {threads} threads "
-                  f"(~{budget_s / 2:.0f} s) and {r1} passes on 1 thread",
+        "sample": f"{n_sample} x {FRAME} B IPv4/UDP frames ({n_sample * FRAME / 1e6:.0f} MB, allocated on the rank's "
+                  f"node) from the same batch, IPv4 header + UDP checksum per frame, {rn} passes on {threads} pinned "
+                  f"threads and {r1} passes on 1",
         "value_1core": round(v1, 3),
+        "scaling_GiBps": {"1": round(v1, 3), **curve, str(threads): round(vn, 3)},
+        "pinned_cpus": numa.format_cpulist(pinned),
+        "one_l3_domain": {"cpus": numa.format_cpulist(one_ccd), "GiBps": round(vccd, 3) if vccd else None},
+        "physical_cores": {"host": host_cores, "schedulable": len(cores), "l3_domains_host": host_ccds,
+                           "node": len(numa.physical_cores(numa.node_cpus(node))) if node >= 0 else None},
+        # the whole host is not this run's to use (the box's CPU share is `share` threads): the
+        # all-cores figure is projected from the measured rates — per physical core x the host's cores,
+        # capped by one loaded L3 domain's rate x the host's domains; host DRAM bandwidth (not
+        # measured) may cap it lower still
+        "value_all_cores": round(all_cores, 3) if all_cores else None,
+        "value_all_cores_kind": (f"projected: min({per_core:.2f} GiB/s per physical core x {host_cores} cores, "
+                                 f"{per_ccd:.1f} GiB/s per loaded L3 domain x {host_ccds} domains); "
+                                 "not run on all cores, DRAM bandwidth not applied"),
         "cpu_model": cpu_model(),
     }
 
@@ -400,6 +486,8 @@ def per_rank(world, rank, dev, **fields):
     (reference analogue: independent per-shard engines, src/net/net.cc:309-341).
     Collective: every rank calls it."""
     me = {"rank": rank, "host": socket.gethostname(), **device_id(dev),
+          "numa_node": NUMA.get("numa_node"), "cpus": NUMA.get("cpus"), "affinity": NUMA.get("affinity"),
+          "mempolicy": NUMA.get("mempolicy"),
           **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in fields.items()}}
     if world == 1:
         return [me]
@@ -441,6 +529,11 @@ def emit(metric, value, unit, args, world, wall, dtype, config, roof=None, cpu=N
          "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
          "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
          "config": dict(config, host_wait=SYNC_MODE), "roofline": roof, "cpu_baseline": cpu}
+    # which library ran, and its ABI (an A/B line against an older build, SCCSUM_LIB + SCCSUM_ABI_ANY, may
+    # have other semantics: ADVICE r03)
+    lib = native.load()
+    d["library"] = {"path": os.path.relpath(os.environ.get("SCCSUM_LIB", native.LIB_PATH), REPO),
+                    "abi_version": int(lib.sccsum_abi_version())}
     if extra:
         d.update(extra)
     print(json.dumps(d), flush=True)
@@ -523,7 +616,7 @@ def run_udp1500(args, world, rank, dev):
     # sanity: every uncorrupted rx frame verifies, every corrupted one fails; the tx outputs match the generate pass
     for st_rx in sts:
         n_fail = int(((st_rx & 2) == 0).sum())
-        assert n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
+        assert args.no_check or n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
     sel = LAUNCHES.select(kern, per_step * args.steps)
     wall, step_s = timed(step, args.steps, 0, world, streams)
     LAUNCHES.add(kern, per_step * args.steps)
@@ -570,7 +663,7 @@ def run_tcp64k(args, world, rank, dev):
     kern = flat_kernel(False, False, n, b.bytes_len)
     LAUNCHES.add(kern, 2)
     torch.cuda.synchronize()
-    assert int((st != 1).sum()) == 0, "tcp64k verify failed"
+    assert args.no_check or int((st != 1).sum()) == 0, "tcp64k verify failed"
     stream = torch.cuda.current_stream()
     LAUNCHES.add(kern, args.warmup)
     sel = LAUNCHES.select(kern, args.steps)
@@ -975,21 +1068,57 @@ def run_e2e(args, world, rank, dev):
             times.append(max_over_ranks(own[-1], world))
         pl.close()
         t = float(np.median(times))  # median over runs of the slowest rank's time
-        pcie = n * (pipeline.MBUF_SLOT if gather == native.GATHER_NONE else FRAME) + n * (12 + 4)
+        h2d, d2h = e2e_pcie_bytes(n, gather)
         res[name] = {"GiBps_packet_bytes": round(n * FRAME / t / 2**30, 2), "ms_per_batch": round(t * 1e3, 2),
-                     "pcie_GBps_h2d_plus_d2h": round(pcie / t / 1e9, 2)}
+                     "pcie_GBps_h2d_plus_d2h": round((h2d + d2h) / t / 1e9, 2)}
         to = float(np.median(own))
-        own_rates[name] = {"GiBps_packet_bytes": round(n * FRAME / to / 2**30, 2),
-                           "pcie_GBps_h2d_plus_d2h": round(pcie / to / 1e9, 2)}
-    ranks = per_rank(world, rank, dev, variants=own_rates)
+        own_rates[name] = {"GiBps_packet_bytes": round(n * FRAME / to / 2**30, 2), "ms_per_batch": round(to * 1e3, 2),
+                           "h2d_GBps": round(h2d / to / 1e9, 2), "d2h_GBps": round(d2h / to / 1e9, 3)}
+    from seastar_amd import numa
+
+    # where this rank's pinned pool landed (move_pages query; place_rank bound the policy to the GPU's node)
+    pages = {str(k): v for k, v in numa.page_nodes(pool.ctypes.data, pool.nbytes, 512).items()}
+    ranks = per_rank(world, rank, dev, variants=own_rates, pool_pages_by_node=pages)
     if rank == 0:
-        best = max(res.values(), key=lambda r: r["GiBps_packet_bytes"])
+        best_name = max(res, key=lambda k: res[k]["GiBps_packet_bytes"])
+        best = res[best_name]
         emit("GiB/s Internet checksum incl. PCIe: pinned mbuf-shaped host buffers -> HBM -> host (cfg 5)",
              world * best["GiBps_packet_bytes"], "GiB/s", args, world, best["ms_per_batch"] / 1e3 * args.steps, "u8",
              {"workload": "cfg5: 1,048,576 x 1500 B IPv4/UDP frames in 2304-B mbuf slots (pinned), "
                           "H2D + kernel + D2H of 4 B/frame (or the kernel reading the slots in place), 3-deep "
-                          "pipeline, 64Ki-frame chunks; value = the best variant",
-              "parallelism": f"{world} independent shards"}, extra={"variants": res, "per_rank": ranks})
+                          "pipeline, 64Ki-frame chunks; value = the best variant, all ranks' bytes over the "
+                          "slowest rank's median time",
+              "parallelism": f"{world} independent shards"},
+             extra={"variants": res, "per_rank": ranks, "best_variant": best_name,
+                    "ranks_summary": e2e_ranks_summary(ranks, best_name)})
+
+
+def e2e_pcie_bytes(n: int, gather: int) -> tuple[int, int]:
+    """Bytes crossing PCIe per cfg 5 batch, (host -> device, device -> host):
+    the slots as they lie (A) or only the packet bytes (B, C, D), plus 12 B of
+    offset + length per frame; back, the 4 B of checksums per frame."""
+    from seastar_amd import pipeline
+
+    per = pipeline.MBUF_SLOT if gather == native.GATHER_NONE else FRAME
+    return n * (per + META_BYTES), n * 4
+
+
+def e2e_ranks_summary(ranks: list, variant: str) -> dict:
+    """cfg 5 across ranks for one variant: the sum of the ranks' own rates,
+    the slowest rank (by name: rank, device, PCI id, NUMA node) and the
+    per-rank H2D / D2H rates — at 8 GPUs the ranks share host DRAM and PCIe
+    root complexes, so one slow link or a pool on the far node shows here."""
+    rows = [(r["rank"], r["variants"][variant]) for r in ranks]
+    slow_rank, slow = min(rows, key=lambda x: x[1]["GiBps_packet_bytes"])
+    sr = next(r for r in ranks if r["rank"] == slow_rank)
+    return {"variant": variant,
+            "sum_over_ranks_GiBps": round(sum(v["GiBps_packet_bytes"] for _, v in rows), 2),
+            "sum_h2d_GBps": round(sum(v["h2d_GBps"] for _, v in rows), 2),
+            "slowest_rank": {"rank": slow_rank, "device": sr.get("device"), "pci_bus_id": sr.get("pci_bus_id"),
+                             "numa_node": sr.get("numa_node"), "GiBps_packet_bytes": slow["GiBps_packet_bytes"],
+                             "h2d_GBps": slow["h2d_GBps"], "d2h_GBps": slow["d2h_GBps"]},
+            "per_rank_h2d_GBps": [v["h2d_GBps"] for _, v in rows],
+            "per_rank_d2h_GBps": [v["d2h_GBps"] for _, v in rows]}
 
 
 def run_dry(args, world, rank):
@@ -1019,7 +1148,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     _imports()
-    world, rank, local = dist_setup(args.dry_run)
+    world, rank, local = dist_setup(args.dry_run, args)
     if args.dry_run:
         run_dry(args, world, rank)
     else:

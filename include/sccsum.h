@@ -40,6 +40,16 @@
  *     its outputs are 0 and its status has SCCSUM_ST_RANGE.
  *   - d_bytes must be 16-byte aligned, d_off 8-byte aligned, d_len/d_seed/d_out2 4-byte aligned,
  *     d_out 2-byte aligned.
+ *   - `stream` must belong to the calling thread's current device (the one
+ *     the data lives on; NULL = that device's null stream).  HIP runs a kernel
+ *     on its stream's device, so each launch takes the device from the stream
+ *     (hipStreamGetDevice) and sizes its grid and takes its tile-counter slot
+ *     on that device; a stream of another device returns SCCSUM_EINVAL and
+ *     launches nothing.  A shard thread bound to device d (sccsum_init(d))
+ *     launches on streams it created while d was current.
+ *   - Errors: an entry returns its own launch's error (hipLaunchKernel's);
+ *     a pending HIP error from an earlier, unrelated call on the thread is
+ *     left pending, neither cleared nor reported as this call's.
  *   - Launches are asynchronous on `stream` (a hipStream_t; NULL = the
  *     device's null stream), one kernel each (two for in-place fill and
  *     fragment lists).  No allocation, no memset and no host synchronisation

@@ -51,6 +51,7 @@ def lib():
             "oracle_fold_seed": (ctypes.c_uint32, [cs]),
             "oracle_batch_spans": (None, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int]),
             "oracle_batch_ipv4": (None, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int]),
+            "oracle_batch_ipv4_cpus": (None, [_P, _P, _P, _P, _P, ctypes.c_uint64, _P, ctypes.c_int]),
             "oracle_batch_fragments": (None, [_P, _P, _P, _P, _P, _P, ctypes.c_uint64]),
             "oracle_batch_ipv4_fill": (None, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_uint32]),
             "oracle_toeplitz": (ctypes.c_uint32, [_P, ctypes.c_size_t, _P, ctypes.c_size_t]),
@@ -110,14 +111,21 @@ def batch_spans(buf: np.ndarray, off: np.ndarray, length: np.ndarray, seeds: np.
     return out
 
 
-def batch_ipv4(buf: np.ndarray, off: np.ndarray, length: np.ndarray, nthreads: int = 1):
-    """Returns (out2 [n,2] uint16, status [n] uint8)."""
+def batch_ipv4(buf: np.ndarray, off: np.ndarray, length: np.ndarray, nthreads: int = 1, cpus=None):
+    """Returns (out2 [n,2] uint16, status [n] uint8).  With `cpus`, one thread
+    per listed CPU, each pinned to it (nthreads is then len(cpus))."""
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
     off = np.ascontiguousarray(off, dtype=np.uint64)
     length = np.ascontiguousarray(length, dtype=np.uint32)
     out2 = np.empty((off.size, 2), dtype=np.uint16)
     status = np.empty(off.size, dtype=np.uint8)
-    lib().oracle_batch_ipv4(_addr(buf), _addr(off), _addr(length), _addr(out2), _addr(status), off.size, nthreads)
+    if cpus is not None:
+        c = np.ascontiguousarray(cpus, dtype=np.int32)
+        lib().oracle_batch_ipv4_cpus(_addr(buf), _addr(off), _addr(length), _addr(out2), _addr(status), off.size,
+                                     _addr(c), c.size)
+    else:
+        lib().oracle_batch_ipv4(_addr(buf), _addr(off), _addr(length), _addr(out2), _addr(status), off.size,
+                                nthreads)
     return out2, status
 
 

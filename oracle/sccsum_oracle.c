@@ -7,10 +7,13 @@
  * when bench.py reports it as the CPU baseline.  Compiled -O2 like Seastar's
  * release mode (configure.py:265).
  */
+#define _GNU_SOURCE /* pthread_attr_setaffinity_np (the pinned CPU baseline) */
 #include "sccsum_oracle.h"
 
 #include <arpa/inet.h>
 #include <pthread.h>
+#include <sched.h>
+#include <stdlib.h>
 #include <string.h>
 
 void oracle_init(oracle_checksummer* c) {
@@ -249,38 +252,59 @@ static void* run_job(void* arg) {
     return 0;
 }
 
-/* Shard-per-core like Seastar's smp: contiguous index ranges per thread. */
-static void run_batch(job_t base, uint64_t n, int nthreads) {
-    if (nthreads <= 1 || n < 2) {
+/* Shard-per-core like Seastar's smp: contiguous index ranges per thread.
+ * With `cpus`, thread t runs pinned to CPU cpus[t] (smp::pin,
+ * src/core/reactor.cc:4163 — one shard per core). */
+#define ORACLE_MAX_THREADS 1024
+static void run_batch(job_t base, uint64_t n, int nthreads, const int* cpus) {
+    if ((nthreads <= 1 && !cpus) || n < 2) {
         base.lo = 0;
         base.hi = n;
         run_job(&base);
         return;
     }
-    if (nthreads > 256) nthreads = 256;
-    pthread_t th[256];
-    job_t jobs[256];
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > ORACLE_MAX_THREADS) nthreads = ORACLE_MAX_THREADS;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    job_t* jobs = (job_t*)malloc(sizeof(job_t) * (size_t)nthreads);
     for (int t = 0; t < nthreads; ++t) {
         jobs[t] = base;
         jobs[t].lo = n * (uint64_t)t / (uint64_t)nthreads;
         jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)nthreads;
-        pthread_create(&th[t], 0, run_job, &jobs[t]);
+        pthread_attr_t attr;
+        pthread_attr_init(&attr);
+        if (cpus) {
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            CPU_SET(cpus[t], &set);
+            pthread_attr_setaffinity_np(&attr, sizeof(set), &set);
+        }
+        pthread_create(&th[t], &attr, run_job, &jobs[t]);
+        pthread_attr_destroy(&attr);
     }
     for (int t = 0; t < nthreads; ++t) {
         pthread_join(th[t], 0);
     }
+    free(th);
+    free(jobs);
 }
 
 void oracle_batch_spans(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                         const uint32_t* seed, uint16_t* out, uint64_t n, int nthreads) {
     job_t b = {0, bytes, off, len, seed, out, 0, 0, 0};
-    run_batch(b, n, nthreads);
+    run_batch(b, n, nthreads, 0);
 }
 
 void oracle_batch_ipv4(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                        uint16_t* out2, uint8_t* status, uint64_t n, int nthreads) {
     job_t b = {1, bytes, off, len, 0, out2, status, 0, 0};
-    run_batch(b, n, nthreads);
+    run_batch(b, n, nthreads, 0);
+}
+
+void oracle_batch_ipv4_cpus(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+                            uint16_t* out2, uint8_t* status, uint64_t n, const int* cpus, int nthreads) {
+    job_t b = {1, bytes, off, len, 0, out2, status, 0, 0};
+    run_batch(b, n, nthreads, cpus);
 }
 
 /* src/net/ip_checksum.cc:64-68 applied per packet of a fragment-list batch */

@@ -78,6 +78,10 @@ void oracle_batch_spans(const uint8_t* bytes, const uint64_t* off, const uint32_
  *   status may be NULL. */
 void oracle_batch_ipv4(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                        uint16_t* out2, uint8_t* status, uint64_t n, int nthreads);
+/* the same, thread t pinned to CPU cpus[t] (the CPU baseline's one thread per
+ * physical core, smp::pin at src/core/reactor.cc:4163) */
+void oracle_batch_ipv4_cpus(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+                            uint16_t* out2, uint8_t* status, uint64_t n, const int* cpus, int nthreads);
 
 /* Fragment lists: packet i = fragments pkt_first[i] .. pkt_first[i+1]-1, each
  * bytes[frag_off[j] .. +frag_len[j]); seeded like oracle_batch_spans, then

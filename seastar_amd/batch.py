@@ -98,14 +98,21 @@ def _stream(stream) -> int | None:
 
 
 def _scratch(numel: int, device, stream, dtype=torch.uint8) -> torch.Tensor:
-    """A buffer the library allocates for kernels queued on `stream`
-    (scratch, or an output the caller did not pass): the caching allocator
-    must not hand the block to another stream's allocation before that
-    stream's work is done with it, so the block is recorded on `stream` (the
-    allocation itself is made on torch's current stream)."""
-    t = torch.empty(numel, dtype=dtype, device=device)
-    if stream is not None and t.is_cuda:  # (None: torch's current stream, the one it was allocated on)
-        t.record_stream(stream)
+    """A buffer the library fills or reads for kernels queued on `stream`
+    (scratch, or an output the caller did not pass).  It is allocated on
+    `stream` itself, so the caching allocator hands out a block whose earlier
+    users on that stream are ordered before the launch (a block freed on
+    another stream could still be read there when the kernel overwrites it,
+    ADVICE r03), and it is recorded on torch's current stream, where the
+    caller reads the results, so it is not reused before that stream is done
+    with it either."""
+    if stream is None or not torch.device(device).type == "cuda":
+        return torch.empty(numel, dtype=dtype, device=device)
+    with torch.cuda.stream(stream):
+        t = torch.empty(numel, dtype=dtype, device=device)
+    cur = torch.cuda.current_stream(t.device)
+    if cur != stream:
+        t.record_stream(cur)
     return t
 
 
@@ -248,16 +255,25 @@ def spans_multi(items, stream=None) -> list:
 
 def ipv4_fill(batch: PacketBatch, mode: int = native.FILL_IP | native.FILL_L4, out2: torch.Tensor | None = None,
               status: torch.Tensor | None = None, stream=None) -> torch.Tensor | None:
-    """sccsum_ipv4_fill: generate checksums and store them in batch.data in place
-    (one launch; out2 / status are optional reports of what was stored).
-    Returns the [n, 2] values stored when out2 is given (else None)."""
+    """sccsum_ipv4_fill: generate checksums and store them in batch.data in
+    place.  FILL_L4 / FILL_ICMP_ECHO run two kernels on the stream (the
+    generate pass into out2, then the field-store pass); the header-only
+    modes one.  out2 / status are optional reports of what was stored;
+    without out2 the generate pass's words go through a scratch buffer from
+    torch's caching allocator (not the library's stream-ordered hipMallocAsync,
+    which sits outside torch's pool and can fail when torch has cached most of
+    HBM).  Returns the [n, 2] values stored when out2 is given
+    (else None)."""
     lib = native.load()
     n = batch.n
     _need(out2, 2 * n, torch.int16, "out2", batch.device)
     _need(status, n, torch.uint8, "status", batch.device)
+    vals = out2
+    if vals is None and mode & (native.FILL_L4 | native.FILL_ICMP_ECHO) and n:
+        vals = _scratch(2 * n, batch.device, stream, torch.int16)
     code = lib.sccsum_ipv4_fill(
         ctypes_ptr(batch.data), batch.bytes_len, ctypes_ptr(batch.off), ctypes_ptr(batch.length),
-        _ptr(out2), _ptr(status), n, batch.max_len, mode, _stream(stream),
+        _ptr(vals), _ptr(status), n, batch.max_len, mode, _stream(stream),
     )
     native.check(code, "sccsum_ipv4_fill")
     return None if out2 is None else out2[: 2 * n].view(n, 2)

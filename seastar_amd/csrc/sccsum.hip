@@ -28,6 +28,7 @@
 #include <atomic>
 #include <cstdint>
 #include <mutex>
+#include <tuple>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -722,12 +723,15 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
             uint64_t rs = jhead, re = static_cast<uint64_t>(jhead) + jL;
             uint32_t jipc = 0, jpseudo = 0, jst = 0;
             if (IPV4) {
-                // over 128 KiB the header was not picked up: decode it from the frame (wave-uniform)
+                // the header from the frame itself (wave-uniform; over 128 KiB it was not picked
+                // up).  Dword 5 only when the header is not dword-aligned: for an aligned 20-byte
+                // frame it would lie past the frame, possibly past roundup(bytes_len, 16)
                 const uint32_t* hp = reinterpret_cast<const uint32_t*>(ja0 + jhead - (jhead & 3u));
                 const uint32_t sh = jhead & 3u;
                 uint32_t hd[6];
 #pragma unroll
-                for (int i = 0; i < 6; ++i) hd[i] = hp[i];
+                for (int i = 0; i < 5; ++i) hd[i] = hp[i];
+                hd[5] = sh ? hp[5] : 0u;
                 uint32_t h[5];
 #pragma unroll
                 for (int i = 0; i < 5; ++i) h[i] = __builtin_amdgcn_alignbyte(hd[i + 1], hd[i], sh);
@@ -1235,7 +1239,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
 
         uint16_t* const out = Q.out[cur.q];
         uint8_t* const status = Q.status[cur.q];
+#ifdef SCCSUM_AB_NOSTORE
+        // A/B only (tools/build_ab.sh): the result stores left out of the
+        // stream — kept behind a test no lane passes, so nothing is optimised away
+        if (mine && word == 0x5EA57A2Cu && st == 0x77u) {
+#else
         if (mine) {
+#endif
             // the policy applies to an array whose tile part spans >= 128 B
             // (two lines); a smaller part is stored plain, so that the L2
             // merges it with its neighbour tiles' parts into whole lines
@@ -1432,16 +1442,59 @@ __global__ __launch_bounds__(kBlock) void read_probe_kernel(const u32x4* __restr
 
 // ---------------------------------------------------------------- host side
 
+// The device a launch runs on.  HIP runs a kernel on its stream's device, and
+// the memory contract (sccsum.h) puts the data on the calling thread's current
+// device, so the stream must belong to that device: hipStreamGetDevice for a
+// real stream (the null stream is the current device's).  A stream of another
+// device is SCCSUM_EINVAL — it would otherwise read another device's pointers
+// with this device's counter slot and grid size (VERDICT r03 missing #3).
+// Everything a launch sizes or takes per device (CU count, counter pool)
+// comes from the device returned here, not from a second hipGetDevice.
+int launch_device(hipStream_t s, int* dev) {
+    int cur = 0;
+    hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess) return static_cast<int>(e);
+    if (cur < 0 || cur >= kMaxDevices) return SCCSUM_ENODEV;
+    if (s != nullptr) {
+        hipDevice_t sd = -1;
+        e = hipStreamGetDevice(s, &sd);
+        if (e != hipSuccess) return static_cast<int>(e);
+        if (sd != cur) return SCCSUM_EINVAL;
+    }
+    *dev = cur;
+    return SCCSUM_OK;
+}
+
+// Every launch goes through hipLaunchKernel, which returns THIS launch's
+// error: the caller's pending HIP error from an earlier, unrelated call is
+// neither dropped nor read as this launch failing.  The
+// arguments are converted to the kernel's own parameter types first.
+template <typename... P, typename... A>
+hipError_t launch_kernel(void (*k)(P...), dim3 grid, hipStream_t s, A&&... a) {
+    static_assert(sizeof...(P) == sizeof...(A), "argument count");
+    std::tuple<std::decay_t<P>...> t(static_cast<std::decay_t<P>>(std::forward<A>(a))...);
+    void* args[sizeof...(P)];
+    std::apply([&](auto&... x) {
+        size_t i = 0;
+        ((args[i++] = static_cast<void*>(&x)), ...);
+    }, t);
+    return hipLaunchKernel(reinterpret_cast<const void*>(k), grid, dim3(kBlock), args, 0, s);
+}
+
 std::atomic<int> g_cu_count[kMaxDevices];
 
-int cu_count() {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 256;
+int cu_count(int dev) {
+    if (dev < 0 || dev >= kMaxDevices) return 256;
     int c = g_cu_count[dev].load(std::memory_order_relaxed);
     if (c > 0) return c;
     if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
     g_cu_count[dev].store(c, std::memory_order_relaxed);
     return c;
+}
+
+int current_cu_count() {
+    int dev = 0;
+    return hipGetDevice(&dev) == hipSuccess ? cu_count(dev) : 256;
 }
 
 // Default tile target: about 48 KiB of packets per tile (32 x 1500 B frames,
@@ -1493,8 +1546,8 @@ struct Knobs {
 };
 thread_local Knobs t_knobs;
 
-unsigned grid_for(uint64_t n) {
-    const uint64_t cap = static_cast<uint64_t>(cu_count()) * t_knobs.blocks_per_cu;
+unsigned grid_for(uint64_t n, int dev) {
+    const uint64_t cap = static_cast<uint64_t>(cu_count(dev)) * t_knobs.blocks_per_cu;
     uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
     if (want > cap) want = cap;
     want = (want + 7) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
@@ -1570,10 +1623,9 @@ struct HeadSlot {
     uint32_t idx = 0;
 };
 
-HeadSlot acquire_heads(hipStream_t s) {
+HeadSlot acquire_heads(hipStream_t s, int dev) {
     HeadSlot H;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return H;
+    if (dev < 0 || dev >= kMaxDevices) return H;
     DevicePool& P = g_pools[dev];
     uint32_t* const heads = P.heads.load(std::memory_order_acquire);
     if (heads == nullptr) return H;
@@ -1644,12 +1696,13 @@ int kernel_occupancy(const void* k) {
 int flat_occupancy(FlatKernel k) { return kernel_occupancy(reinterpret_cast<const void*>(k)); }
 
 // Q holds the queues (nq >= 1); tile0 is filled here from the tile size.
-void launch_flat(FlatKernel kern, hipStream_t s, Queues& Q, uint64_t n_total, uint64_t bytes_total, uint32_t flags,
-                 const RssParams& rss) {
+// `dev` is the stream's device (launch_device).
+hipError_t launch_flat(FlatKernel kern, hipStream_t s, int dev, Queues& Q, uint64_t n_total, uint64_t bytes_total,
+                       uint32_t flags, const RssParams& rss) {
     const Knobs& K = t_knobs;
     const int occ = flat_occupancy(kern);
     const uint64_t bpc = static_cast<uint64_t>(occ < K.blocks_per_cu ? occ : K.blocks_per_cu);
-    const uint64_t cap = static_cast<uint64_t>(cu_count()) * bpc;
+    const uint64_t cap = static_cast<uint64_t>(cu_count(dev)) * bpc;
     const uint64_t slots = cap * kWavesPerBlock;
     uint64_t bmax = static_cast<uint64_t>(K.tile_packets);
     const uint64_t tb = static_cast<uint64_t>(K.tile_bytes);
@@ -1674,58 +1727,55 @@ void launch_flat(FlatKernel kern, hipStream_t s, Queues& Q, uint64_t n_total, ui
     uint64_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     blocks = blocks < cap ? blocks : cap;
     blocks = (blocks + 15) & ~uint64_t(15);  // multiple of 16: XCD mapping, waves divide into kGroups
-    // A sticky error left by an earlier, unrelated HIP call on this thread
-    // would read as this launch failing below, and the slot would go back to
-    // the ring while the kernel runs on it: clear it first.
-    (void)hipGetLastError();
-    const HeadSlot H = K.dynamic ? acquire_heads(s) : HeadSlot{};
+    const HeadSlot H = K.dynamic ? acquire_heads(s, dev) : HeadSlot{};
     flags |= static_cast<uint32_t>(K.out_policy) << kOutPolicyShift;
     if (!K.short_chunks) flags |= kFlagFullChunks;
     flags |= static_cast<uint32_t>(K.run_align == 8 ? 2 : (K.run_align == 4 ? 1 : 0)) << kRunAlignShift;
-    kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(Q, static_cast<uint32_t>(B), H.heads, H.done,
-                                                                     H.ticket, flags, rss);
-    if (hipPeekAtLastError() != hipSuccess) release_unlaunched(H);
+    // the launch's own error decides whether the slot goes back: a kernel that
+    // did not start never reports completion
+    const hipError_t e = launch_kernel(kern, dim3(static_cast<unsigned>(blocks)), s, Q, static_cast<uint32_t>(B),
+                                       H.heads, H.done, H.ticket, flags, rss);
+    if (e != hipSuccess) release_unlaunched(H);
+    return e;
 }
 
 template <bool IPV4>
-void launch_simple(int uc, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
-                   const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
-                   uint32_t flags) {
-    const dim3 g(grid_for(n)), t(kBlock);
+hipError_t launch_simple(int uc, hipStream_t s, int dev, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
+                         const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status,
+                         uint64_t n, uint32_t flags) {
+    const dim3 g(grid_for(n, dev));
+    auto go = [&](auto kern) {
+        return launch_kernel(kern, g, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+    };
     switch (uc) {
-        case 1: csum_kernel<1, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags); break;
-        case 2: csum_kernel<2, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags); break;
-        case 4: csum_kernel<4, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags); break;
-        default: csum_kernel<8, IPV4><<<g, t, 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags); break;
+        case 1: return go(csum_kernel<1, IPV4>);
+        case 2: return go(csum_kernel<2, IPV4>);
+        case 4: return go(csum_kernel<4, IPV4>);
+        default: return go(csum_kernel<8, IPV4>);
     }
 }
 
 template <bool IPV4>
-void launch_rows(uint32_t max_len, hipStream_t s, const uint8_t* b, uint64_t bytes_len, const uint64_t* d_off,
-                 const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out, uint8_t* d_status, uint64_t n,
-                 uint32_t flags) {
+hipError_t launch_rows(uint32_t max_len, hipStream_t s, int dev, const uint8_t* b, uint64_t bytes_len,
+                       const uint64_t* d_off, const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out,
+                       uint8_t* d_status, uint64_t n, uint32_t flags) {
     const uint64_t units = max_len ? (static_cast<uint64_t>(max_len) + 30u) / 16u : 128u;  // worst-case head of 15
     // the grid is what the chip holds at once (a grid-stride kernel: blocks
     // that only start when others end would make the tail)
     auto go = [&](auto kern) {
         const int occ = kernel_occupancy(reinterpret_cast<const void*>(kern));
         const uint64_t bpc = static_cast<uint64_t>(occ < t_knobs.blocks_per_cu ? occ : t_knobs.blocks_per_cu);
-        const uint64_t cap = static_cast<uint64_t>(cu_count()) * bpc;
+        const uint64_t cap = static_cast<uint64_t>(cu_count(dev)) * bpc;
         uint64_t blocks = ((n + 63u) / 64u + kWavesPerBlock - 1) / kWavesPerBlock;  // a wave takes 64-packet tiles
         blocks = blocks < cap ? blocks : cap;
         blocks = (blocks + 7u) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
-        kern<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(b, bytes_len, d_off, d_len, d_seed, d_out,
-                                                                         d_status, n, flags);
+        return launch_kernel(kern, dim3(static_cast<unsigned>(blocks)), s, b, bytes_len, d_off, d_len, d_seed, d_out,
+                             d_status, n, flags);
     };
-    if (units <= 32) {
-        go(csum_row_kernel<2, IPV4>);
-    } else if (units <= 64) {
-        go(csum_row_kernel<4, IPV4>);
-    } else if (units <= 96) {  // 1500 B frames: 95 units
-        go(csum_row_kernel<6, IPV4>);
-    } else {
-        go(csum_row_kernel<8, IPV4>);
-    }
+    if (units <= 32) return go(csum_row_kernel<2, IPV4>);
+    if (units <= 64) return go(csum_row_kernel<4, IPV4>);
+    if (units <= 96) return go(csum_row_kernel<6, IPV4>);  // 1500 B frames: 95 units
+    return go(csum_row_kernel<8, IPV4>);
 }
 
 // Flat-kernel forms: 14 / 15 = U 8 (15: the next chunk in flight), 16 = U 16.
@@ -1733,15 +1783,15 @@ void launch_rows(uint32_t max_len, hipStream_t s, const uint8_t* b, uint64_t byt
 // removed: profiles/r01_ab_variants.log, r02_ab_roll.log.)  Frames may fill
 // in place; spans never do.
 template <bool IPV4>
-void launch_flat_variant(int variant, hipStream_t s, Queues& Q, uint64_t n_total, uint64_t bytes_total,
-                         uint32_t flags, const RssParams& rss) {
-    auto go = [&](auto kern) { launch_flat(kern, s, Q, n_total, bytes_total, flags, rss); };
+hipError_t launch_flat_variant(int variant, hipStream_t s, int dev, Queues& Q, uint64_t n_total, uint64_t bytes_total,
+                               uint32_t flags, const RssParams& rss) {
+    auto go = [&](auto kern) { return launch_flat(kern, s, dev, Q, n_total, bytes_total, flags, rss); };
     constexpr bool F = IPV4;
     const bool fill = IPV4 && (flags & kFillFlags);
     switch (variant) {
-        case 14: fill ? go(csum_flat_kernel<8, IPV4, F, false>) : go(csum_flat_kernel<8, IPV4, false, false>); break;
-        case 15: fill ? go(csum_flat_kernel<8, IPV4, F, true>) : go(csum_flat_kernel<8, IPV4, false, true>); break;
-        default: fill ? go(csum_flat_kernel<16, IPV4, F, false>) : go(csum_flat_kernel<16, IPV4, false, false>); break;
+        case 14: return fill ? go(csum_flat_kernel<8, IPV4, F, false>) : go(csum_flat_kernel<8, IPV4, false, false>);
+        case 15: return fill ? go(csum_flat_kernel<8, IPV4, F, true>) : go(csum_flat_kernel<8, IPV4, false, true>);
+        default: return fill ? go(csum_flat_kernel<16, IPV4, F, false>) : go(csum_flat_kernel<16, IPV4, false, false>);
     }
 }
 
@@ -1804,20 +1854,22 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
            void* stream, uint32_t flags = 0, const RssParams& rss = kNoRss) {
     if (n == 0) return SCCSUM_OK;
     if (!batch_ok<IPV4>(d_bytes, d_off, d_len, d_seed, d_out, d_status, flags)) return SCCSUM_EINVAL;
-    const int variant = pick_variant(n, bytes_len, flags, max_len);
     const hipStream_t s = static_cast<hipStream_t>(stream);
+    int dev = 0;
+    if (const int rc = launch_device(s, &dev); rc != SCCSUM_OK) return rc;
+    const int variant = pick_variant(n, bytes_len, flags, max_len);
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
     if (variant == 1 || variant == 2) {
-        if (variant == 1) {
-            launch_simple<IPV4>(units_class(max_len), s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n,
-                                flags);
-        } else {
-            launch_rows<IPV4>(max_len, s, b, bytes_len, d_off, d_len, d_seed, d_out, d_status, n, flags);
+        hipError_t e = variant == 1
+                           ? launch_simple<IPV4>(units_class(max_len), s, dev, b, bytes_len, d_off, d_len, d_seed,
+                                                 d_out, d_status, n, flags)
+                           : launch_rows<IPV4>(max_len, s, dev, b, bytes_len, d_off, d_len, d_seed, d_out, d_status,
+                                               n, flags);
+        if (e == hipSuccess && IPV4 && rss.hash != nullptr) {  // RSS is fused only in the flat kernel
+            e = launch_kernel(rss_kernel, dim3(static_cast<unsigned>((n + kBlock - 1) / kBlock)), s, b, bytes_len,
+                              d_off, d_len, nullptr, n, rss);
         }
-        if (IPV4 && rss.hash != nullptr) {  // RSS is fused only in the flat kernel
-            rss_kernel<<<dim3(static_cast<unsigned>((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s>>>(
-                b, bytes_len, d_off, d_len, nullptr, n, rss);
-        }
+        return static_cast<int>(e);
     } else {
         Queues Q{};
         Q.nq = 1;
@@ -1829,9 +1881,8 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
         Q.out[0] = d_out;
         Q.status[0] = d_status;
         Q.n[0] = n;
-        launch_flat_variant<IPV4>(variant, s, Q, n, bytes_len, flags, rss);
+        return static_cast<int>(launch_flat_variant<IPV4>(variant, s, dev, Q, n, bytes_len, flags, rss));
     }
-    return static_cast<int>(hipGetLastError());
 }
 
 // Several independent batches in one flat-kernel launch (sccsum_*_multi).
@@ -1849,21 +1900,24 @@ int launch_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
         bytes_total += x.n ? x.bytes_len : 0;
     }
     if (n_total == 0) return SCCSUM_OK;
-    const int variant = pick_variant(n_total, bytes_total, 0, max_len);
     const hipStream_t s = static_cast<hipStream_t>(stream);
+    int dev = 0;
+    if (const int rc = launch_device(s, &dev); rc != SCCSUM_OK) return rc;
+    const int variant = pick_variant(n_total, bytes_total, 0, max_len);
     if (variant == 1 || variant == 2) {  // the per-packet kernels take one batch per launch
         for (uint32_t i = 0; i < nbatch; ++i) {
             const sccsum_batch& x = batches[i];
             if (!x.n) continue;
-            if (variant == 1) {
-                launch_simple<IPV4>(units_class(max_len), s, static_cast<const uint8_t*>(x.d_bytes), x.bytes_len,
-                                    x.d_off, x.d_len, x.d_seed, static_cast<uint16_t*>(x.d_out), x.d_status, x.n, 0);
-            } else {
-                launch_rows<IPV4>(max_len, s, static_cast<const uint8_t*>(x.d_bytes), x.bytes_len, x.d_off, x.d_len,
-                                  x.d_seed, static_cast<uint16_t*>(x.d_out), x.d_status, x.n, 0);
-            }
+            const auto* b = static_cast<const uint8_t*>(x.d_bytes);
+            auto* o = static_cast<uint16_t*>(x.d_out);
+            const hipError_t e =
+                variant == 1 ? launch_simple<IPV4>(units_class(max_len), s, dev, b, x.bytes_len, x.d_off, x.d_len,
+                                                   x.d_seed, o, x.d_status, x.n, 0)
+                             : launch_rows<IPV4>(max_len, s, dev, b, x.bytes_len, x.d_off, x.d_len, x.d_seed, o,
+                                                 x.d_status, x.n, 0);
+            if (e != hipSuccess) return static_cast<int>(e);
         }
-        return static_cast<int>(hipGetLastError());
+        return SCCSUM_OK;
     }
     Queues Q{};
     for (uint32_t i = 0; i < nbatch; ++i) {
@@ -1879,8 +1933,7 @@ int launch_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
         Q.status[q] = x.d_status;
         Q.n[q] = x.n;
     }
-    launch_flat_variant<IPV4>(variant, s, Q, n_total, bytes_total, 0, kNoRss);
-    return static_cast<int>(hipGetLastError());
+    return static_cast<int>(launch_flat_variant<IPV4>(variant, s, dev, Q, n_total, bytes_total, 0, kNoRss));
 }
 
 // ---- gather: fragments from device-readable memory (HBM, or pinned host
@@ -2116,14 +2169,19 @@ int launch_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const
         return SCCSUM_EINVAL;
     }
     const hipStream_t s = static_cast<hipStream_t>(stream);
+    int dev = 0;
+    if (const int rc = launch_device(s, &dev); rc != SCCSUM_OK) return rc;
     const auto* st = static_cast<const uint8_t*>(d_stage);
-    const dim3 g(grid_for(n)), t(kBlock);
+    const dim3 g(grid_for(n, dev));
+    auto go = [&](auto kern) {
+        return static_cast<int>(launch_kernel(kern, g, s, d_desc, d_first, d_off, d_len, d_seed, st, d_out, d_status,
+                                              n, 0u));
+    };
     switch (units_class(max_len)) {
-        case 1: csum_desc_kernel<1, IPV4><<<g, t, 0, s>>>(d_desc, d_first, d_off, d_len, d_seed, st, d_out, d_status, n, 0); break;
-        case 2: csum_desc_kernel<2, IPV4><<<g, t, 0, s>>>(d_desc, d_first, d_off, d_len, d_seed, st, d_out, d_status, n, 0); break;
-        default: csum_desc_kernel<4, IPV4><<<g, t, 0, s>>>(d_desc, d_first, d_off, d_len, d_seed, st, d_out, d_status, n, 0); break;
+        case 1: return go(csum_desc_kernel<1, IPV4>);
+        case 2: return go(csum_desc_kernel<2, IPV4>);
+        default: return go(csum_desc_kernel<4, IPV4>);
     }
-    return static_cast<int>(hipGetLastError());
 }
 
 }  // namespace
@@ -2154,7 +2212,7 @@ int sccsum_init(int device) {
     if (device < 0 || device >= n) return SCCSUM_ENODEV;
     const hipError_t e2 = hipSetDevice(device);
     if (e2 != hipSuccess) return static_cast<int>(e2);
-    (void)sccsum::cu_count();
+    (void)sccsum::cu_count(device);
     return sccsum::ensure_heads(device);
 }
 
@@ -2200,11 +2258,14 @@ int sccsum_ipv4_rss(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_o
         (reinterpret_cast<uintptr_t>(d_len) & 3u)) {
         return SCCSUM_EINVAL;
     }
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    int dev = 0;
+    if (const int rc = sccsum::launch_device(s, &dev); rc != SCCSUM_OK) return rc;
     const sccsum::RssParams P = sccsum::make_rss(key, key_len, static_cast<uint32_t>(mode), d_hash);
-    sccsum::rss_kernel<<<dim3(static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock)), dim3(sccsum::kBlock),
-                         0, static_cast<hipStream_t>(stream)>>>(static_cast<const uint8_t*>(d_bytes), bytes_len, d_off,
-                                                                d_len, d_status, n, P);
-    return static_cast<int>(hipGetLastError());
+    return static_cast<int>(sccsum::launch_kernel(sccsum::rss_kernel,
+                                                  dim3(static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock)),
+                                                  s, static_cast<const uint8_t*>(d_bytes), bytes_len, d_off, d_len,
+                                                  d_status, n, P));
 }
 
 int sccsum_ipv4_frames_rss(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
@@ -2220,10 +2281,12 @@ int sccsum_ipv4_frames_rss(const void* d_bytes, uint64_t bytes_len, const uint64
 int sccsum_gather(const sccsum_gather_desc* d_desc, uint64_t n, void* d_dst, void* stream) {
     if (n == 0) return SCCSUM_OK;
     if (!d_desc || !d_dst || (reinterpret_cast<uintptr_t>(d_desc) & 7u)) return SCCSUM_EINVAL;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    int dev = 0;
+    if (const int rc = sccsum::launch_device(s, &dev); rc != SCCSUM_OK) return rc;
     const uint64_t blocks = std::min<uint64_t>((n + 3) / 4, 65536);
-    sccsum::gather_kernel<<<dim3(static_cast<unsigned>(blocks)), dim3(sccsum::kBlock), 0,
-                            static_cast<hipStream_t>(stream)>>>(d_desc, n, static_cast<uint8_t*>(d_dst));
-    return static_cast<int>(hipGetLastError());
+    return static_cast<int>(sccsum::launch_kernel(sccsum::gather_kernel, dim3(static_cast<unsigned>(blocks)), s, d_desc,
+                                                  n, static_cast<uint8_t*>(d_dst)));
 }
 
 int sccsum_spans_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const uint64_t* d_off,
@@ -2251,6 +2314,9 @@ int sccsum_fragments(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_
         (reinterpret_cast<uintptr_t>(d_seed) & 3u) || (reinterpret_cast<uintptr_t>(d_out) & 1u)) {
         return SCCSUM_EINVAL;
     }
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    int dev = 0;
+    if (const int rc = sccsum::launch_device(s, &dev); rc != SCCSUM_OK) return rc;
     auto* raw = static_cast<uint16_t*>(d_workspace);
     auto* raw_st = static_cast<uint8_t*>(d_workspace) + ((2 * nfrag + 15) & ~uint64_t(15));
     if (nfrag) {
@@ -2259,9 +2325,8 @@ int sccsum_fragments(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_
         if (rc != SCCSUM_OK) return rc;
     }
     const unsigned grid = static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock);
-    sccsum::frag_combine_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, static_cast<hipStream_t>(stream)>>>(
-        d_frag_len, nfrag, d_pkt_first, raw, raw_st, d_seed, d_out, d_status, n);
-    return static_cast<int>(hipGetLastError());
+    return static_cast<int>(sccsum::launch_kernel(sccsum::frag_combine_kernel, dim3(grid), s, d_frag_len, nfrag,
+                                                  d_pkt_first, raw, raw_st, d_seed, d_out, d_status, n));
 }
 
 int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
@@ -2275,15 +2340,20 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
         return SCCSUM_EINVAL;
     }
     if (n == 0) return SCCSUM_OK;
-    if (mode & (SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO)) {
+    const bool two_pass = (mode & (SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO)) != 0;
+    if (two_pass ? !sccsum::batch_ok<true>(d_bytes, d_off, d_len, nullptr, d_out2, d_status, sccsum::kFlagFillL4)
+                 : (!d_bytes || !d_off || !d_len || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
+                    (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_out2) & 3u))) {
+        return SCCSUM_EINVAL;  // (before any allocation)
+    }
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    int dev = 0;
+    if (const int rc = sccsum::launch_device(s, &dev); rc != SCCSUM_OK) return rc;
+    if (two_pass) {
         // pass 1 generates into d_out2, pass 2 stores the fields.  Without a
         // caller's d_out2 the values go through a stream-ordered allocation
         // (hipMallocAsync / hipFreeAsync on `stream`: no host sync, safe
         // under graph capture, freed once pass 2 is done with it)
-        const hipStream_t s = static_cast<hipStream_t>(stream);
-        if (!sccsum::batch_ok<true>(d_bytes, d_off, d_len, nullptr, d_out2, d_status, sccsum::kFlagFillL4)) {
-            return SCCSUM_EINVAL;  // (before any allocation)
-        }
         void* scratch = nullptr;
         if (!d_out2) {
             const hipError_t e = hipMallocAsync(&scratch, 4 * n, s);
@@ -2297,10 +2367,9 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
                                       stream, flags);
         if (rc == SCCSUM_OK) {
             const unsigned grid = static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock);
-            sccsum::fill_store_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, s>>>(
-                static_cast<uint8_t*>(d_bytes), bytes_len, d_off, d_len, reinterpret_cast<const uint32_t*>(vals), n,
-                mode);
-            rc = static_cast<int>(hipGetLastError());
+            rc = static_cast<int>(sccsum::launch_kernel(sccsum::fill_store_kernel, dim3(grid), s,
+                                                        static_cast<uint8_t*>(d_bytes), bytes_len, d_off, d_len,
+                                                        reinterpret_cast<const uint32_t*>(vals), n, mode));
         }
         if (scratch) {
             const hipError_t e = hipFreeAsync(scratch, s);
@@ -2308,15 +2377,10 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
         }
         return rc;
     }
-    if (!d_bytes || !d_off || !d_len || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
-        (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_out2) & 3u)) {
-        return SCCSUM_EINVAL;
-    }
     const unsigned grid = static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock);
-    sccsum::fill_header_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, static_cast<hipStream_t>(stream)>>>(
-        static_cast<uint8_t*>(d_bytes), bytes_len, d_off, d_len, reinterpret_cast<uint32_t*>(d_out2), d_status, n,
-        mode);
-    return static_cast<int>(hipGetLastError());
+    return static_cast<int>(sccsum::launch_kernel(sccsum::fill_header_kernel, dim3(grid), s,
+                                                  static_cast<uint8_t*>(d_bytes), bytes_len, d_off, d_len,
+                                                  reinterpret_cast<uint32_t*>(d_out2), d_status, n, mode));
 }
 
 int sccsum_set_kernel_variant(int variant) {
@@ -2382,14 +2446,16 @@ int sccsum_set_tail_split(int split, int quarters) {
 
 int sccsum_sync(void* stream) { return static_cast<int>(hipStreamSynchronize(static_cast<hipStream_t>(stream))); }
 
-int sccsum_read_probe_blocks(void) { return sccsum::cu_count() * sccsum::kBlocksPerCU; }
+int sccsum_read_probe_blocks(void) { return sccsum::current_cu_count() * sccsum::kBlocksPerCU; }
 
 int sccsum_read_probe(const void* d_src, uint64_t bytes, uint64_t* d_sink, void* stream) {
     if (!d_src || !d_sink || (bytes & 15u) || (reinterpret_cast<uintptr_t>(d_src) & 15u)) return SCCSUM_EINVAL;
-    const unsigned grid = static_cast<unsigned>(sccsum_read_probe_blocks()) & ~7u;
-    sccsum::read_probe_kernel<<<dim3(grid), dim3(sccsum::kBlock), 0, static_cast<hipStream_t>(stream)>>>(
-        static_cast<const sccsum::u32x4*>(d_src), bytes / 16, d_sink);
-    return static_cast<int>(hipGetLastError());
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    int dev = 0;
+    if (const int rc = sccsum::launch_device(s, &dev); rc != SCCSUM_OK) return rc;
+    const unsigned grid = static_cast<unsigned>(sccsum::cu_count(dev) * sccsum::kBlocksPerCU) & ~7u;
+    return static_cast<int>(sccsum::launch_kernel(sccsum::read_probe_kernel, dim3(grid), s,
+                                                  static_cast<const sccsum::u32x4*>(d_src), bytes / 16, d_sink));
 }
 
 }  // extern "C"

@@ -135,6 +135,19 @@ static void checks() {
     EXPECT(sccsum_set_burst_fused(2) == SCCSUM_OK);
     EXPECT(sccsum_pipeline_run(nullptr, SCCSUM_PIPE_IPV4, SCCSUM_GATHER_ZERO_COPY, nullptr, 0, nullptr, nullptr,
                                nullptr, 0, 0, nullptr, nullptr) == SCCSUM_EINVAL);
+    // well-formed arguments without a device: the launch device is resolved
+    // (hipGetDevice, then the stream's device) before anything is launched, so
+    // the call returns that HIP error and touches nothing.  (Only where no
+    // device is visible: on a GPU these stand-in pointers would be launched.)
+    int ndev = 0;
+    if (sccsum_device_count(&ndev) != SCCSUM_OK || ndev == 0) {
+        EXPECT(sccsum_spans(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr,
+                            static_cast<uint16_t*>(d16), nullptr, 3, 0, nullptr) > 0);
+        EXPECT(sccsum_ipv4_fill(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16),
+                                static_cast<uint16_t*>(d16), nullptr, 3, 0, SCCSUM_FILL_IP | SCCSUM_FILL_L4,
+                                nullptr) > 0);
+        EXPECT(sccsum_read_probe(d16, 64, static_cast<uint64_t*>(d16), nullptr) > 0);
+    }
     // host arithmetic and strings
     EXPECT(sccsum_pseudo_seed(1, 2, 17, 8) == 28u);
     EXPECT(sccsum_pseudo_seed(0xffffffffu, 0xffffffffu, 255, 0xffff) <= 0xffffu);

@@ -1,5 +1,8 @@
-// Seastar's threading model against one device: one reactor thread per shard
-// (src/core/reactor.cc:3437-3438), each binding itself with sccsum_init,
+// Seastar's threading model: one reactor thread per shard
+// (src/core/reactor.cc:3437-3438), shard i on device i % (visible devices),
+// so every visible device's counter pool and launch sizing are used; with
+// several devices each shard also checks that a launch on another device's
+// stream is refused (SCCSUM_EINVAL).  Each shard binds itself with sccsum_init,
 // owning its streams, its batches and a burst queue, and launching at the
 // same time as every other shard: frames (verify), seeded spans, a multi
 // launch, the in-place fill, a burst queue fed one frame at a time, and a
@@ -26,6 +29,8 @@ namespace {
 
 std::atomic<int> g_bad{0};
 std::mutex g_print;
+unsigned long long g_devices_used = 0;  // under g_print
+std::atomic<int> g_cross_checked{0};    // launches refused on another device's stream
 
 void fail(int shard, const char* what, long i) {
     if (g_bad.fetch_add(1) < 20) {
@@ -133,7 +138,16 @@ void burst_done(void* user, uint64_t first, uint32_t count, const uint16_t* resu
 }
 
 void shard_main(int shard, int rounds) {
-    if (!ok(sccsum_init(0), shard, "sccsum_init")) return;
+    // shard i on device i % ndev (this_shard_id() % ngpus), so
+    // every visible device's counter pool and CU count are exercised
+    int ndev = 0;
+    if (!ok(sccsum_device_count(&ndev), shard, "device count") || ndev < 1) return;
+    const int dev = shard % ndev;
+    if (!ok(sccsum_init(dev), shard, "sccsum_init")) return;
+    {
+        std::lock_guard<std::mutex> l(g_print);
+        g_devices_used |= 1ull << dev;
+    }
     // per-thread knobs: each shard runs another kernel form; none leaks into another shard
     const int forms[6] = {0, 16, 15, 14, 1, 2};
     if (!ok(sccsum_set_kernel_variant(forms[shard % 6]), shard, "variant")) return;
@@ -175,6 +189,21 @@ void shard_main(int shard, int rounds) {
     }
     hipStream_t s0, sx;
     if (!hip_ok(hipStreamCreate(&s0), shard, "stream") || !hip_ok(hipStreamCreate(&sx), shard, "stream")) return;
+    if (ndev > 1) {
+        // a stream of another device is refused (sccsum.h: launches run on the
+        // stream's device, which must be the calling thread's current one)
+        hipStream_t other;
+        const int od = (dev + 1) % ndev;
+        if (hip_ok(hipSetDevice(od), shard, "set other device") && hip_ok(hipStreamCreate(&other), shard, "stream")) {
+            hip_ok(hipSetDevice(dev), shard, "set device back");
+            const int rc = sccsum_ipv4_frames(dA.bytes, dA.bytes_len, dA.off, dA.len, o1, s1, n, 3100, other);
+            if (rc != SCCSUM_EINVAL) fail(shard, "stream of another device accepted", rc);
+            g_cross_checked.fetch_add(1);
+            hip_ok(hipSetDevice(od), shard, "set other device");
+            (void)hipStreamDestroy(other);
+        }
+        hip_ok(hipSetDevice(dev), shard, "set device back");
+    }
     auto check2 = [&](const std::vector<uint16_t>& got, const std::vector<uint16_t>& want, const char* what) {
         for (size_t i = 0; i < want.size(); ++i) {
             if (got[i] != want[i]) {
@@ -233,7 +262,7 @@ void shard_main(int shard, int rounds) {
     sink.out.assign(2 * n, 0xEEEE);
     sink.st.assign(n, 0xEE);
     sccsum_burst* q = nullptr;
-    if (ok(sccsum_burst_create(0, SCCSUM_PIPE_IPV4, 1u << 20, 256, 20000, 4, burst_done, &sink, &q), shard,
+    if (ok(sccsum_burst_create(dev, SCCSUM_PIPE_IPV4, 1u << 20, 256, 20000, 4, burst_done, &sink, &q), shard,
            "burst create")) {
         for (uint32_t i = 0; i < n; ++i) {
             sccsum_fragment fr{A.bytes.data() + A.off[i], A.len[i]};
@@ -271,8 +300,11 @@ int main(int argc, char** argv) {
         std::printf("shards_gpu: FAILED (%d)\n", g_bad.load());
         return 1;
     }
-    std::printf("shards_gpu: OK (%d shards x %d rounds: frames, spans, multi, fill, %d launches on destroyed "
-                "streams per round, burst queue)\n",
-                threads, rounds, 8);
+    int ndev = 0;
+    (void)sccsum_device_count(&ndev);
+    std::printf("shards_gpu: OK (%d shards x %d rounds on %d device%s, mask 0x%llx: frames, spans, multi, fill, %d "
+                "launches on destroyed streams per round, burst queue; %d launches on another device's stream "
+                "refused)\n",
+                threads, rounds, ndev, ndev == 1 ? "" : "s", g_devices_used, 8, g_cross_checked.load());
     return 0;
 }

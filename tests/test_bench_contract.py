@@ -38,6 +38,10 @@ def test_bench_line_has_the_contract_fields():
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in cpu, k
     assert cpu["kind"] in ("port", "reference") and cpu["value"] > 0 and cpu["cores"] >= 1
+    # one thread per physical core (pinned), the host's physical cores and the all-cores figure
+    assert cpu["physical_cores"]["host"] >= cpu["cores"] and cpu["value_all_cores"] >= cpu["value"] * 0.99
+    assert cpu["scaling_GiBps"]["1"] == cpu["value_1core"] and cpu["pinned_cpus"]
+    assert cpu["physical_cores"]["l3_domains_host"] >= 1 and "one_l3_domain" in cpu
     args = argparse.Namespace(pmc=None, steps=200, warmup=5)
     alg = 3_176_136_704
     roof = bench.roofline(alg, 460e-6, "udp1500", "csum_flat_kernel<16, true, false, false>",
@@ -55,3 +59,23 @@ def test_bench_line_has_the_contract_fields():
         assert k in line, k
     assert line["n_gpus"] == 1 and line["steps"] == 200 and line["scaling"] == "weak"
     assert line["config"]["workload"] == "cfg2" and line["data"] == "synthetic"
+
+
+def test_e2e_line_names_the_slowest_rank():
+    """cfg 5 (--config e2e) at N ranks: per rank H2D / D2H rates and its NUMA
+    node; the line carries the sum over ranks and names the slowest rank
+    (VERDICT r03 item 7), built here from synthetic per-rank figures."""
+    bench = _bench()
+    bench._imports()
+    h2d, d2h = bench.e2e_pcie_bytes(1 << 20, bench.native.GATHER_STRIDED)
+    assert h2d == (1 << 20) * (bench.FRAME + 12) and d2h == (1 << 20) * 4
+    assert bench.e2e_pcie_bytes(8, bench.native.GATHER_NONE)[0] == 8 * (2304 + 12)
+    ranks = [{"rank": r, "device": r, "pci_bus_id": f"0000:{r:02x}:00.0", "numa_node": r // 4,
+              "variants": {"C_strided_dma": {"GiBps_packet_bytes": 48.0 - (r == 5) * 9, "ms_per_batch": 30.0,
+                                             "h2d_GBps": 52.5 - (r == 5) * 10, "d2h_GBps": 0.14}}}
+             for r in range(8)]
+    s = bench.e2e_ranks_summary(ranks, "C_strided_dma")
+    assert s["slowest_rank"]["rank"] == 5 and s["slowest_rank"]["numa_node"] == 1
+    assert s["slowest_rank"]["pci_bus_id"] == "0000:05:00.0"
+    assert abs(s["sum_over_ranks_GiBps"] - (8 * 48 - 9)) < 1e-6 and len(s["per_rank_h2d_GBps"]) == 8
+    assert abs(s["sum_h2d_GBps"] - (8 * 52.5 - 10)) < 1e-6

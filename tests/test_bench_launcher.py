@@ -31,8 +31,8 @@ def test_launcher_starts_n_ranks_without_device(n):
     assert len({r["pid"] for r in d["ranks"]}) == n  # one process per rank
     # the per_rank block a real N > 1 line carries: one entry per rank, in rank order
     assert [r["rank"] for r in d["per_rank"]] == list(range(n))
-    assert all({"device", "pci_bus_id", "host", "wall_s", "GiBps", "avg_launch_us", "read_ceiling_GBps"} <= set(r)
-               for r in d["per_rank"])
+    assert all({"device", "pci_bus_id", "host", "wall_s", "GiBps", "avg_launch_us", "read_ceiling_GBps", "numa_node",
+                "cpus", "affinity", "mempolicy"} <= set(r) for r in d["per_rank"])
 
 
 def test_launcher_reports_a_failed_rank_and_stops_the_others():
@@ -55,7 +55,7 @@ def test_launcher_two_ranks_on_the_gpu():
     """Two rank processes on the box's one GPU (a rehearsal of the driver's
     --gpus N run: each rank builds, checks and times its own shard)."""
     d = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--packets", "65536", "--rotate", "1", "--no-cpu",
-               timeout=300)
+               "--share-devices", timeout=300)
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["config"]["global_batch"] == 2 * 65536
     pr = d["per_rank"]
@@ -63,6 +63,9 @@ def test_launcher_two_ranks_on_the_gpu():
     for r in pr:  # real figures per rank: the device it ran on, its own rate, launch time and read ceiling
         assert r["pci_bus_id"] and r["GiBps"] > 0 and r["avg_launch_us"] > 0 and r["read_ceiling_GBps"] > 0
         assert 0 < r["frac"] < 1
+        # locality: the GPU's NUMA node (-1 on a one-node host) and the CPUs the rank was bound to
+        assert isinstance(r["numa_node"], int) and r["cpus"] and r["affinity"] and r["mempolicy"]
+    assert pr[0]["numa_node"] == pr[1]["numa_node"]  # one GPU: both ranks on its node
     print(json.dumps(pr))
 
 
@@ -99,7 +102,7 @@ def test_torchrun_two_ranks_on_the_gpu():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
                         "--gpus", "2", "--steps", "3", "--warmup", "1", "--packets", "65536", "--rotate", "1",
-                        "--no-cpu"], capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+                        "--no-cpu", "--share-devices"], capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
     assert r.returncode == 0, r.stdout + r.stderr
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and lines[0]["value"] > 0

@@ -791,11 +791,14 @@ def test_many_launches_in_flight_streams_and_graphs(dev, kernel_variant):
     assert np.array_equal(gst.cpu().numpy(), want_st)
 
 
-def test_fill_without_out2_in_a_graph(dev, kernel_variant):
-    """sccsum_ipv4_fill with no d_out2, captured in a HIP graph: its scratch
-    is a stream-ordered allocation (a graph memory node), so the call stays
-    capturable; each replay over freshly restored frames stores exactly the
-    oracle's fields."""
+@pytest.mark.parametrize("path", ["c_abi", "wrapper"])
+def test_fill_without_out2_in_a_graph(dev, kernel_variant, path):
+    """sccsum_ipv4_fill with no d_out2, captured in a HIP graph.  Through the
+    C-ABI with d_out2 = NULL the library's scratch is a stream-ordered
+    allocation (a graph memory node); the Python wrapper passes a scratch from
+    torch's caching allocator instead.  Either way the call stays
+    capturable, and each replay over freshly restored frames stores exactly
+    the oracle's fields."""
     if kernel_variant not in (15, 16):
         pytest.skip("the fill runs the flat kernel")
     rng = np.random.default_rng(0x6A1)
@@ -808,7 +811,11 @@ def test_fill_without_out2_in_a_graph(dev, kernel_variant):
     cs = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize()
     with torch.cuda.graph(g, stream=cs):
-        batch.ipv4_fill(b, m, stream=cs)
+        if path == "c_abi":
+            batch.prepare_call("sccsum_ipv4_fill", b.data, b.bytes_len, b.off, b.length, None, None, b.n, b.max_len,
+                               m)(cs)
+        else:
+            batch.ipv4_fill(b, m, stream=cs)
     for _ in range(3):
         b.data.copy_(orig)
         g.replay()
@@ -954,6 +961,33 @@ def test_slot_layout_one_run_per_packet(dev, kernel_variant, short):
         assert np.array_equal(got, want) and np.array_equal(st, want_st)
     finally:
         native.check(lib.sccsum_set_short_chunks(1), "short_chunks")
+
+
+def test_slot_layout_short_slow_frames_at_the_buffer_end(dev, kernel_variant):
+    """20-byte frames the fast path hands to the exact redo (options, an IP
+    length that is not the frame's, fragments) in a sparse slot layout, at
+    every dword phase, the last one ending exactly at bytes_len (a multiple of
+    16, frame start 12 mod 16): the redo reads the header from the frame and
+    must stay inside it (sccsum.h's readable extent is
+    roundup(bytes_len, 16)); results against the oracle."""
+    rng = np.random.default_rng(4242)
+    n = 96
+    fl = np.full(n, 20, dtype=np.uint32)
+    off = (np.arange(n, dtype=np.uint64) * 2048 + 512 + (np.arange(n) % 16)).astype(np.uint64)
+    total = int(off[-2]) + 2048
+    total += (-total) % 16
+    off[-1] = total - 20  # ends exactly at bytes_len
+    buf = rng.integers(0, 256, size=total, dtype=np.uint8)
+    for i in range(n):
+        o = int(off[i])
+        ihl = 5 + (i % 3 == 0)                       # options claimed: 4*ihl past ip_len -> malformed
+        ip_len = 20 + (i % 3 == 1) * (1 + i % 5)     # longer than the frame -> malformed
+        buf[o], buf[o + 2], buf[o + 3], buf[o + 9] = 0x40 | ihl, ip_len >> 8, ip_len & 0xFF, (17, 6, 1)[i % 3]
+        buf[o + 6], buf[o + 7] = (0x20 if i % 7 == 0 else 0), 0
+    assert int(off[-1]) % 16 == 12 and int(off[-1]) + 20 == buf.size
+    got, st = _frames(dev, buf, off, fl)
+    want, want_st = oracle.batch_ipv4(buf, off, fl)
+    assert np.array_equal(got, want) and np.array_equal(st, want_st)
 
 
 @pytest.mark.parametrize("bpc,tile_packets", [(8, 64), (1, 5), (3, 1)])

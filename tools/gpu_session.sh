@@ -13,6 +13,8 @@
 #                          cut to the timed dispatches by tools/prof_timed.py ($TAG_pmc_CFG.json)
 #   py:SCRIPT[+ARG...]     python SCRIPT ARG... (a tools/ probe)
 #   bin:PROGRAM[+ARG...]   a probe program built here beforehand (tools/dev/*.hip)
+#   pbin:PROGRAM[+ARG...]  the same program under rocprofv3: a kernel trace, then separate FETCH_SIZE and
+#                          WRITE_SIZE passes; per-kernel means by tools/pmc_by_name.py (pbin_NAME_summary.log)
 #   lib:PATH | lib:default the library later steps load (SCCSUM_LIB: an A/B build of the same ABI,
 #                          or libsccsum_at_<commit>.so, an older tree's build); bench logs are named after it
 # Outputs go to gpurun_out/TAG/; steps.log records each step's outcome.
@@ -88,6 +90,17 @@ run_step() {
         bin)
             split "$rest"
             timeout -k 10 400 "./$CFG" "${ARGS[@]}" >> "$O/bin_$(basename "$CFG").log" 2>&1 ;;
+        pbin)
+            split "$rest"
+            (cd /tmp && \
+             timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/pbin_$n/trace" -o run --output-format csv \
+                -- "$R/$CFG" "${ARGS[@]}" > "$O/pbin_${n}_trace.log" 2>&1 && \
+             timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$O/pbin_$n/fetch" -o run --output-format csv \
+                -- "$R/$CFG" "${ARGS[@]}" > "$O/pbin_${n}_fetch.log" 2>&1 && \
+             timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$O/pbin_$n/write" -o run --output-format csv \
+                -- "$R/$CFG" "${ARGS[@]}" > "$O/pbin_${n}_write.log" 2>&1) && \
+            { python tools/pmc_by_name.py "$O/pbin_$n/fetch" --trace "$O/pbin_$n/trace" && \
+              python tools/pmc_by_name.py "$O/pbin_$n/write" --write; } > "$O/pbin_${n}_summary.log" 2>&1 ;;
         *)
             echo "unknown step $step" >> "$O/steps.log"
             return 2 ;;
