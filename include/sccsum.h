@@ -111,6 +111,14 @@ const char* sccsum_strerror(int err);
 /* Number of visible HIP devices. */
 int sccsum_device_count(int* count);
 
+/* The NUMA node a device's PCI function sits on (sysfs numa_node of its
+ * hipDeviceGetPCIBusId address), -1 when the platform reports none.  Seastar
+ * pins each shard's thread to a core and binds its memory to that core's
+ * node (src/core/reactor.cc:4163, src/core/memory.cc:1898-1951); a shard
+ * should drive a GPU on its own node, so its batches and pinned pools do not
+ * cross the socket link ("Which GPU a shard drives"). */
+int sccsum_device_numa_node(int device, int* node);
+
 /* Bind the calling host thread to `device` (hipSetDevice), cache its
  * compute-unit count for launch sizing and, on the device's first call,
  * allocate its pool of tile counters (2048 slots, 34 MB of HBM, plus 8 KiB

@@ -26,7 +26,9 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cctype>
 #include <cstdint>
+#include <cstdio>
 #include <mutex>
 #include <tuple>
 #include <type_traits>
@@ -2203,6 +2205,27 @@ const char* sccsum_strerror(int err) {
 int sccsum_device_count(int* count) {
     if (!count) return SCCSUM_EINVAL;
     return static_cast<int>(hipGetDeviceCount(count));
+}
+
+int sccsum_device_numa_node(int device, int* node) {
+    if (!node) return SCCSUM_EINVAL;
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return static_cast<int>(e);
+    if (device < 0 || device >= n) return SCCSUM_ENODEV;
+    char bdf[64] = {};
+    const hipError_t e2 = hipDeviceGetPCIBusId(bdf, static_cast<int>(sizeof(bdf)), device);
+    if (e2 != hipSuccess) return static_cast<int>(e2);
+    for (char* c = bdf; *c; ++c) *c = static_cast<char>(std::tolower(static_cast<unsigned char>(*c)));
+    char path[160];
+    std::snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bdf);
+    *node = -1;
+    if (FILE* f = std::fopen(path, "r")) {
+        int v = -1;
+        if (std::fscanf(f, "%d", &v) == 1) *node = v;
+        std::fclose(f);
+    }
+    return SCCSUM_OK;
 }
 
 int sccsum_init(int device) {

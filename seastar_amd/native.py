@@ -55,6 +55,7 @@ _PROTOS = {
     "sccsum_abi_version": (ctypes.c_int, []),
     "sccsum_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "sccsum_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "sccsum_device_numa_node": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "sccsum_init": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_pseudo_seed": (_u32, [_u32, _u32, ctypes.c_uint8, ctypes.c_uint16]),
     "sccsum_spans": (ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),

@@ -139,6 +139,7 @@ static void checks() {
     // (hipGetDevice, then the stream's device) before anything is launched, so
     // the call returns that HIP error and touches nothing.  (Only where no
     // device is visible: on a GPU these stand-in pointers would be launched.)
+    EXPECT(sccsum_device_numa_node(0, nullptr) == SCCSUM_EINVAL);
     int ndev = 0;
     if (sccsum_device_count(&ndev) != SCCSUM_OK || ndev == 0) {
         EXPECT(sccsum_spans(d16, 64, static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr,

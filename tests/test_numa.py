@@ -148,3 +148,24 @@ def test_bench_refuses_more_ranks_than_devices(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
     assert d["n_gpus"] == 3 and all(e["affinity"].startswith("unchanged") for e in d["per_rank"])
+
+
+@pytest.mark.gpu
+def test_device_numa_node_matches_sysfs():
+    """sccsum_device_numa_node (the C-ABI's answer for C++ shards) agrees with
+    the sysfs node of the PCI address torch reports for the same device."""
+    import ctypes
+
+    import torch
+
+    from seastar_amd import native
+
+    lib = native.load()
+    p = torch.cuda.get_device_properties(0)
+    bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    node = ctypes.c_int(-7)
+    native.check(lib.sccsum_device_numa_node(0, ctypes.byref(node)), "sccsum_device_numa_node")
+    assert node.value == numa.pci_numa_node(bdf)
+    assert lib.sccsum_device_numa_node(0, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_device_numa_node(10_000, ctypes.byref(node)) == native.SCCSUM_ENODEV
+    print(f"device 0 {bdf}: NUMA node {node.value}")

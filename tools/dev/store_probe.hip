@@ -14,7 +14,10 @@
 //   rd+st2d   as rd+st2, but the tile's first line of each frame is loaded default-policy
 //   rd+side   the read pass stashes each frame's head line in a dense side array
 //   side2line a second pass writes the stashed lines back whole (no partial-line RMW)
-// usage: store_probe [reps] [set: 1 = the side-buffer set only]
+//   rdH16/64  the read pass with the units over each frame's first 16 / 64 bytes loaded default-policy
+//             (the rest nt), so the heads may still be cached when a store pass follows; rdD: every unit
+//             default-policy
+// usage: store_probe [reps] [set: 1 = the side-buffer set only, 2 = the fill-floor set]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -307,6 +310,42 @@ __global__ __launch_bounds__(256) void k_side2line(uint8_t* buf, uint64_t n, con
     L[t % 4] = __builtin_nontemporal_load(side + i * 4 + t % 4);
 }
 
+// Read pass whose units overlapping the first HB bytes of each frame are
+// loaded with the default policy (the rest nt), so the frame heads — where
+// the fields are — may stay in L2 / MALL for a store pass right after it.
+template <uint32_t HB>
+__global__ __launch_bounds__(256) void k_rdhead(const uint8_t* buf, uint64_t n, uint64_t* sink) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t(blockIdx.x) * 256 + threadIdx.x) >> 6;
+    const uint64_t nw = uint64_t(gridDim.x) * 4;
+    const uint64_t tiles = n / 64;
+    uint32_t acc = 0;
+    for (uint64_t t = wave; t < tiles; t += nw) {
+        const uint64_t tb = reinterpret_cast<uint64_t>(buf) + t * 64 * kFrame;
+        const u32x4* base = reinterpret_cast<const u32x4*>(tb);
+        constexpr uint32_t units = 64 * kFrame / 16;
+        for (uint32_t u = lane; u < units; u += 64 * 8) {
+            u32x4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t uu = u + 64 * k;
+                if (uu < units) {
+                    // frame holding this unit's first byte, and the unit's offset from that frame's start
+                    const uint64_t a = tb + uint64_t(uu) * 16;
+                    const uint64_t fo = (a - reinterpret_cast<uint64_t>(buf)) % kFrame;
+                    const bool head = fo < HB || fo + 16 > kFrame;  // overlaps [frame, frame + HB)
+                    v[k] = head ? base[uu] : __builtin_nontemporal_load(base + uu);
+                } else {
+                    v[k] = u32x4{0, 0, 0, 0};
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
+        }
+    }
+    if (acc == 0x12345u) sink[0] = acc;
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? std::atoi(argv[1]) : 3;
     constexpr int R = 4;
@@ -343,6 +382,59 @@ int main(int argc, char** argv) {
     };
     u32x4* side;
     CK(hipMalloc(&side, kFrames * 64));
+    if (argc > 2 && std::atoi(argv[2]) == 2) {  // the fill's floor: does a cached frame head make the store pass cheap?
+        const unsigned g4 = g_frames * 4;
+        run("rd only", [&](uint8_t* b) { k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+        run("rdH16 only", [&](uint8_t* b) { k_rdhead<16><<<cus * 4, 256>>>(b, kFrames, sink); });
+        run("rdH64 only", [&](uint8_t* b) { k_rdhead<64><<<cus * 4, 256>>>(b, kFrames, sink); });
+        run("st2", [&](uint8_t* b) { k_st2<<<g_frames, 256>>>(b, kFrames, 0x1234); });
+        run("st64rw", [&](uint8_t* b) { k_st64rw<<<g4, 256>>>(b, kFrames, 0x1234); });
+        run("st64rw1", [&](uint8_t* b) { k_st64rw1<<<g_frames, 256>>>(b, kFrames, 0x1234); });
+        run("st16rw1", [&](uint8_t* b) { k_st16rw1<<<g_frames, 256>>>(b, kFrames, 0x1234); });
+        run("rd;st2", [&](uint8_t* b) {
+            k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st2<<<g_frames, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rd;st64rw", [&](uint8_t* b) {
+            k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st64rw<<<g4, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rd;st16rw1", [&](uint8_t* b) {
+            k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st16rw1<<<g_frames, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rdH16;st2", [&](uint8_t* b) {
+            k_rdhead<16><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st2<<<g_frames, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rdH64;st2", [&](uint8_t* b) {
+            k_rdhead<64><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st2<<<g_frames, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rdH64;st64rw", [&](uint8_t* b) {
+            k_rdhead<64><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st64rw<<<g4, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rdH64;st64rw1", [&](uint8_t* b) {
+            k_rdhead<64><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st64rw1<<<g_frames, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rdH64;st16rw1", [&](uint8_t* b) {
+            k_rdhead<64><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st16rw1<<<g_frames, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rdD only", [&](uint8_t* b) { k_rdhead<1500><<<cus * 4, 256>>>(b, kFrames, sink); });
+        run("rdD;st2", [&](uint8_t* b) {
+            k_rdhead<1500><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st2<<<g_frames, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rdD;st64rw", [&](uint8_t* b) {
+            k_rdhead<1500><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st64rw<<<g4, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rd only", [&](uint8_t* b) { k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+        return 0;
+    }
     if (argc > 2 && std::atoi(argv[2]) == 1) {  // side-buffer set only
         run("rd only", [&](uint8_t* b) { k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink); });
         run("rd;st2", [&](uint8_t* b) {
