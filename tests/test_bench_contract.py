@@ -79,3 +79,12 @@ def test_e2e_line_names_the_slowest_rank():
     assert s["slowest_rank"]["pci_bus_id"] == "0000:05:00.0"
     assert abs(s["sum_over_ranks_GiBps"] - (8 * 48 - 9)) < 1e-6 and len(s["per_rank_h2d_GBps"]) == 8
     assert abs(s["sum_h2d_GBps"] - (8 * 52.5 - 10)) < 1e-6
+    # the whole line, as test_bench_launcher's GPU test checks the real one
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_bench_launcher import check_e2e_line
+
+    for r in ranks:
+        r.update(cpus="0-7", pool_pages_by_node={"1": 512})
+        r["variants"]["C_strided_dma"]["GiBps_packet_bytes"] = float(r["variants"]["C_strided_dma"]["GiBps_packet_bytes"])
+    check_e2e_line({"n_gpus": 8, "best_variant": "C_strided_dma", "variants": {"C_strided_dma": {}}, "per_rank": ranks,
+                    "ranks_summary": s}, 8)

@@ -107,3 +107,32 @@ def test_torchrun_two_ranks_on_the_gpu():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and lines[0]["value"] > 0
     assert [x["rank"] for x in lines[0]["per_rank"]] == [0, 1]
+
+
+def check_e2e_line(d: dict, n: int) -> None:
+    """The cfg 5 line at N ranks: per rank H2D / D2H
+    GB/s per variant, its NUMA node and where its pinned pool's pages are;
+    the sum over ranks and the slowest rank named."""
+    assert d["n_gpus"] == n and d["best_variant"] in d["variants"]
+    pr = d["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(n))
+    for r in pr:
+        assert isinstance(r["numa_node"], int) and r["cpus"] and r["pool_pages_by_node"]
+        for v in r["variants"].values():
+            assert v["h2d_GBps"] > 0 and v["d2h_GBps"] > 0 and v["GiBps_packet_bytes"] > 0
+    s = d["ranks_summary"]
+    assert s["variant"] == d["best_variant"] and len(s["per_rank_h2d_GBps"]) == n
+    assert s["slowest_rank"]["rank"] in range(n) and s["slowest_rank"]["pci_bus_id"]
+    own = [r["variants"][s["variant"]]["GiBps_packet_bytes"] for r in pr]
+    assert abs(s["sum_over_ranks_GiBps"] - sum(own)) < 0.05 * n
+    assert s["slowest_rank"]["GiBps_packet_bytes"] == min(own)
+
+
+@pytest.mark.gpu
+def test_e2e_two_ranks_report_per_rank_pcie():
+    """cfg 5 with two ranks sharing the box's one GPU (--share-devices): the
+    line names the slowest rank and carries every rank's H2D / D2H rates."""
+    d = _bench("--gpus", "2", "--config", "e2e", "--steps", "4", "--warmup", "1", "--packets", "131072",
+               "--share-devices", timeout=400)
+    check_e2e_line(d, 2)
+    print(json.dumps(d["ranks_summary"]))
