@@ -885,51 +885,40 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
     const uint64_t rest = ntiles > nwaves ? ntiles - nwaves : 0;
     const uint32_t tiles_g = rest > grp ? static_cast<uint32_t>((rest - grp + kGroups - 1) / kGroups) : 0u;
     const uint32_t waves_g = static_cast<uint32_t>(nwaves / kGroups);
-    // A dequeue in two halves: claim_issue sends the atomic (lane 0) and
-    // returns at once; claim_take waits for its number — once the current
-    // tile's first loads are in flight — and, for the group's last number,
-    // resets the counter and reports the slot.
-    auto claim_issue = [&]() -> uint32_t {
-        uint32_t d = 0;
-        if (heads != nullptr && lane == 0) {
-            d = __hip_atomic_fetch_add(heads + grp * kHeadStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return d;
-    };
-    auto claim_take = [&](uint64_t prev, uint32_t d) -> uint64_t {
+    auto next_tile = [&](uint64_t prev) -> uint64_t {
         if (heads == nullptr) return prev + nwaves;
-        if (lane == 0 && d == tiles_g + waves_g - 1) {
-            // The slot's words are only ever touched by agent-scope atomics,
-            // which are performed at the device's coherence point; waiting
-            // for each to complete (s_waitcnt) orders reset -> count ->
-            // report without the L2 write-backs a release fence costs
-            // (profiles/r03_ab_pool_rows.log).
+        uint32_t d = 0;
+        if (lane == 0) {
             uint32_t* h = heads + grp * kHeadStride;
-            __hip_atomic_store(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            uint32_t* const groups_done = heads + kGroups * kHeadStride;
-            const uint32_t gd = __hip_atomic_fetch_add(groups_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (gd == kGroups - 1) {  // every group has reset: the slot is free for another launch
-                __hip_atomic_store(groups_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            d = __hip_atomic_fetch_add(h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (d == tiles_g + waves_g - 1) {
+                // The slot's words are only ever touched by agent-scope atomics,
+                // which are performed at the device's coherence point; waiting
+                // for each to complete (s_waitcnt) orders reset -> count ->
+                // report without the L2 write-backs a release fence costs
+                // (profiles/r03_ab_pool_rows.log).
+                __hip_atomic_store(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(done, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                uint32_t* const groups_done = heads + kGroups * kHeadStride;
+                const uint32_t gd = __hip_atomic_fetch_add(groups_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (gd == kGroups - 1) {  // every group has reset: the slot is free for another launch
+                    __hip_atomic_store(groups_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(done, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         }
         d = __builtin_amdgcn_readfirstlane(d);
         return d < tiles_g ? nwaves + grp + static_cast<uint64_t>(kGroups) * d : ntiles;
     };
-    // Tile pipeline, ONE tile ahead (round 4): while tile t streams, the next
-    // tile is claimed — the atomic goes out with t's first loads and is taken
-    // once they are in flight — and its plan (offset, length, seed) loads, so
-    // no tile starts on an exposed atomic or metadata round trip.  Round 2's
-    // form held TWO tiles ahead (the one after next dequeued at the top of
-    // each tile, blocking on the atomic): when the queue ran dry, a wave could
-    // still hold two unstarted 48 KiB tiles while others sat idle, and the
-    // launch's drain grew to two tile times (profiles/r04_ab_launch_len_terms.log:
-    // T(k batches) = 21 us + k x 223 us).  Every wave still makes exactly one
-    // failing dequeue (the counter reset relies on it).
+    // Two-deep tile pipeline: while tile t streams, the plan (offset, length,
+    // seed) of the next tile is already loading and the tile after it is being
+    // dequeued, so no tile starts on an exposed metadata or atomic round trip.
+    // Every wave still makes exactly one failing dequeue (the counter reset
+    // relies on it).
     uint64_t t = wglob;
-    if (t >= ntiles && heads != nullptr) t = claim_take(t, claim_issue());
+    if (t >= ntiles && heads != nullptr) t = next_tile(t);
+    uint64_t t1 = t < ntiles ? next_tile(t) : ntiles;
     auto plan_load = [&](uint64_t tt, uint64_t& o_, uint32_t& L_, uint32_t& sd_) {
         const TileRef tr = tile_ref(tt < ntiles ? tt : 0);
         const uint32_t qq = tr.q;
@@ -1019,18 +1008,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
     plan_load(t, o_n, L_n, sd_n);
     Tile cur{};
     while (t < ntiles) {
+        const uint64_t t2 = t1 < ntiles ? next_tile(t1) : ntiles;
         cur = derive(t, o_n, L_n, sd_n);
-        const uint32_t claim = claim_issue();
-        uint64_t t1 = ntiles;
-        bool claimed = false;
-        // after this tile's first loads are issued: take the claimed number and
-        // load that tile's plan (the registers derive() just consumed)
-        auto take_next = [&]() {
-            if (claimed) return;
-            claimed = true;
-            t1 = claim_take(t, claim);
-            if (t1 < ntiles) plan_load(t1, o_n, L_n, sd_n);
-        };
+        if (t1 < ntiles) plan_load(t1, o_n, L_n, sd_n);
         const uint64_t base = cur.base;
         const bool mine = cur.mine;
         const uint32_t L = cur.L, sd = cur.sd, head = cur.head, nunits = cur.nunits;
@@ -1088,7 +1068,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
             if (PIPE) {
                 u32x4 va[U], vb[U];
                 load(r, 0, va);
-                take_next();
                 for (uint32_t g = 0; g < ext; g += 2 * C) {
                     load(r, g + C, vb);
                     chunk(g, va);
@@ -1105,28 +1084,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
                     if (!short_chunks || left > C / 2) {
                         u32x4 v[U];
                         load(r, g, v);
-                        take_next();
                         chunk(g, v);
                     } else if (left > C / 4) {
                         u32x4 v[U / 2];
                         load(r, g, v);
-                        take_next();
                         chunk(g, v);
                     } else if (U < 8 || left > C / 8) {
                         u32x4 v[U / 4];
                         load(r, g, v);
-                        take_next();
                         chunk(g, v);
                     } else {
                         u32x4 v[U >= 8 ? U / 8 : 1];
                         load(r, g, v);
-                        take_next();
                         chunk(g, v);
                     }
                 }
             }
         }
-        take_next();  // (a tile that streamed nothing)
         const uint32_t res = pend - pst;  // sum of the packet's units, mod 2^32
         if (IPV4 && huge && mine && !range_bad) {  // not streamed (phase D redoes its sum): head units from the frame
             const auto* hu = reinterpret_cast<const u32x4*>(a0);
@@ -1295,6 +1269,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
             if (status) tile_store(status + base, lane, static_cast<uint8_t>(st), pol_st);
         }
         t = t1;
+        t1 = t2;
     }
 }
 
