@@ -769,6 +769,15 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
     }
 }
 
+#ifdef SCCSUM_AB_TIMELINE
+// A/B diagnostic only (tools/build_ab.sh timeline=SCCSUM_AB_TIMELINE,
+// tools/dev/timeline_probe.py): per wave of the last flat launch, the
+// constant-clock times (100 MHz) of its start, its first chunk's data in
+// registers, its failing dequeue, and its tile count.
+constexpr uint32_t kTimelineWaves = 16384;
+__device__ unsigned long long g_timeline[kTimelineWaves][4];
+#endif
+
 constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B) between packets
 
 // The batches one flat-kernel launch works through: up to kMaxQueues
@@ -1007,7 +1016,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
     uint32_t L_n = 0, sd_n = 0;
     plan_load(t, o_n, L_n, sd_n);
     Tile cur{};
+#ifdef SCCSUM_AB_TIMELINE
+    const unsigned long long tl_start = wall_clock64();
+    unsigned long long tl_first = 0, tl_tiles = 0;
+#endif
     while (t < ntiles) {
+#ifdef SCCSUM_AB_TIMELINE
+        ++tl_tiles;
+#endif
         const uint64_t t2 = t1 < ntiles ? next_tile(t1) : ntiles;
         cur = derive(t, o_n, L_n, sd_n);
         if (t1 < ntiles) plan_load(t1, o_n, L_n, sd_n);
@@ -1064,6 +1080,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
                     hl = ubuf[b];
                 }
                 __builtin_amdgcn_wave_barrier();  // this chunk's LDS reads precede the next chunk's writes
+#ifdef SCCSUM_AB_TIMELINE
+                if (tl_first == 0) tl_first = wall_clock64();
+#endif
             };
             if (PIPE) {
                 u32x4 va[U], vb[U];
@@ -1271,6 +1290,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
         t = t1;
         t1 = t2;
     }
+#ifdef SCCSUM_AB_TIMELINE
+    if (lane == 0 && wglob < kTimelineWaves) {
+        g_timeline[wglob][0] = tl_start;
+        g_timeline[wglob][1] = tl_first;
+        g_timeline[wglob][2] = wall_clock64();
+        g_timeline[wglob][3] = tl_tiles;
+    }
+#endif
 }
 
 // Fragment lists (checksummer::sum(const packet&), src/net/ip_checksum.cc:64-68):
@@ -2473,6 +2500,14 @@ int sccsum_set_tail_split(int split, int quarters) {
 }
 
 int sccsum_sync(void* stream) { return static_cast<int>(hipStreamSynchronize(static_cast<hipStream_t>(stream))); }
+
+#ifdef SCCSUM_AB_TIMELINE
+// A/B builds only: the per-wave timeline of the last flat launch (4 u64 per wave).
+int sccsum_ab_timeline(void* host, uint64_t bytes) {
+    const uint64_t n = bytes < sizeof(sccsum::g_timeline) ? bytes : sizeof(sccsum::g_timeline);
+    return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(sccsum::g_timeline), n, 0, hipMemcpyDeviceToHost));
+}
+#endif
 
 int sccsum_read_probe_blocks(void) { return sccsum::current_cu_count() * sccsum::kBlocksPerCU; }
 
