@@ -18,6 +18,12 @@ ORDER = ["headline", "udp1500", "udp1500_launch_single", "mixed", "mixed_align_6
 
 def lines(d: str) -> dict[str, dict]:
     out = {}
+    # a prof: step's trace pass prints the bench line of the profiled command (--steps 10)
+    for f in sorted(glob.glob(os.path.join(d, "prof_*_trace.log"))):
+        name = os.path.basename(f)[len("prof_"):-len("_trace.log")]
+        for ln in open(f):
+            if ln.startswith("{"):
+                out[name] = json.loads(ln)
     for f in sorted(glob.glob(os.path.join(d, "bench_*.log"))):
         name = os.path.basename(f)[len("bench_"):-len(".log")]
         for ln in open(f):
