@@ -91,6 +91,11 @@ def parse():
                     help="A/B: grid cap in workgroups per CU (sccsum_set_blocks_per_cu)")
     ap.add_argument("--out-policy", type=int, default=None,
                     help="A/B: cache policy of the flat kernel's result stores (sccsum_set_out_policy)")
+    ap.add_argument("--engine-in-flight", type=int, default=2,
+                    help="--launch engine: steps published ahead of the grid (max_in_flight)")
+    ap.add_argument("--engine-wt", type=int, default=None,
+                    help="A/B: engine result stores written through (1) or stored as a launch does (0) "
+                         "(sccsum_set_engine_write_through)")
     ap.add_argument("--run-align", type=int, default=None, help="A/B: run-start alignment in units (sccsum_set_run_align)")
     ap.add_argument("--sync", default="auto", choices=["auto", "spin", "yield"],
                     help="how the host thread waits on the device (hipSetDeviceFlags schedule)")
@@ -100,11 +105,12 @@ def parse():
     ap.add_argument("--streams", type=int, default=1,
                     help="udp1500 / mixed / fill: step k launches on stream k %% S (A/B: with 2, consecutive steps' "
                          "launches run concurrently)")
-    ap.add_argument("--launch", default=None, choices=["multi", "single"],
+    ap.add_argument("--launch", default=None, choices=["multi", "single", "engine"],
                     help="udp1500 / mixed: one sccsum_ipv4_frames_multi launch per step over the tx and rx batches "
                          "(multi; udp1500's default) or one sccsum_ipv4_frames launch per batch (single; mixed: "
                          "the rx batch only, mixed's default — its multi step measured 1-2 %% slower on three "
-                         "boxes, DESIGN.md §5.3)")
+                         "boxes, DESIGN.md §5.3); engine = one resident grid per timed run, the steps submitted "
+                         "into it as they go, at most 2 in flight (sccsum_engine_*, DESIGN.md §5.11)")
     ap.add_argument("--rx-out2", action="store_true",
                     help="udp1500 / mixed: the verify (rx) half also writes both checksums per frame (default: status "
                          "bits only, what the reference's verify keeps: ip.cc:121-127, tcp.hh:876-883)")
@@ -355,7 +361,8 @@ def cpu_baseline(tx, budget_s: float):
     per_core = vn / max(threads, 1)
     per_ccd = vccd if vccd else per_core * max(len(one_ccd), 1)
     cands = [per_core * host_cores] + ([per_ccd * host_ccds] if host_ccds else [])
-    all_cores = min(cands) if host_cores else None
+    # never below what the pinned threads measured (with every host core pinned, the projection is that run)
+    all_cores = max(min(cands), vn) if host_cores else None
     return {
         "value": round(vn, 3),
         "unit": "GiB/s",
@@ -433,7 +440,7 @@ def make_streams(args, dev):
 OWN = {}  # this rank's own timing of the last timed() region (per_rank diagnostics)
 
 
-def timed(step, steps, warmup, world, streams):
+def timed(step, steps, warmup, world, streams, begin=None, end=None):
     """Warm up, then time `steps` calls bracketed by barrier + sync; returns
     (max-over-ranks wall seconds, seconds per step from ONE pair of HIP events
     around the timed launches: the start event on streams[0], which every other
@@ -444,8 +451,13 @@ def timed(step, steps, warmup, world, streams):
     streams = streams if isinstance(streams, (list, tuple)) else [streams]
     s0 = streams[0]
     torch.cuda.synchronize()  # inputs built on the default stream are complete before any step stream reads them
-    for k in range(warmup):
-        step(k)
+    if warmup:
+        if begin:  # (--launch engine: a run of its own)
+            begin()
+        for k in range(warmup):
+            step(k)
+        if end:
+            end()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world)
@@ -454,8 +466,12 @@ def timed(step, steps, warmup, world, streams):
     e0.record(s0)
     for s in streams[1:]:
         s.wait_event(e0)
+    if begin:  # --launch engine: the grid's launch (and its counters' reset) is inside the timed region
+        begin()
     for k in range(warmup, warmup + steps):
         step(k)
+    if end:
+        end()
     for s in streams[1:]:
         ev = torch.cuda.Event()
         ev.record(s)
@@ -583,9 +599,14 @@ def run_udp1500(args, world, rank, dev):
         rxs.append(rx)
         sts.append(torch.empty(n, dtype=torch.uint8, device=dev))
     multi = args.launch == "multi"
-    per_step = 1 if multi else 2  # launches per step
+    engine = args.launch == "engine"
+    per_step = 1 if (multi or engine) else 2  # launches per step
     if multi:  # the tx and rx batches of a step form ONE launch of 2 * n frames
         kern = flat_kernel(True, False, 2 * n, 2 * n * FRAME)
+    if engine:  # one resident grid per run; each step (tx + rx batch) submitted into it
+        kern = "csum_engine_kernel<16, true>"
+        streams = streams[:1]
+        ns = 1
 
     # multi: each (rotation, stream) pair's launch is prebuilt, so a step only
     # crosses the C-ABI (no per-step Python argument marshalling)
@@ -597,37 +618,61 @@ def run_udp1500(args, world, rank, dev):
                 pre[(r, i)] = batch.prepare_ipv4_frames_multi([(txs[r], o_tx, None),
                                                                (rxs[r], o_rx if args.rx_out2 else None, sts[r])])
 
+    warm = max(args.warmup, R)
+    eng = begin = end = None
+    if engine:
+        eng = batch.Engine(dev.index or 0, frames=True, max_steps=max(warm, args.steps) + 4,
+                           max_in_flight=args.engine_in_flight)
+        o_tx, o_rx = outs[0]
+        pre = {r: eng.prepare([(txs[r], o_tx, None), (rxs[r], o_rx if args.rx_out2 else None, sts[r])])
+               for r in range(R)}
+
+        def begin():
+            eng.start(streams[0])
+
+        def end():
+            eng.stop()
+
     def step(k):
         r = k % R
         s = streams[k % ns]
         o_tx, o_rx = outs[k % ns]
-        if multi:
+        if engine:
+            eng.submit_prepared(pre[r])
+        elif multi:
             pre[(r, k % ns)](s)
         else:
             batch.ipv4_frames(txs[r], out2=o_tx, stream=s)
             batch.ipv4_frames(rxs[r], out2=o_rx, status=sts[r], stream=s)
 
-    warm = max(args.warmup, R)
     torch.cuda.synchronize()  # the batches were built on the default stream
+    if begin:
+        begin()
     for k in range(warm):
         step(k)
-    LAUNCHES.add(kern, per_step * warm)
+    if end:
+        end()
+    LAUNCHES.add(kern, 1 if engine else per_step * warm)
     torch.cuda.synchronize()
     # sanity: every uncorrupted rx frame verifies, every corrupted one fails; the tx outputs match the generate pass
     for st_rx in sts:
         n_fail = int(((st_rx & 2) == 0).sum())
         assert args.no_check or n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
-    sel = LAUNCHES.select(kern, per_step * args.steps)
-    wall, step_s = timed(step, args.steps, 0, world, streams)
-    LAUNCHES.add(kern, per_step * args.steps)
+    sel = LAUNCHES.select(kern, 1 if engine else per_step * args.steps)
+    wall, step_s = timed(step, args.steps, 0, world, streams, begin, end)
+    LAUNCHES.add(kern, 1 if engine else per_step * args.steps)
     avg_launch_s = step_s / per_step
     stream = streams[0]
 
     value = world * 2 * n * FRAME * args.steps / wall / 2**30
     # per launch: every frame byte + 12 B metadata + the results written: tx 4 B (IP, UDP checksums), rx 1 B
     # of status bits (+ 4 B with --rx-out2; --launch single always writes both)
-    rx_out = 4 if (args.rx_out2 or not multi) else 0
+    rx_out = 4 if (args.rx_out2 or not (multi or engine)) else 0
     alg = (n * (FRAME + META_BYTES + 4) + n * (FRAME + META_BYTES + 1 + rx_out)) // per_step
+    roof_alg, roof_s = alg, avg_launch_s
+    if engine:  # the launch is the run: every step's bytes over the run's time (the same ratio)
+        roof_alg, roof_s = alg * args.steps, avg_launch_s * args.steps
+        eng.close()
     ceiling = read_ceiling(txs[0].data, txs[0].bytes_len, stream)
     ranks = per_rank(world, rank, dev, **rank_rate(2 * n * FRAME, args.steps), avg_launch_us=avg_launch_s * 1e6,
                      read_ceiling_GBps=ceiling, frac=alg / avg_launch_s / 1e9 / HBM_PEAK_GBPS)
@@ -640,12 +685,16 @@ def run_udp1500(args, world, rank, dev):
                           "step = generate (IP+UDP csum) + verify (1% corrupted) pass",
               "packets_per_gpu": n, "frame_bytes": FRAME,
               "launch": ("one sccsum_ipv4_frames_multi launch per step over the tx and rx batches" if multi
-                         else "one sccsum_ipv4_frames launch per batch (2 per step)"),
+                         else ("one resident engine grid per timed run (sccsum_engine_*): each step's tx and rx "
+                               f"batches submitted into it as one step, at most {args.engine_in_flight} steps in flight" if engine
+                               else "one sccsum_ipv4_frames launch per batch (2 per step)")),
               "rotation": f"{R} distinct tx/rx batch pairs launched in turn ({2 * R * n * FRAME / 1e9:.1f} GB per GPU)",
               "streams": f"{ns} (step k on stream k % {ns})",
               "global_batch": n * world, "parallelism": f"{world} independent shards, no collective"},
-             roofline(alg, avg_launch_s, "udp1500", kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi
-                                                                   else " (sccsum_ipv4_frames)"), sel, args,
+             roofline(roof_alg, roof_s, "udp1500" if not engine else "udp1500_engine",
+                      kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi else
+                              (" (sccsum_engine_*, tx + rx per step; one launch = the timed run)" if engine
+                               else " (sccsum_ipv4_frames)")), sel, args,
                       {"measured_read_ceiling_GBps": round(ceiling, 1)}), cpu, extra={"per_rank": ranks})
 
 
@@ -1161,6 +1210,9 @@ def main():
             native.check(native.load().sccsum_set_blocks_per_cu(args.blocks_per_cu), "sccsum_set_blocks_per_cu")
         if args.out_policy is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_out_policy(args.out_policy), "sccsum_set_out_policy")
+        if args.engine_wt is not None:  # A/B only (sccsum_diag.h)
+            native.check(native.load().sccsum_set_engine_write_through(args.engine_wt),
+                         "sccsum_set_engine_write_through")
         if args.run_align is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_run_align(args.run_align), "sccsum_set_run_align")
         {"udp1500": run_udp1500, "tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e, "fill": run_fill,

@@ -91,6 +91,7 @@ extern "C" {
 #define SCCSUM_EINVAL (-1)   /* bad argument (null pointer, misalignment) */
 #define SCCSUM_ENODEV (-2)   /* no HIP device / device index out of range */
 #define SCCSUM_EBUSY  (-3)   /* burst queue: every batch slot is in flight; poll and retry */
+#define SCCSUM_EIDLE  (-4)   /* engine: its grid gave up waiting for steps (idle limit); start a new run */
 
 /* per-packet status bits (d_status) */
 #define SCCSUM_ST_OK        0x01u /* spans: result == 0; frames: IPv4 header verifies */
@@ -193,6 +194,48 @@ typedef struct sccsum_batch {
 
 int sccsum_spans_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len, void* stream);
 int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len, void* stream);
+
+/* ---- Resident engine: steps streamed into a running grid -------------------
+ * A launch pays a fixed cost — the grid's ramp, the drain of its last tiles
+ * and the kernel boundary, ~18-21 us on MI355X — on every call.
+ * An engine launches ONE grid that stays resident and takes STEPS from the
+ * host while it runs, the way Seastar's reactor keeps polling its queues
+ * (src/core/reactor.cc:3543-3550): each step is up to SCCSUM_ENGINE_MAX_BATCHES
+ * batches (a step's tx and rx halves, a shard's rx queues), computed exactly
+ * as sccsum_*_multi would compute them, and its tiles flow into the same
+ * grid without a boundary.  Per step the engine reports completion; its
+ * results are written through to device memory, so they may be read (any
+ * stream, hipMemcpy) as soon as sccsum_engine_wait returns for it.
+ *
+ *   sccsum_engine_create(device, mode, max_steps, max_in_flight, &e)
+ *       mode SCCSUM_PIPE_IPV4 (frames) or SCCSUM_PIPE_SPANS; at most
+ *       max_steps steps per run (descriptors are never reused within a run:
+ *       max_steps x 512 B of pinned memory), at most max_in_flight (1..64)
+ *       submitted and not yet done.
+ *   sccsum_engine_start(e, stream)      launch the grid on `stream` (a run)
+ *   sccsum_engine_submit(e, batches, nbatch, max_len, timeout_ns, &step)
+ *       publish one step; waits (spinning, up to timeout_ns) while
+ *       max_in_flight steps are pending.  SCCSUM_EBUSY: the run already took
+ *       max_steps steps (stop and start a new run) or the wait timed out.
+ *   sccsum_engine_wait(e, step, timeout_ns)   0 once the step is done
+ *   sccsum_engine_stop(e)               no more steps: the grid leaves once the
+ *       published steps are done (synchronise `stream` to wait for it)
+ *   sccsum_engine_destroy(e)            stops and synchronises a running engine
+ *
+ * The grid holds the device's compute units while it runs (every CU, all of
+ * their LDS): other kernels on the device wait for the run to stop.  A grid
+ * left without steps and without a stop for 1 s leaves on its own, and every
+ * later call on that run returns SCCSUM_EIDLE.  One engine belongs to one host
+ * thread, like a burst queue. */
+#define SCCSUM_ENGINE_MAX_BATCHES 4
+typedef struct sccsum_engine sccsum_engine;
+int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, sccsum_engine** out);
+int sccsum_engine_start(sccsum_engine* e, void* stream);
+int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
+                         uint64_t timeout_ns, uint64_t* step);
+int sccsum_engine_wait(sccsum_engine* e, uint64_t step, uint64_t timeout_ns);
+int sccsum_engine_stop(sccsum_engine* e);
+int sccsum_engine_destroy(sccsum_engine* e);
 
 /* Checksum n packets that are FRAGMENT LISTS, like checksummer::sum(const
  * packet&) (src/net/ip_checksum.cc:64-68): packet i is the concatenation of

@@ -58,6 +58,10 @@ int sccsum_set_tail_split(int split, int quarters);
  * store; buffer stores with 1 = nt, the default, 2 = sc1, 3 = sc0 sc1,
  * 4 = sc0).  SCCSUM_EINVAL outside 0..4. */
 int sccsum_set_out_policy(int policy);
+/* Engine result stores: written through, sc0 sc1 (1, default), or stored as a
+ * launch stores them (out_policy and the 128-byte rule) with an agent-scope
+ * release before each step's completion count (0).  A/B only. */
+int sccsum_set_engine_write_through(int on);
 
 /* Flat kernel forms without a chunk in flight (U 8 form 14, U 16): a run's
  * last chunk loads and scans only the rows its units reach, U / 8 .. U (1, the

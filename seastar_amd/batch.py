@@ -423,3 +423,93 @@ def as_u16(t: torch.Tensor) -> np.ndarray:
 
 def pseudo_seed(src_host: int, dst_host: int, proto: int, length: int) -> int:
     return int(native.load().sccsum_pseudo_seed(src_host, dst_host, proto, length & 0xFFFF))
+
+
+class Engine:
+    """sccsum_engine_*: ONE resident grid that takes steps (up to 4 batches
+    each: a step's tx and rx halves, a shard's rx queues) while it runs, so the
+    launch's ramp, drain and kernel boundary are paid once per run instead of
+    once per step (include/sccsum.h, "Resident engine").
+
+        eng = Engine(device=0, frames=True, max_steps=1024, max_in_flight=2)
+        eng.start(stream)
+        step = eng.submit([(tx, out2, None), (rx, None, status)])   # like prepare_ipv4_frames_multi's items
+        eng.wait(step)                                               # results readable on any stream
+        eng.stop(); stream.synchronize()
+
+    A step's tensors must stay alive (and unmodified) until its wait returns;
+    submit keeps a reference until then."""
+
+    def __init__(self, device: int = 0, frames: bool = True, max_steps: int = 1024, max_in_flight: int = 2):
+        self._lib = native.load()
+        h = ctypes.c_void_p()
+        native.check(self._lib.sccsum_engine_create(int(device), native.PIPE_IPV4 if frames else native.PIPE_SPANS,
+                                                     int(max_steps), int(max_in_flight), ctypes.byref(h)),
+                     "sccsum_engine_create")
+        self._h = h
+        self.frames = frames
+        self.max_in_flight = int(max_in_flight)
+        self._keep: dict[int, tuple] = {}
+        self._stream = None
+
+    def start(self, stream=None):
+        s = torch.cuda.current_stream() if stream is None else stream
+        native.check(self._lib.sccsum_engine_start(self._h, s.cuda_stream), "sccsum_engine_start")
+        self._stream = s
+        self._keep.clear()
+
+    def prepare(self, items):
+        """A step's descriptor array, checked once (items as for
+        prepare_ipv4_frames_multi: (PacketBatch, out | None, status | None
+        [, seeds])); submit_prepared(prep) then only crosses the C-ABI."""
+        if not items or len(items) > native.ENGINE_MAX_BATCHES:
+            raise ValueError(f"1..{native.ENGINE_MAX_BATCHES} batches per step")
+        width = 2 if self.frames else 1
+        arr = (native.Batch * len(items))()
+        ml = 0
+        for i, it in enumerate(items):
+            b, out, status = it[0], it[1], it[2]
+            seeds = it[3] if len(it) > 3 else None
+            if self.frames and seeds is not None:
+                raise ValueError("frames take no seeds")
+            if out is None and status is None:
+                raise ValueError(f"batch {i}: give out, status or both")
+            _need(out, width * b.n, torch.int16, f"batch {i} out", b.device)
+            _need(status, b.n, torch.uint8, f"batch {i} status", b.device)
+            _need(seeds, b.n, torch.int32, f"batch {i} seeds", b.device)
+            arr[i] = native.Batch(ctypes_ptr(b.data), b.bytes_len, ctypes_ptr(b.off), ctypes_ptr(b.length),
+                                  _ptr(seeds), _ptr(out), _ptr(status), b.n)
+            ml = max(ml, b.max_len)
+        return (arr, len(items), ml, items)
+
+    def submit_prepared(self, prep, timeout_s: float = 10.0) -> int:
+        arr, nb, ml, items = prep
+        step = ctypes.c_uint64()
+        native.check(self._lib.sccsum_engine_submit(self._h, ctypes.cast(arr, ctypes.c_void_p), nb, ml,
+                                                     int(timeout_s * 1e9), ctypes.byref(step)),
+                     "sccsum_engine_submit")
+        self._keep[step.value] = prep
+        for s in [k for k in self._keep if k + self.max_in_flight < step.value]:
+            del self._keep[s]  # done: submit waited for it
+        return step.value
+
+    def submit(self, items, timeout_s: float = 10.0) -> int:
+        return self.submit_prepared(self.prepare(items), timeout_s)
+
+    def wait(self, step: int, timeout_s: float = 10.0) -> None:
+        native.check(self._lib.sccsum_engine_wait(self._h, int(step), int(timeout_s * 1e9)), "sccsum_engine_wait")
+
+    def stop(self) -> None:
+        native.check(self._lib.sccsum_engine_stop(self._h), "sccsum_engine_stop")
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.sccsum_engine_destroy(self._h)
+            self._h = None
+            self._keep.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

@@ -27,6 +27,9 @@
 
 #include <atomic>
 #include <cctype>
+#include <chrono>
+#include <cstring>
+#include <new>
 #include <cstdint>
 #include <cstdio>
 #include <mutex>
@@ -52,6 +55,8 @@ constexpr uint32_t kFlagFillIp = 4;  // frames (with kFlagFillL4): also generate
 constexpr uint32_t kFlagFillIcmp = 8;  // frames: turn ICMP echo requests into replies in place (ip.cc:464-474)
 constexpr uint32_t kFillFlags = kFlagFillL4 | kFlagFillIcmp;  // the in-place (FILL) instantiation
 constexpr uint32_t kFlagFullChunks = 16;  // flat kernel: a run's last chunk loads all U rows (diagnostic A/B)
+constexpr uint32_t kFlagEngineWT = 32;    // engine: results written through (sc0 sc1), else stored by the launch
+                                          // rule and released (agent scope) before a step's count
 constexpr uint32_t kRunAlignShift = 12;   // flat kernel, flags bits 12-13: run extents start on 1 / 4 / 8-unit boundaries
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -102,8 +107,24 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
            static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 48));
 }
 
+// Global (address space 1) views of device pointers.  A pointer the compiler
+// cannot place — one read from memory or made from an integer, like the
+// engine's descriptor fields — would otherwise be accessed as FLAT, and one
+// FLAT access in flight makes every later wait a full vmcnt(0): a chunk then
+// waits for all of its loads before summing the first (measured: the engine
+// ran 15 % slower than a launch until its pointers were cast, profiles/r04j).
+#define SCCSUM_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ const SCCSUM_GLOBAL T* gld(const T* p) {
+    return (const SCCSUM_GLOBAL T*)p;
+}
+template <typename T>
+__device__ __forceinline__ SCCSUM_GLOBAL T* gst(T* p) {
+    return (SCCSUM_GLOBAL T*)p;
+}
+
 __device__ __forceinline__ u32x4 load_unit(const uint8_t* p) {
-    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return __builtin_nontemporal_load(gld(reinterpret_cast<const u32x4*>(p)));
 }
 
 // Logical block id with XCD affinity: blocks b, b+8, b+16 ... are dealt to one
@@ -548,7 +569,7 @@ constexpr uint32_t kOutPolicyShift = 8;
 template <typename T>
 __device__ __forceinline__ void tile_store(T* t, uint32_t lane, T v, uint32_t pol) {
     if (pol == 0) {
-        t[lane] = v;
+        gst(t)[lane] = v;
         return;
     }
     const auto r = rsrc(reinterpret_cast<const uint8_t*>(t), 64u * sizeof(T));
@@ -776,6 +797,9 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
 // registers, its failing dequeue, and its tile count.
 constexpr uint32_t kTimelineWaves = 16384;
 __device__ unsigned long long g_timeline[kTimelineWaves][4];
+// engine runs: per wave, [waits that slept, ticks asleep, published reloads,
+// descriptor walks, ticks in walks, flushes, ticks in flushes, -]
+__device__ unsigned long long g_engine_stats[kTimelineWaves][8];
 #endif
 
 constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B) between packets
@@ -825,45 +849,46 @@ struct Queues {
 // (waves_per_eu: the U = 8 forms fit 168 VGPRs and keep 3 waves per SIMD —
 // the in-place form with a chunk in flight needed 172 without the bound; the
 // U = 16 forms are held to 2 by their LDS anyway)
-template <int U, bool IPV4, bool FILL, bool PIPE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 ? 2 : 3))) void csum_flat_kernel(const Queues Q, uint32_t B, uint32_t* __restrict__ heads,
-                                                          uint32_t* __restrict__ done, uint32_t ticket,
-                                                          uint32_t flags, const RssParams rss) {
-    static_assert(!FILL || IPV4, "in-place generate is a frames mode");
-    constexpr uint32_t C = kWave * U;  // units per chunk
-    constexpr uint32_t kLdsUnits = C;
-    constexpr int kHead = FILL ? 4 : (IPV4 ? 3 : 1);
-    const bool short_chunks = (flags & kFlagFullChunks) == 0;
-    // a run's streamed extent starts on a 64 / 128-byte boundary (clamped to
-    // the batch's first unit), so each 1 KiB load row covers whole lines
-    const uint32_t ra_code = (flags >> kRunAlignShift) & 3u;
-    const uint64_t ra_mask = ra_code == 0 ? 0ull : (ra_code == 1 ? 3ull : 7ull);
-    const bool raw = !IPV4 && (flags & kFlagRaw);
-    const bool fill_ip = FILL && (flags & kFlagFillIp);
-    const bool fill_l4 = FILL && (flags & kFlagFillL4);
-    const bool fill_icmp = FILL && (flags & kFlagFillIcmp);
-    __shared__ u32x4 ubuf_all[kWavesPerBlock][kLdsUnits];
-    __shared__ uint32_t pbuf_all[kWavesPerBlock][kLdsUnits];
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    u32x4* ubuf = ubuf_all[wv];
-    uint32_t* pbuf = pbuf_all[wv];
-    const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
-    // B packets per whole tile, numbered across the queues; the tail's whole
-    // tiles count 2^sub_log2 virtual tiles each
-    const uint64_t ntiles = Q.tsplit + ((Q.tile0[Q.nq] - Q.tsplit) << Q.sub_log2);
-    const uint32_t vo = 16u * lane;
-    // (wave-uniform) virtual tile tt -> its queue, first packet and packet
-    // count (0 for a sub-tile past the end of a short last tile): a scalar
-    // walk over <= kMaxQueues prefixes
-    struct TileRef {
+// A flat launch's tiles come from a tile SOURCE: QueueSrc (one launch over
+// the queue set in its arguments, csum_flat_kernel) or EngineSrc (a resident
+// grid fed steps through a ring, csum_engine_kernel, §5.11 of DESIGN.md).
+// Both give the same body (flat_body) a tile's batch and packet range (Ref),
+// the next tile number to work on, and what to do once a tile is stored.
+struct QueueSrc {
+    static constexpr bool kEngine = false;
+    const Queues& Q;
+    const uint32_t B;
+    uint32_t* const heads;
+    uint32_t* const done;
+    const uint32_t ticket;
+    uint64_t ntiles = 0, nwaves = 0, wglob = 0;
+    uint32_t grp = 0, tiles_g = 0, waves_g = 0, lane = 0;
+    struct Ref {
         uint32_t q, cnt;
         uint64_t base;
     };
-    auto tile_ref = [&](uint64_t tt) -> TileRef {
+    __device__ QueueSrc(const Queues& q, uint32_t b, uint32_t* h, uint32_t* d, uint32_t tk)
+        : Q(q), B(b), heads(h), done(d), ticket(tk) {}
+    __device__ void init(uint64_t wglob_, uint64_t nwaves_, uint32_t lane_) {
+        // B packets per whole tile, numbered across the queues; the tail's whole
+        // tiles count 2^sub_log2 virtual tiles each
+        ntiles = Q.tsplit + ((Q.tile0[Q.nq] - Q.tsplit) << Q.sub_log2);
+        nwaves = nwaves_;
+        wglob = wglob_;
+        lane = lane_;
+        grp = static_cast<uint32_t>(wglob % kGroups);
+        const uint64_t rest = ntiles > nwaves ? ntiles - nwaves : 0;
+        tiles_g = rest > grp ? static_cast<uint32_t>((rest - grp + kGroups - 1) / kGroups) : 0u;
+        waves_g = static_cast<uint32_t>(nwaves / kGroups);
+    }
+    __device__ uint64_t end() const { return ntiles; }
+    // (wave-uniform) virtual tile tt -> its queue, first packet and packet
+    // count (0 for a sub-tile past the end of a short last tile): a scalar
+    // walk over <= kMaxQueues prefixes
+    __device__ Ref ref(uint64_t tt) const {
         const bool sub = tt >= Q.tsplit;
         const uint64_t w = sub ? Q.tsplit + ((tt - Q.tsplit) >> Q.sub_log2) : tt;
-        TileRef r;
+        Ref r;
         r.q = 0;
         while (r.q + 1 < Q.nq && w >= Q.tile0[r.q + 1]) ++r.q;
         r.base = (w - Q.tile0[r.q]) * B;
@@ -876,7 +901,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
             r.cnt = c < Q.bsub ? c : Q.bsub;
         }
         return r;
-    };
+    }
+    __device__ const uint8_t* bytes(const Ref& r) const { return Q.bytes[r.q]; }
+    __device__ uint64_t bytes_len(const Ref& r) const { return Q.bytes_len[r.q]; }
+    __device__ const uint64_t* off(const Ref& r) const { return Q.off[r.q]; }
+    __device__ const uint32_t* len(const Ref& r) const { return Q.len[r.q]; }
+    __device__ const uint32_t* seed(const Ref& r) const { return Q.seed[r.q]; }
+    __device__ uint16_t* out(const Ref& r) const { return Q.out[r.q]; }
+    __device__ uint8_t* status(const Ref& r) const { return Q.status[r.q]; }
+    __device__ uint32_t tile_packets(const Ref&) const { return B; }
 
     // Tile order.  Wave w first takes tile w (static: no start-up contention).
     // With `heads`, the remaining tiles [W, ntiles) are split over kGroups
@@ -889,12 +922,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
     // the last group to do so stores this launch's ticket to `done` (pinned
     // host memory): the host may then hand the slot to another launch
     // (acquire_heads).  Without `heads`: static round robin.
-    const uint64_t wglob = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
-    const uint32_t grp = static_cast<uint32_t>(wglob % kGroups);
-    const uint64_t rest = ntiles > nwaves ? ntiles - nwaves : 0;
-    const uint32_t tiles_g = rest > grp ? static_cast<uint32_t>((rest - grp + kGroups - 1) / kGroups) : 0u;
-    const uint32_t waves_g = static_cast<uint32_t>(nwaves / kGroups);
-    auto next_tile = [&](uint64_t prev) -> uint64_t {
+    __device__ uint64_t claim(uint64_t prev) {
         if (heads == nullptr) return prev + nwaves;
         uint32_t d = 0;
         if (lane == 0) {
@@ -919,49 +947,322 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
         }
         d = __builtin_amdgcn_readfirstlane(d);
         return d < tiles_g ? nwaves + grp + static_cast<uint64_t>(kGroups) * d : ntiles;
+    }
+    __device__ uint64_t first() {
+        uint64_t t = wglob;
+        if (t >= ntiles && heads != nullptr) t = claim(t);
+        return t;
+    }
+    // every tile of the launch is known at launch: nothing to wait for
+    __device__ bool ready(uint64_t) { return true; }
+    __device__ bool wait_ready(uint64_t) { return true; }
+    __device__ void retire(const Ref&) {}
+};
+
+// ---- the resident engine (sccsum_engine_*)
+//
+// One grid stays resident and takes STEPS — up to kEngineQueues batches each,
+// the tx and rx halves of a step, a shard's rx queues — that the host
+// publishes while it runs.  A step is a 512-byte descriptor in pinned host
+// memory (one 8-byte word per lane, read with system-scope loads); its tiles
+// continue the run's global tile numbering, so tile v of the run is claimed
+// from group counter v % kGroups exactly as in a launch, and step boundaries
+// cost nothing: no kernel boundary, no ramp, no drain between steps.  The
+// host publishes a step by raising `published_tiles` (ctl[0]) after its
+// descriptor is written; a wave that claims a tile past it finishes the tile
+// it holds first and only then waits (sleeping), so a wave never waits while
+// it holds published work.  Each tile's results are written through (sc0 sc1)
+// and counted per step and group; the last tile of a step stores the step's
+// ticket into its pinned done word.  Exit: the host sets stop (ctl[8]); a
+// wave that needs a tile past every published step then leaves — and so does
+// one that has waited `idle_ticks` with no stop (it raises ctl[9] first).
+constexpr uint32_t kEngineQueues = 4;
+constexpr uint32_t kEngineSlotWords = 64;  // 512-byte descriptors
+constexpr uint32_t kEngineCountSlots = 64;  // completion counters: steps in flight at most
+// descriptor words
+constexpr uint32_t kEdFirst = 0;   // the step's first tile in the run
+constexpr uint32_t kEdTiles = 1;   // tiles | B (packets per tile) << 32
+constexpr uint32_t kEdStep = 2;    // the step's index in the run
+constexpr uint32_t kEdNq = 3;      // batches in the step (1..kEngineQueues)
+constexpr uint32_t kEdTile0 = 4;   // tile0[0..nq]: the batches' first tiles within the step
+constexpr uint32_t kEdQueue = 9;   // + 8 q: bytes, bytes_len, off, len, seed, out, status, n
+// ctl words (pinned): each on its own 64-byte line
+constexpr uint32_t kEcPublished = 0, kEcStop = 8, kEcError = 16, kEcDone = 24;  // done[s] at 24 + 8 s
+
+struct EngineArgs {
+    const uint64_t* ring;   // descriptors, kEngineSlotWords words per step (device view of pinned memory)
+    uint64_t* ctl;          // control words (device view of pinned memory)
+    uint32_t* claims;       // kGroups claim counters, kHeadStride apart (device)
+    uint32_t* counts;       // kEngineCountSlots x kGroups completion counters, kHeadStride apart (device)
+    uint32_t* gdone;        // kEngineCountSlots groups-done counters, kHeadStride apart (device)
+    uint64_t idle_ticks;    // 100 MHz ticks a wave waits for a step before it gives up
+};
+
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+    return static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x)))) |
+           static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32))))
+               << 32;
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t k) {
+    return static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(x), k))) |
+           static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(x >> 32), k)))
+               << 32;
+}
+
+struct EngineSrc {
+    static constexpr bool kEngine = true;
+    const EngineArgs& E;
+    const bool wt;                                     // results written through (kFlagEngineWT)
+    uint32_t lane = 0, grp = 0;
+    uint64_t pub = 0;                                  // published_tiles as last read
+    uint64_t step = ~0ull, sfirst = 0, slast = 0;      // the cursor: step `step` holds tiles [sfirst, slast)
+    uint64_t dw = 0;                                   // lane i: word i of the cursor's descriptor
+#ifdef SCCSUM_AB_TIMELINE
+    unsigned long long ab[8] = {};
+#endif
+    struct Ref {
+        uint32_t cnt, B;
+        uint64_t base, step, first, last;
+        const uint8_t* bytes;
+        uint64_t bytes_len;
+        const uint64_t* off;
+        const uint32_t* len;
+        const uint32_t* seed;
+        uint16_t* out;
+        uint8_t* status;
     };
+    __device__ EngineSrc(const EngineArgs& e, uint32_t flags) : E(e), wt((flags & kFlagEngineWT) != 0) {}
+    __device__ void init(uint64_t wglob, uint64_t, uint32_t lane_) {
+        lane = lane_;
+        grp = static_cast<uint32_t>(wglob % kGroups);
+    }
+    __device__ uint64_t end() const { return ~0ull; }
+    __device__ uint64_t claim(uint64_t) {
+        uint32_t d = 0;
+        if (lane == 0) d = __hip_atomic_fetch_add(E.claims + grp * kHeadStride, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        d = __builtin_amdgcn_readfirstlane(d);
+        return grp + static_cast<uint64_t>(kGroups) * d;
+    }
+    __device__ uint64_t ctl_load(uint32_t w) {
+        uint64_t v = 0;
+        if (lane == 0) v = __hip_atomic_load(E.ctl + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return rfl64(v);
+    }
+    __device__ bool ready(uint64_t v) {
+        if (v < pub) return true;
+#ifdef SCCSUM_AB_TIMELINE
+        ++ab[2];
+#endif
+        pub = ctl_load(kEcPublished);
+        return v < pub;
+    }
+    __device__ bool wait_ready(uint64_t v) {
+        if (ready(v)) return true;
+        flush();  // never wait holding counts: a step's completion may hang on them
+        const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
+#ifdef SCCSUM_AB_TIMELINE
+        ++ab[0];
+        struct Slept {
+            unsigned long long* a;
+            uint64_t t0;
+            __device__ ~Slept() { a[1] += static_cast<uint64_t>(wall_clock64()) - t0; }
+        } slept{ab, t0};
+#endif
+        for (;;) {
+            __builtin_amdgcn_s_sleep(127);  // ~3.4 us: an idle grid polls host memory gently
+            const uint64_t stop = ctl_load(kEcStop);  // read before published_tiles: the host raises it after the last step
+            if (ready(v)) return true;
+            if (stop) return false;  // stopped, and v lies past every published step
+            if (static_cast<uint64_t>(wall_clock64()) - t0 > E.idle_ticks) {
+                if (lane == 0) __hip_atomic_store(E.ctl + kEcError, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return false;
+            }
+        }
+    }
+    __device__ uint64_t first() {
+        const uint64_t v = claim(0);
+        return wait_ready(v) ? v : end();
+    }
+    // tile v (published) -> its step, batch and packets.  Steps are walked in
+    // order: a run never reuses a descriptor, so a step passed over stays valid.
+    __device__ Ref ref(uint64_t v) {
+#ifdef SCCSUM_AB_TIMELINE
+        const uint64_t w0 = (step == ~0ull || v >= slast) ? static_cast<uint64_t>(wall_clock64()) : 0;
+#endif
+        while (step == ~0ull || v >= slast) {
+#ifdef SCCSUM_AB_TIMELINE
+            ++ab[3];
+#endif
+            step = step + 1;  // (~0 + 1 = step 0)
+            dw = __hip_atomic_load(E.ring + step * kEngineSlotWords + lane, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            sfirst = rl64(dw, kEdFirst);
+            slast = sfirst + static_cast<uint32_t>(rl64(dw, kEdTiles));
+        }
+#ifdef SCCSUM_AB_TIMELINE
+        if (w0) ab[4] += static_cast<uint64_t>(wall_clock64()) - w0;
+#endif
+        Ref r;
+        const uint64_t t_in = v - sfirst;
+        const uint32_t nq = static_cast<uint32_t>(rl64(dw, kEdNq));
+        uint32_t q = 0;
+        while (q + 1 < nq && t_in >= rl64(dw, kEdTile0 + q + 1)) ++q;
+        r.B = static_cast<uint32_t>(rl64(dw, kEdTiles) >> 32);
+        r.base = (t_in - rl64(dw, kEdTile0 + q)) * r.B;
+        const uint32_t qw = kEdQueue + 8u * q;
+        const uint64_t left = rl64(dw, qw + 7) - r.base;  // >= 1
+        r.cnt = left < r.B ? static_cast<uint32_t>(left) : r.B;
+        r.bytes = reinterpret_cast<const uint8_t*>(rl64(dw, qw + 0));
+        r.bytes_len = rl64(dw, qw + 1);
+        r.off = reinterpret_cast<const uint64_t*>(rl64(dw, qw + 2));
+        r.len = reinterpret_cast<const uint32_t*>(rl64(dw, qw + 3));
+        r.seed = reinterpret_cast<const uint32_t*>(rl64(dw, qw + 4));
+        r.out = reinterpret_cast<uint16_t*>(rl64(dw, qw + 5));
+        r.status = reinterpret_cast<uint8_t*>(rl64(dw, qw + 6));
+        r.step = step;
+        r.first = sfirst;
+        r.last = slast;
+        return r;
+    }
+    __device__ const uint8_t* bytes(const Ref& r) const { return r.bytes; }
+    __device__ uint64_t bytes_len(const Ref& r) const { return r.bytes_len; }
+    __device__ const uint64_t* off(const Ref& r) const { return r.off; }
+    __device__ const uint32_t* len(const Ref& r) const { return r.len; }
+    __device__ const uint32_t* seed(const Ref& r) const { return r.seed; }
+    __device__ uint16_t* out(const Ref& r) const { return r.out; }
+    __device__ uint8_t* status(const Ref& r) const { return r.status; }
+    __device__ uint32_t tile_packets(const Ref& r) const { return r.B; }
+    // A tile's results are stored: count it for its step, per group (so no
+    // counter sees more than its group's share).  A wave's tiles of one step
+    // come in a row (claims rise), so it counts them itself and adds the count
+    // once, when its tiles move on to a later step or before it waits: one
+    // atomic round trip per step per wave instead of one per tile (per tile it
+    // cost 18 % of cfg 2's step: profiles/r04g).  The step's last count resets
+    // the counters and reports the step done.
+    uint64_t pend_step = ~0ull, pend_first = 0, pend_last = 0;
+    uint32_t pend = 0;
+    __device__ void flush() {
+        if (pend == 0) return;
+        const uint32_t k = pend;
+        pend = 0;
+#ifdef SCCSUM_AB_TIMELINE
+        ++ab[5];
+        struct Flushed {
+            unsigned long long* a;
+            uint64_t t0;
+            __device__ ~Flushed() { a[6] += static_cast<uint64_t>(wall_clock64()) - t0; }
+        } flushed{ab, static_cast<uint64_t>(wall_clock64())};
+#endif
+        if (lane != 0) return;
+        if (wt) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the counted tiles' write-through result stores are done
+        } else {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // their stores leave this XCD's L2 first
+        }
+        const uint64_t fg = pend_first + ((grp + kGroups - pend_first % kGroups) % kGroups);  // the group's first tile
+        const uint32_t expect = fg < pend_last ? static_cast<uint32_t>((pend_last - 1 - fg) / kGroups + 1) : 0u;
+        const uint32_t slot = static_cast<uint32_t>(pend_step % kEngineCountSlots);
+        uint32_t* const c = E.counts + (slot * kGroups + grp) * kHeadStride;
+        const uint32_t x = __hip_atomic_fetch_add(c, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (x + k != expect) return;
+        __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t* const gd = E.gdone + slot * kHeadStride;
+        const uint64_t ntl = pend_last - pend_first;
+        const uint32_t groups = ntl < kGroups ? static_cast<uint32_t>(ntl) : kGroups;
+        const uint32_t y = __hip_atomic_fetch_add(gd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (y + 1 != groups) return;
+        __hip_atomic_store(gd, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(E.ctl + kEcDone + 8u * pend_step, pend_step + 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#ifdef SCCSUM_AB_TIMELINE
+    __device__ void ab_stats(uint64_t wglob) {
+        if (lane == 0 && wglob < kTimelineWaves)
+            for (int i = 0; i < 8; ++i) g_engine_stats[wglob][i] = ab[i];
+    }
+#endif
+    __device__ void retire(const Ref& r) {
+        if (r.step != pend_step) {
+            flush();
+            pend_step = r.step;
+            pend_first = r.first;
+            pend_last = r.last;
+        }
+        ++pend;
+    }
+};
+
+template <int U, bool IPV4, bool FILL, bool PIPE, class Src>
+__device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const RssParams& rss) {
+    static_assert(!FILL || IPV4, "in-place generate is a frames mode");
+    static_assert(!FILL || !Src::kEngine, "the engine does not fill in place");
+    constexpr uint32_t C = kWave * U;  // units per chunk
+    constexpr uint32_t kLdsUnits = C;
+    constexpr int kHead = FILL ? 4 : (IPV4 ? 3 : 1);
+    using Ref = typename Src::Ref;
+    const bool short_chunks = (flags & kFlagFullChunks) == 0;
+    // a run's streamed extent starts on a 64 / 128-byte boundary (clamped to
+    // the batch's first unit), so each 1 KiB load row covers whole lines
+    const uint32_t ra_code = (flags >> kRunAlignShift) & 3u;
+    const uint64_t ra_mask = ra_code == 0 ? 0ull : (ra_code == 1 ? 3ull : 7ull);
+    const bool raw = !IPV4 && (flags & kFlagRaw);
+    const bool fill_ip = FILL && (flags & kFlagFillIp);
+    const bool fill_l4 = FILL && (flags & kFlagFillL4);
+    const bool fill_icmp = FILL && (flags & kFlagFillIcmp);
+    __shared__ u32x4 ubuf_all[kWavesPerBlock][kLdsUnits];
+    __shared__ uint32_t pbuf_all[kWavesPerBlock][kLdsUnits];
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    u32x4* ubuf = ubuf_all[wv];
+    uint32_t* pbuf = pbuf_all[wv];
+    const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+    const uint32_t vo = 16u * lane;
+    const uint64_t wglob = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
+    src.init(wglob, nwaves, lane);
+    const uint64_t ntiles = src.end();
+    auto next_tile = [&](uint64_t prev) -> uint64_t { return src.claim(prev); };
     // Two-deep tile pipeline: while tile t streams, the plan (offset, length,
     // seed) of the next tile is already loading and the tile after it is being
     // dequeued, so no tile starts on an exposed metadata or atomic round trip.
     // Every wave still makes exactly one failing dequeue (the counter reset
-    // relies on it).
-    uint64_t t = wglob;
-    if (t >= ntiles && heads != nullptr) t = next_tile(t);
+    // relies on it).  (One tile ahead instead lost: profiles/r04_ab_dequeue_depth.log.)
+    uint64_t t = src.first();
     uint64_t t1 = t < ntiles ? next_tile(t) : ntiles;
-    auto plan_load = [&](uint64_t tt, uint64_t& o_, uint32_t& L_, uint32_t& sd_) {
-        const TileRef tr = tile_ref(tt < ntiles ? tt : 0);
-        const uint32_t qq = tr.q;
-        const uint32_t c_ = tt < ntiles ? tr.cnt : 0u;
+    auto plan_load = [&](const Ref& tr, bool valid, uint64_t& o_, uint32_t& L_, uint32_t& sd_) {
+        const uint32_t c_ = valid ? tr.cnt : 0u;
         const uint64_t q_ = tr.base + (lane < c_ ? lane : 0);
-        o_ = Q.off[qq][q_];
-        L_ = lane < c_ ? Q.len[qq][q_] : 0u;
-        const uint32_t* sq = IPV4 ? nullptr : Q.seed[qq];
-        sd_ = sq != nullptr ? sq[q_] : 0u;
+        o_ = gld(src.off(tr))[q_];
+        L_ = lane < c_ ? gld(src.len(tr))[q_] : 0u;
+        const uint32_t* sq = IPV4 ? nullptr : src.seed(tr);
+        sd_ = sq != nullptr ? gld(sq)[q_] : 0u;
     };
     // ---- A: a tile's per-lane packet plan and its runs: lane j starts a new
     // run unless packet j-1 and j both take part and j's span starts at most
     // kGapUnits past j-1's end and ends no earlier (so a run's extent is
     // [fu of its first, lu of its last])
     struct Tile {
+        Ref ref;
         uint64_t base, o, a0, fu, lu, starts, streamed;
-        uint32_t q, cnt, L, sd, head, nunits;
+        uint32_t cnt, L, sd, head, nunits;
         bool mine, range_bad, short_frame, huge, fast, part;
     };
-    auto derive = [&](uint64_t tt, uint64_t o_, uint32_t L_, uint32_t sd_) {
+    auto derive = [&](const Ref& tr, uint64_t o_, uint32_t L_, uint32_t sd_) {
         Tile c;
-        const TileRef tr = tile_ref(tt);
-        c.q = tr.q;
+        c.ref = tr;
         c.base = tr.base;
         c.cnt = tr.cnt;
         c.mine = lane < c.cnt;
         c.o = o_;
         c.L = L_;
         c.sd = sd_;
-        const uint64_t bytes_len = Q.bytes_len[c.q];
+        const uint64_t bytes_len = src.bytes_len(tr);
         c.range_bad = c.o > bytes_len || c.L > bytes_len - c.o;
         c.short_frame = IPV4 && c.L < 20;
         c.huge = c.L > kExactMax;
-        const uint8_t* ptr = Q.bytes[c.q] + (c.range_bad ? 0 : c.o);
+        const uint8_t* ptr = src.bytes(tr) + (c.range_bad ? 0 : c.o);
         c.head = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ptr) & 15u);
         c.a0 = reinterpret_cast<uint64_t>(ptr - c.head);
         c.fast = c.mine && !c.range_bad && !c.short_frame && !c.huge;
@@ -996,7 +1297,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
         const uint32_t Fhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(c.fu >> 32), k);
         const uint32_t Flo = __builtin_amdgcn_readlane(static_cast<uint32_t>(c.fu), k);
         rn.F = (static_cast<uint64_t>(Fhi) << 32) | Flo;
-        const uint64_t lo_u = reinterpret_cast<uint64_t>(Q.bytes[c.q]) >> 4;  // the batch's first unit
+        const uint64_t lo_u = reinterpret_cast<uint64_t>(src.bytes(c.ref)) >> 4;  // the batch's first unit
         const uint64_t Fa = rn.F & ~ra_mask;
         rn.F = Fa >= lo_u ? Fa : lo_u;  // (F >= lo_u: the run's first packet lies in the batch)
         const uint32_t Llo = __builtin_amdgcn_readlane(static_cast<uint32_t>(c.lu), rn.k2 - 1);
@@ -1014,7 +1315,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
 
     uint64_t o_n = 0;
     uint32_t L_n = 0, sd_n = 0;
-    plan_load(t, o_n, L_n, sd_n);
+    // the next tile's Ref, from its plan to its derive (an engine's Ref
+    // resolves its step once)
+    Ref r_n{};
+    if (Src::kEngine) {
+        if (t < ntiles) {
+            r_n = src.ref(t);
+            plan_load(r_n, true, o_n, L_n, sd_n);
+        }
+    } else {
+        r_n = src.ref(t < ntiles ? t : 0);
+        plan_load(r_n, t < ntiles, o_n, L_n, sd_n);
+    }
     Tile cur{};
 #ifdef SCCSUM_AB_TIMELINE
     const unsigned long long tl_start = wall_clock64();
@@ -1024,9 +1336,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
 #ifdef SCCSUM_AB_TIMELINE
         ++tl_tiles;
 #endif
-        const uint64_t t2 = t1 < ntiles ? next_tile(t1) : ntiles;
-        cur = derive(t, o_n, L_n, sd_n);
-        if (t1 < ntiles) plan_load(t1, o_n, L_n, sd_n);
+        uint64_t t2 = t1 < ntiles ? next_tile(t1) : ntiles;
+        cur = derive(r_n, o_n, L_n, sd_n);
+        // an engine's next tile may belong to a step not published yet: its plan
+        // then waits until this tile is done (a wave never waits holding work)
+        bool planned = false;
+        if (t1 < ntiles && src.ready(t1)) {
+            r_n = src.ref(t1);
+            plan_load(r_n, true, o_n, L_n, sd_n);
+            planned = true;
+        }
         const uint64_t base = cur.base;
         const bool mine = cur.mine;
         const uint32_t L = cur.L, sd = cur.sd, head = cur.head, nunits = cur.nunits;
@@ -1122,7 +1441,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
         }
         const uint32_t res = pend - pst;  // sum of the packet's units, mod 2^32
         if (IPV4 && huge && mine && !range_bad) {  // not streamed (phase D redoes its sum): head units from the frame
-            const auto* hu = reinterpret_cast<const u32x4*>(a0);
+            const auto* hu = gld(reinterpret_cast<const u32x4*>(a0));
 #pragma unroll
             for (int j = 0; j < kHead; ++j) hs[j] = hu[j];
         }
@@ -1263,8 +1582,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
             }
         }
 
-        uint16_t* const out = Q.out[cur.q];
-        uint8_t* const status = Q.status[cur.q];
+        uint16_t* const out = src.out(cur.ref);
+        uint8_t* const status = src.status(cur.ref);
 #ifdef SCCSUM_AB_NOSTORE
         // A/B only (tools/build_ab.sh): the result stores left out of the
         // stream — kept behind a test no lane passes, so nothing is optimised away
@@ -1277,15 +1596,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
             // merges it with its neighbour tiles' parts into whole lines
             // (nt parts of a line leave as separate partial writes: cfg 4's
             // 1-segment tiles wrote 107 B per segment and ran 8 % slower)
-            const uint32_t pol = (flags >> kOutPolicyShift) & 7u;
-            const uint32_t pol_out = B * (IPV4 ? 4u : 2u) >= 128u ? pol : 0u;
-            const uint32_t pol_st = B >= 128u ? pol : 0u;
+            // (an engine's results are written through, sc0 sc1: the host may read
+            // a step's results as soon as the step reports, while the grid runs)
+            const uint32_t B = src.tile_packets(cur.ref);
+            const bool wt = Src::kEngine && (flags & kFlagEngineWT);
+            const uint32_t pol = wt ? 3u : (flags >> kOutPolicyShift) & 7u;
+            const uint32_t pol_out = wt || B * (IPV4 ? 4u : 2u) >= 128u ? pol : 0u;
+            const uint32_t pol_st = wt || B >= 128u ? pol : 0u;
             if (IPV4) {
                 if (out) tile_store(reinterpret_cast<uint32_t*>(out) + base, lane, word, pol_out);
             } else {
                 tile_store(out + base, lane, static_cast<uint16_t>(word), pol_out);
             }
             if (status) tile_store(status + base, lane, static_cast<uint8_t>(st), pol_st);
+        }
+        src.retire(cur.ref);
+        if (Src::kEngine && t1 < ntiles && !planned) {
+            if (src.wait_ready(t1)) {
+                r_n = src.ref(t1);
+                plan_load(r_n, true, o_n, L_n, sd_n);
+            } else {
+                t1 = t2 = ntiles;  // stopped: t1 (and t2 after it) lie past every step
+            }
         }
         t = t1;
         t1 = t2;
@@ -1297,7 +1629,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
         g_timeline[wglob][2] = wall_clock64();
         g_timeline[wglob][3] = tl_tiles;
     }
+    if constexpr (Src::kEngine) src.ab_stats(wglob);
 #endif
+}
+
+template <int U, bool IPV4, bool FILL, bool PIPE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 ? 2 : 3))) void csum_flat_kernel(
+    const Queues Q, uint32_t B, uint32_t* __restrict__ heads, uint32_t* __restrict__ done, uint32_t ticket,
+    uint32_t flags, const RssParams rss) {
+    QueueSrc src(Q, B, heads, done, ticket);
+    flat_body<U, IPV4, FILL, PIPE>(src, flags, rss);
+}
+
+template <int U, bool IPV4>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 ? 2 : 3))) void csum_engine_kernel(
+    const EngineArgs E, uint32_t flags) {
+    EngineSrc src(E, flags);
+    flat_body<U, IPV4, false, false>(src, flags, RssParams{});
 }
 
 // Fragment lists (checksummer::sum(const packet&), src/net/ip_checksum.cc:64-68):
@@ -1577,6 +1925,7 @@ struct Knobs {
     int out_policy = kOutPolicy;     // flat kernel: cache policy of the result stores (tile_store)
     int short_chunks = 1;            // flat kernel (no chunk in flight): a run's last chunk covers only its rows
     int run_align = kRunAlign;       // flat kernel: run extents start on 1 / 4 / 8-unit (16 / 64 / 128 B) boundaries
+    int engine_wt = 1;               // engine: results written through (1) or stored as a launch stores them (0)
 };
 thread_local Knobs t_knobs;
 
@@ -2218,10 +2567,239 @@ int launch_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const
     }
 }
 
+// Engine launch: the grid is what the chip holds at once (every wave's tiles
+// come from the claim counters, so no block waits for another to finish).
+template <bool IPV4>
+hipError_t launch_engine(hipStream_t s, int dev, const EngineArgs& E, uint32_t flags, uint64_t* waves) {
+    auto kern = csum_engine_kernel<16, IPV4>;
+    const int occ = kernel_occupancy(reinterpret_cast<const void*>(kern));
+    const uint64_t bpc = static_cast<uint64_t>(occ < t_knobs.blocks_per_cu ? occ : t_knobs.blocks_per_cu);
+    uint64_t blocks = static_cast<uint64_t>(cu_count(dev)) * bpc;
+    blocks = blocks & ~uint64_t(15);  // multiple of 16: XCD mapping, waves divide into kGroups
+    if (blocks == 0) blocks = 16;
+    *waves = blocks * kWavesPerBlock;
+    return launch_kernel(kern, dim3(static_cast<unsigned>(blocks)), s, E, flags);
+}
+
 }  // namespace
 }  // namespace sccsum
 
+// ---- resident engine, host side (sccsum.h "Resident engine")
+struct sccsum_engine {
+    int device = 0;
+    bool frames = true;
+    uint32_t max_steps = 0, max_in_flight = 0;
+    uint64_t* ring_h = nullptr;  // pinned descriptors (host view)
+    uint64_t* ctl_h = nullptr;   // pinned control words (host view)
+    sccsum::EngineArgs args{};   // device views + device counters
+    hipStream_t stream = nullptr;
+    bool running = false;
+    uint64_t waves = 0;          // the running grid's waves (tile sizing)
+    uint64_t next_step = 0, next_first = 0;
+};
+
+namespace {
+
+uint64_t now_ns() {
+    return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                     std::chrono::steady_clock::now().time_since_epoch())
+                                     .count());
+}
+
+// spin until step s is done, the grid gave up, or the deadline passes
+int engine_wait_done(sccsum_engine* e, uint64_t s, uint64_t timeout_ns) {
+    const uint64_t t0 = now_ns();
+    uint64_t* const w = e->ctl_h + sccsum::kEcDone + 8u * s;
+    for (uint32_t k = 0;; ++k) {
+        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == s + 1) return SCCSUM_OK;
+        if (__atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE)) return SCCSUM_EIDLE;
+        if ((k & 255u) == 255u && now_ns() - t0 > timeout_ns) return SCCSUM_EBUSY;
+    }
+}
+
+}  // namespace
+
 extern "C" {
+
+int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, sccsum_engine** out) {
+    if (!out || (mode != SCCSUM_PIPE_IPV4 && mode != SCCSUM_PIPE_SPANS) || max_steps == 0 || max_steps > (1u << 20) ||
+        max_in_flight == 0 || max_in_flight > sccsum::kEngineCountSlots) {
+        return SCCSUM_EINVAL;
+    }
+    *out = nullptr;
+    int n = 0;
+    hipError_t e0 = hipGetDeviceCount(&n);
+    if (e0 != hipSuccess) return static_cast<int>(e0);
+    if (device < 0 || device >= n) return SCCSUM_ENODEV;
+    if ((e0 = hipSetDevice(device)) != hipSuccess) return static_cast<int>(e0);
+    auto* e = new (std::nothrow) sccsum_engine;
+    if (!e) return static_cast<int>(hipErrorOutOfMemory);
+    e->device = device;
+    e->frames = mode == SCCSUM_PIPE_IPV4;
+    e->max_steps = max_steps;
+    e->max_in_flight = max_in_flight;
+    const uint64_t ring_bytes = uint64_t(max_steps) * sccsum::kEngineSlotWords * 8u;
+    const uint64_t ctl_bytes = (sccsum::kEcDone + 8u * uint64_t(max_steps)) * 8u;
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
+    void *rh = nullptr, *ch = nullptr, *rd = nullptr, *cd = nullptr, *cl = nullptr, *co = nullptr, *gd = nullptr;
+    hipError_t r = hipHostMalloc(&rh, ring_bytes, fl);
+    if (r == hipSuccess) r = hipHostMalloc(&ch, ctl_bytes, fl);
+    if (r == hipSuccess) r = hipHostGetDevicePointer(&rd, rh, 0);
+    if (r == hipSuccess) r = hipHostGetDevicePointer(&cd, ch, 0);
+    const size_t claims_b = size_t(sccsum::kGroups) * sccsum::kHeadStride * 4u;
+    const size_t counts_b = size_t(sccsum::kEngineCountSlots) * sccsum::kGroups * sccsum::kHeadStride * 4u;
+    const size_t gdone_b = size_t(sccsum::kEngineCountSlots) * sccsum::kHeadStride * 4u;
+    if (r == hipSuccess) r = hipMalloc(&cl, claims_b);
+    if (r == hipSuccess) r = hipMalloc(&co, counts_b);
+    if (r == hipSuccess) r = hipMalloc(&gd, gdone_b);
+    if (r != hipSuccess) {
+        for (void* p : {rh, ch}) if (p) (void)hipHostFree(p);
+        for (void* p : {cl, co, gd}) if (p) (void)hipFree(p);
+        delete e;
+        return static_cast<int>(r);
+    }
+    std::memset(rh, 0, ring_bytes);
+    std::memset(ch, 0, ctl_bytes);
+    e->ring_h = static_cast<uint64_t*>(rh);
+    e->ctl_h = static_cast<uint64_t*>(ch);
+    e->args.ring = static_cast<const uint64_t*>(rd);
+    e->args.ctl = static_cast<uint64_t*>(cd);
+    e->args.claims = static_cast<uint32_t*>(cl);
+    e->args.counts = static_cast<uint32_t*>(co);
+    e->args.gdone = static_cast<uint32_t*>(gd);
+    e->args.idle_ticks = 100000000ull;  // 1 s at the constant 100 MHz clock
+    *out = e;
+    return SCCSUM_OK;
+}
+
+int sccsum_engine_start(sccsum_engine* e, void* stream) {
+    if (!e || e->running) return SCCSUM_EINVAL;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    int dev = 0;
+    if (const int rc = sccsum::launch_device(s, &dev); rc != SCCSUM_OK) return rc;
+    if (dev != e->device) return SCCSUM_EINVAL;
+    // a new run: no step published, none done, counters zero (stream-ordered before the grid)
+    std::memset(e->ctl_h, 0, (sccsum::kEcDone + 8u * uint64_t(e->max_steps)) * 8u);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    const size_t claims_b = size_t(sccsum::kGroups) * sccsum::kHeadStride * 4u;
+    const size_t counts_b = size_t(sccsum::kEngineCountSlots) * sccsum::kGroups * sccsum::kHeadStride * 4u;
+    const size_t gdone_b = size_t(sccsum::kEngineCountSlots) * sccsum::kHeadStride * 4u;
+    hipError_t r = hipMemsetAsync(e->args.claims, 0, claims_b, s);
+    if (r == hipSuccess) r = hipMemsetAsync(e->args.counts, 0, counts_b, s);
+    if (r == hipSuccess) r = hipMemsetAsync(e->args.gdone, 0, gdone_b, s);
+    if (r != hipSuccess) return static_cast<int>(r);
+    const sccsum::Knobs& K = sccsum::t_knobs;
+    uint32_t flags = static_cast<uint32_t>(K.out_policy) << sccsum::kOutPolicyShift;
+    if (K.engine_wt) flags |= sccsum::kFlagEngineWT;
+    if (!K.short_chunks) flags |= sccsum::kFlagFullChunks;
+    flags |= static_cast<uint32_t>(K.run_align == 8 ? 2 : (K.run_align == 4 ? 1 : 0)) << sccsum::kRunAlignShift;
+    r = e->frames ? sccsum::launch_engine<true>(s, dev, e->args, flags, &e->waves)
+                  : sccsum::launch_engine<false>(s, dev, e->args, flags, &e->waves);
+    if (r != hipSuccess) return static_cast<int>(r);
+    e->stream = s;
+    e->running = true;
+    e->next_step = 0;
+    e->next_first = 0;
+    return SCCSUM_OK;
+}
+
+int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
+                         uint64_t timeout_ns, uint64_t* step) {
+    if (!e || !e->running || !step || nbatch == 0 || nbatch > SCCSUM_ENGINE_MAX_BATCHES || !batches) {
+        return SCCSUM_EINVAL;
+    }
+    uint64_t n_total = 0, bytes_total = 0;
+    for (uint32_t i = 0; i < nbatch; ++i) {
+        const sccsum_batch& x = batches[i];
+        const bool ok = e->frames
+                            ? sccsum::batch_ok<true>(x.d_bytes, x.d_off, x.d_len, nullptr, x.d_out, x.d_status, 0)
+                            : sccsum::batch_ok<false>(x.d_bytes, x.d_off, x.d_len, x.d_seed, x.d_out, x.d_status, 0);
+        if (x.n && !ok) return SCCSUM_EINVAL;
+        if (e->frames && x.d_seed) return SCCSUM_EINVAL;  // frames derive their pseudo-header in-kernel
+        n_total += x.n;
+        bytes_total += x.n ? x.bytes_len : 0;
+    }
+    if (__atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE)) return SCCSUM_EIDLE;
+    const uint64_t s = e->next_step;
+    if (s >= e->max_steps) return SCCSUM_EBUSY;  // the run's descriptors are used up: stop, start again
+    if (s >= e->max_in_flight) {
+        const int rc = engine_wait_done(e, s - e->max_in_flight, timeout_ns);
+        if (rc != SCCSUM_OK) return rc;
+    }
+    // tile size as a launch would pick it (launch_flat): ~tile_bytes of packets, at most 64
+    const sccsum::Knobs& K = sccsum::t_knobs;
+    uint64_t bmax = static_cast<uint64_t>(K.tile_packets);
+    if (K.tile_bytes && n_total) {
+        const uint64_t mean = bytes_total / n_total ? bytes_total / n_total : 1;
+        const uint64_t bb = static_cast<uint64_t>(K.tile_bytes) / mean ? static_cast<uint64_t>(K.tile_bytes) / mean : 1;
+        bmax = bb < bmax ? bb : bmax;
+    }
+    uint64_t B = e->waves ? (n_total + e->waves - 1) / e->waves : 1;
+    B = B < 1 ? 1 : (B > bmax ? bmax : B);
+    uint64_t* const d = e->ring_h + s * sccsum::kEngineSlotWords;
+    uint64_t tile0[SCCSUM_ENGINE_MAX_BATCHES + 1] = {};
+    uint32_t nq = 0;
+    for (uint32_t i = 0; i < nbatch; ++i) {
+        const sccsum_batch& x = batches[i];
+        if (!x.n) continue;
+        const uint32_t q = nq++;
+        uint64_t* w = d + sccsum::kEdQueue + 8u * q;
+        w[0] = reinterpret_cast<uint64_t>(x.d_bytes);
+        w[1] = x.bytes_len;
+        w[2] = reinterpret_cast<uint64_t>(x.d_off);
+        w[3] = reinterpret_cast<uint64_t>(x.d_len);
+        w[4] = e->frames ? 0u : reinterpret_cast<uint64_t>(x.d_seed);
+        w[5] = reinterpret_cast<uint64_t>(x.d_out);
+        w[6] = reinterpret_cast<uint64_t>(x.d_status);
+        w[7] = x.n;
+        tile0[q + 1] = tile0[q] + (x.n + B - 1) / B;
+    }
+    const uint64_t ntiles = tile0[nq];
+    d[sccsum::kEdFirst] = e->next_first;
+    d[sccsum::kEdTiles] = ntiles | (B << 32);
+    d[sccsum::kEdStep] = s;
+    d[sccsum::kEdNq] = nq ? nq : 1;
+    for (uint32_t q = 0; q <= SCCSUM_ENGINE_MAX_BATCHES; ++q) d[sccsum::kEdTile0 + q] = tile0[q];
+    if (ntiles == 0) {  // nothing to sum: done at once (the descriptor still keeps the walk in order)
+        __atomic_store_n(e->ctl_h + sccsum::kEcDone + 8u * s, s + 1, __ATOMIC_RELEASE);
+    }
+    e->next_first += ntiles;
+    e->next_step = s + 1;
+    // publish: the descriptor is complete before any of its tiles is claimable
+    __atomic_store_n(e->ctl_h + sccsum::kEcPublished, e->next_first, __ATOMIC_SEQ_CST);
+    *step = s;
+    return SCCSUM_OK;
+}
+
+int sccsum_engine_wait(sccsum_engine* e, uint64_t step, uint64_t timeout_ns) {
+    if (!e || step >= e->next_step) return SCCSUM_EINVAL;
+    return engine_wait_done(e, step, timeout_ns);
+}
+
+int sccsum_engine_stop(sccsum_engine* e) {
+    if (!e || !e->running) return SCCSUM_EINVAL;
+    __atomic_store_n(e->ctl_h + sccsum::kEcStop, 1ull, __ATOMIC_SEQ_CST);
+    e->running = false;
+    return __atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE) ? SCCSUM_EIDLE : SCCSUM_OK;
+}
+
+int sccsum_engine_destroy(sccsum_engine* e) {
+    if (!e) return SCCSUM_OK;
+    int rc = SCCSUM_OK;
+    if (e->running) {
+        (void)sccsum_engine_stop(e);
+        rc = static_cast<int>(hipStreamSynchronize(e->stream));
+    } else if (e->stream) {
+        rc = static_cast<int>(hipStreamSynchronize(e->stream));
+    }
+    (void)hipHostFree(e->ring_h);
+    (void)hipHostFree(e->ctl_h);
+    (void)hipFree(e->args.claims);
+    (void)hipFree(e->args.counts);
+    (void)hipFree(e->args.gdone);
+    delete e;
+    return rc;
+}
 
 int sccsum_abi_version(void) { return SCCSUM_ABI_VERSION; }
 
@@ -2230,6 +2808,7 @@ const char* sccsum_strerror(int err) {
     if (err == SCCSUM_EINVAL) return "invalid argument";
     if (err == SCCSUM_ENODEV) return "no such HIP device";
     if (err == SCCSUM_EBUSY) return "every batch slot is in flight";
+    if (err == SCCSUM_EIDLE) return "the engine's grid gave up waiting for steps";
     if (err > 0) return hipGetErrorString(static_cast<hipError_t>(err));
     return "unknown sccsum error";
 }
@@ -2480,6 +3059,11 @@ int sccsum_set_out_policy(int policy) {
     return SCCSUM_OK;
 }
 
+int sccsum_set_engine_write_through(int on) {
+    sccsum::t_knobs.engine_wt = on ? 1 : 0;
+    return SCCSUM_OK;
+}
+
 int sccsum_set_short_chunks(int on) {
     if (on != 0 && on != 1) return SCCSUM_EINVAL;
     sccsum::t_knobs.short_chunks = on;
@@ -2506,6 +3090,11 @@ int sccsum_sync(void* stream) { return static_cast<int>(hipStreamSynchronize(sta
 int sccsum_ab_timeline(void* host, uint64_t bytes) {
     const uint64_t n = bytes < sizeof(sccsum::g_timeline) ? bytes : sizeof(sccsum::g_timeline);
     return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(sccsum::g_timeline), n, 0, hipMemcpyDeviceToHost));
+}
+// and the per-wave counters of the last engine run (8 u64 per wave)
+int sccsum_ab_engine_stats(void* host, uint64_t bytes) {
+    const uint64_t n = bytes < sizeof(sccsum::g_engine_stats) ? bytes : sizeof(sccsum::g_engine_stats);
+    return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(sccsum::g_engine_stats), n, 0, hipMemcpyDeviceToHost));
 }
 #endif
 

@@ -21,6 +21,7 @@ SCCSUM_OK = 0
 SCCSUM_EINVAL = -1
 SCCSUM_ENODEV = -2
 SCCSUM_EBUSY = -3
+SCCSUM_EIDLE = -4
 ST_OK = 0x01
 ST_L4_OK = 0x02
 ST_MALFORMED = 0x04
@@ -77,6 +78,7 @@ _PROTOS = {
     "sccsum_set_tile_bytes": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_tail_split": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "sccsum_set_out_policy": (ctypes.c_int, [ctypes.c_int]),
+    "sccsum_set_engine_write_through": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_short_chunks": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_run_align": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_read_probe": (ctypes.c_int, [_vp, _u64, _vp, _vp]),
@@ -98,6 +100,12 @@ _PROTOS = {
     "sccsum_burst_destroy": (ctypes.c_int, [_vp]),
     "sccsum_host_alloc": (ctypes.c_int, [ctypes.POINTER(_vp), _u64]),
     "sccsum_host_free": (ctypes.c_int, [_vp]),
+    "sccsum_engine_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _u32, _u32, ctypes.POINTER(_vp)]),
+    "sccsum_engine_start": (ctypes.c_int, [_vp, _vp]),
+    "sccsum_engine_submit": (ctypes.c_int, [_vp, _vp, _u32, _u32, _u64, ctypes.POINTER(_u64)]),
+    "sccsum_engine_wait": (ctypes.c_int, [_vp, _u64, _u64]),
+    "sccsum_engine_stop": (ctypes.c_int, [_vp]),
+    "sccsum_engine_destroy": (ctypes.c_int, [_vp]),
 }
 PIPE_SPANS = 0
 PIPE_IPV4 = 1
@@ -117,6 +125,7 @@ class Batch(ctypes.Structure):
 
 
 MAX_BATCHES = 16
+ENGINE_MAX_BATCHES = 4
 
 
 class Fragment(ctypes.Structure):

@@ -11,6 +11,7 @@
 #   trace:CFG[+ARG...]     rocprofv3 --kernel-trace --stats of the bench command
 #   prof:CFG[+ARG...]      trace + separate FETCH_SIZE and WRITE_SIZE passes of the bench command,
 #                          cut to the timed dispatches by tools/prof_timed.py ($TAG_pmc_CFG.json)
+#   sq:CFG[+ARG...]        two SQ counter passes of the bench command (instruction mix, waits; tools/pmc_sum.py)
 #   py:SCRIPT[+ARG...]     python SCRIPT ARG... (a tools/ probe)
 #   bin:PROGRAM[+ARG...]   a probe program built here beforehand (tools/dev/*.hip)
 #   pbin:PROGRAM[+ARG...]  the same program under rocprofv3: a kernel trace, then separate FETCH_SIZE and
@@ -37,7 +38,7 @@ split() {  # split CFG+A+B -> CFG and args array ARGS
 }
 
 name_of() {  # file-name form of a step's config + args
-    echo "$1" | tr '+' '_' | tr -d '-'
+    echo "$1" | tr '+/' '__' | tr -d '-'
 }
 
 run_step() {
@@ -84,6 +85,18 @@ run_step() {
                 --fetch "$O/prof_$n/fetch" --write "$O/prof_$n/write" --probe-bytes "${PROBE_BYTES:-0}" \
                 --config "$CFG" --label "$TAG bench.py --config $CFG $PROF_STEPS ${ARGS[*]}" \
                 --out "$O/${TAG}_pmc_$n.json" --trace-out "$O/${TAG}_trace_$n.csv" > "$O/prof_${n}_summary.log" 2>&1 ;;
+        sq)  # two SQ counter passes of the bench command (instruction mix, wait cycles), summed per kernel
+            split "$rest"
+            (cd /tmp && \
+             timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM \
+                SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d "$O/sq_$n/a" -o run \
+                --output-format csv -- python3 "$R/bench.py" --config "$CFG" $PROF_STEPS "${ARGS[@]}" \
+                > "$O/sq_${n}_a.log" 2>&1 && \
+             timeout -k 10 -s KILL 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_VALU \
+                SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH -d "$O/sq_$n/b" -o run \
+                --output-format csv -- python3 "$R/bench.py" --config "$CFG" $PROF_STEPS "${ARGS[@]}" \
+                > "$O/sq_${n}_b.log" 2>&1) && \
+            python tools/pmc_sum.py "$O/sq_$n/a" "$O/sq_$n/b" > "$O/sq_${n}_summary.log" 2>&1 ;;
         py)
             split "$rest"
             timeout -k 10 400 python "$CFG" "${ARGS[@]}" >> "$O/py_$(basename "$CFG" .py).log" 2>&1 ;;
