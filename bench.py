@@ -91,7 +91,7 @@ def parse():
                     help="A/B: grid cap in workgroups per CU (sccsum_set_blocks_per_cu)")
     ap.add_argument("--out-policy", type=int, default=None,
                     help="A/B: cache policy of the flat kernel's result stores (sccsum_set_out_policy)")
-    ap.add_argument("--engine-in-flight", type=int, default=2,
+    ap.add_argument("--engine-in-flight", type=int, default=8,
                     help="--launch engine: steps published ahead of the grid (max_in_flight)")
     ap.add_argument("--engine-wt", type=int, default=None,
                     help="A/B: engine result stores written through (1) or stored as a launch does (0) "
@@ -448,9 +448,22 @@ def timed(step, steps, warmup, world, streams, begin=None, end=None):
     other stream).  An event between every two launches leaves the GPU idle
     ~5 us at each (a timestamp packet), which per-launch events would add to
     the wall time."""
+    import gc
+
     streams = streams if isinstance(streams, (list, tuple)) else [streams]
     s0 = streams[0]
     torch.cuda.synchronize()  # inputs built on the default stream are complete before any step stream reads them
+    # no collector pauses inside the step loops: a full collection (tens of ms with torch loaded) would
+    # starve a resident engine, which holds only max_in_flight steps of work ahead of the host
+    gc.collect()
+    gc.disable()
+    try:
+        return _timed(step, steps, warmup, world, streams, s0, begin, end)
+    finally:
+        gc.enable()
+
+
+def _timed(step, steps, warmup, world, streams, s0, begin, end):
     if warmup:
         if begin:  # (--launch engine: a run of its own)
             begin()
@@ -740,11 +753,13 @@ def run_mixed(args, world, rank, dev):
     by sccsum_ipv4_fill; --launch single, the default), or, like cfg 2, both
     directions in one sccsum_ipv4_frames_multi launch: generate over a tx
     batch (checksum fields zero) plus verify-only over the rx batch (its own
-    Zipf draw) (--launch multi; 1-2 % slower on three boxes)."""
+    Zipf draw) (--launch multi; 1-2 % slower on three boxes), or the single
+    form's steps submitted into one resident engine grid (--launch engine)."""
     from seastar_amd import synth
 
     n = args.packets if args.packets != (1 << 20) else 3_400_000
     multi = (args.launch or "single") == "multi"
+    engine = args.launch == "engine"
     lens = synth.zipf_lengths(n, seed=SEED + rank)
     lens_rx = synth.zipf_lengths(n, seed=SEED + 7717 + rank) if multi else lens
     R = max(1, args.rotate)  # distinct batches launched in turn (no cached-line replay)
@@ -753,7 +768,7 @@ def run_mixed(args, world, rank, dev):
     txs = ([devsynth.mixed_frames(lens, seed=SEED + 131 * rank + 17 * r + 5, device=dev, align=align)
             for r in range(R)] if multi else [])
     streams = make_streams(args, dev)
-    if R % len(streams):  # a batch (and its status buffer) must always come back to the same stream
+    if R % len(streams) or engine:  # a batch (and its status buffer) must always come back to the same stream
         streams = streams[:1]
     ns = len(streams)
     stream = streams[0]
@@ -784,13 +799,31 @@ def run_mixed(args, world, rank, dev):
                                           rxs[r].length, outs[i][1], None, rxs[r].n, rxs[r].max_len)
                for r in range(R) for i in range(ns)}
     warm = max(args.warmup, R)
-    LAUNCHES.add(kern, warm)
-    sel = LAUNCHES.select(kern, args.steps)
-    wall, launch_s = timed(lambda k: pre[(k % R, k % ns)](streams[k % ns]), args.steps, warm, world, streams)
+    step, begin, end, eng = (lambda k: pre[(k % R, k % ns)](streams[k % ns])), None, None, None
+    if engine:  # the single form's steps, submitted into one resident grid per run
+        kern = "csum_engine_kernel<16, true>"
+        eng = batch.Engine(dev.index or 0, frames=True, max_steps=max(warm, args.steps) + 4,
+                           max_in_flight=args.engine_in_flight)
+        pre_e = {r: eng.prepare([(rxs[r], outs[0][1], None)]) for r in range(R)}
+
+        def step(k):
+            eng.submit_prepared(pre_e[k % R])
+
+        def begin():
+            eng.start(streams[0])
+
+        end = eng.stop
+    LAUNCHES.add(kern, 1 if engine else warm)
+    sel = LAUNCHES.select(kern, 1 if engine else args.steps)
+    wall, launch_s = timed(step, args.steps, warm, world, streams, begin, end)
     # per launch: every frame byte + 12 B metadata + the results: 4 B per frame, except a multi step's rx
     # half, which writes 1 B of status bits (+ 4 B with --rx-out2)
     alg = (total + n * (META_BYTES + 4) + n * (META_BYTES + 1 + (4 if args.rx_out2 else 0)) if multi
            else total + n * (META_BYTES + 4))
+    roof_alg, roof_s = alg, launch_s
+    if engine:  # the launch is the run: every step's bytes over the run's time (the same ratio)
+        roof_alg, roof_s = alg * args.steps, launch_s * args.steps
+        eng.close()
     ceiling = read_ceiling(rxs[0].data, rxs[0].bytes_len, stream)
     ranks = per_rank(world, rank, dev, **rank_rate(nbytes, args.steps), avg_launch_us=launch_s * 1e6,
                      read_ceiling_GBps=ceiling, frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS)
@@ -804,12 +837,15 @@ def run_mixed(args, world, rank, dev):
               "packets_per_gpu": (2 * n if multi else n), "bytes_per_gpu": total,
               "mean_len": round(total / (2 * n if multi else n), 1),
               "launch": ("one sccsum_ipv4_frames_multi launch per step over the tx and rx batches" if multi
-                         else "one sccsum_ipv4_frames launch per step"),
+                         else (f"one resident engine grid per timed run (sccsum_engine_*): each step's batch "
+                               f"submitted into it, at most {args.engine_in_flight} steps in flight" if engine
+                               else "one sccsum_ipv4_frames launch per step")),
               "rotation": f"{R} distinct batch {'pairs' if multi else 'sets'} launched in turn",
               "streams": f"{ns} (step k on stream k % {ns})", "parallelism": f"{world} independent shards"},
-             roofline(alg, launch_s, "mixed" if align == 1 else f"mixed_align{align}",
-                      kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi
-                                                      else " (sccsum_ipv4_frames)"), sel, args,
+             roofline(roof_alg, roof_s, ("mixed" if align == 1 else f"mixed_align{align}") + ("_engine" if engine else ""),
+                      kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi else
+                              (" (sccsum_engine_*; one launch = the timed run)" if engine
+                               else " (sccsum_ipv4_frames)")), sel, args,
                       {"measured_read_ceiling_GBps": round(ceiling, 1)}), extra={"per_rank": ranks})
 
 

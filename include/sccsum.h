@@ -209,9 +209,9 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  *
  *   sccsum_engine_create(device, mode, max_steps, max_in_flight, &e)
  *       mode SCCSUM_PIPE_IPV4 (frames) or SCCSUM_PIPE_SPANS; at most
- *       max_steps steps per run (descriptors are never reused within a run:
- *       max_steps x 512 B of pinned memory), at most max_in_flight (1..64)
- *       submitted and not yet done.
+ *       max_steps (1..65536) steps per run (descriptors are never reused
+ *       within a run: max_steps x 512 B of pinned memory and as much device
+ *       memory), at most max_in_flight (1..64) submitted and not yet done.
  *   sccsum_engine_start(e, stream)      launch the grid on `stream` (a run)
  *   sccsum_engine_submit(e, batches, nbatch, max_len, timeout_ns, &step)
  *       publish one step; waits (spinning, up to timeout_ns) while

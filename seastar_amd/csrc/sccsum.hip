@@ -797,8 +797,8 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
 // registers, its failing dequeue, and its tile count.
 constexpr uint32_t kTimelineWaves = 16384;
 __device__ unsigned long long g_timeline[kTimelineWaves][4];
-// engine runs: per wave, [waits that slept, ticks asleep, published reloads,
-// descriptor walks, ticks in walks, flushes, ticks in flushes, -]
+// engine runs: per wave, [waits that slept, ticks asleep, mirror reloads,
+// descriptor walks, ticks in walks, flushes, ticks in flushes, host polls]
 __device__ unsigned long long g_engine_stats[kTimelineWaves][8];
 #endif
 
@@ -963,22 +963,29 @@ struct QueueSrc {
 //
 // One grid stays resident and takes STEPS — up to kEngineQueues batches each,
 // the tx and rx halves of a step, a shard's rx queues — that the host
-// publishes while it runs.  A step is a 512-byte descriptor in pinned host
-// memory (one 8-byte word per lane, read with system-scope loads); its tiles
-// continue the run's global tile numbering, so tile v of the run is claimed
-// from group counter v % kGroups exactly as in a launch, and step boundaries
-// cost nothing: no kernel boundary, no ramp, no drain between steps.  The
-// host publishes a step by raising `published_tiles` (ctl[0]) after its
-// descriptor is written; a wave that claims a tile past it finishes the tile
-// it holds first and only then waits (sleeping), so a wave never waits while
-// it holds published work.  Each tile's results are written through (sc0 sc1)
-// and counted per step and group; the last tile of a step stores the step's
-// ticket into its pinned done word.  Exit: the host sets stop (ctl[8]); a
-// wave that needs a tile past every published step then leaves — and so does
-// one that has waited `idle_ticks` with no stop (it raises ctl[9] first).
+// publishes while it runs.  A step is a 512-byte descriptor (one 8-byte word
+// per lane); its tiles continue the run's global tile numbering, so tile v of
+// the run is claimed from group counter v % kGroups exactly as in a launch,
+// and step boundaries cost nothing: no kernel boundary, no ramp, no drain
+// between steps.  The host writes the descriptor into pinned memory and raises
+// `published_steps` (ctl[0]).  Host memory is read by ONE wave at a time: the
+// wave that finds no published tile for its claim takes the poll token, reads
+// ctl[0] (and stop) over PCIe, copies the new descriptors into a device ring
+// and raises a device mirror of the published tiles; every other wave reads
+// only the mirror and the device ring.  (With every waiting wave polling the
+// host itself, 2 048 waves' reads flooded PCIe: a 262 144-frame step took
+// 22 ms instead of 0.13 ms, profiles/r04m.)  A wave that claims a tile past
+// the mirror finishes the tile it holds first and only then waits (sleeping),
+// so a wave never waits while it holds published work.  Each tile's results
+// are written through (sc0 sc1) and counted per step and group; the last count
+// of a step stores the step's ticket into its pinned done word.  Exit: the
+// host sets stop (ctl[8]); a wave that needs a tile past every published step
+// then leaves — and so does one that has waited `idle_ticks` with no stop (it
+// raises ctl[16] first).
 constexpr uint32_t kEngineQueues = 4;
 constexpr uint32_t kEngineSlotWords = 64;  // 512-byte descriptors
 constexpr uint32_t kEngineCountSlots = 64;  // completion counters: steps in flight at most
+constexpr uint32_t kEngineMaxSteps = 1u << 16;  // steps per run (2 x 32 MiB of descriptor rings at most)
 // descriptor words
 constexpr uint32_t kEdFirst = 0;   // the step's first tile in the run
 constexpr uint32_t kEdTiles = 1;   // tiles | B (packets per tile) << 32
@@ -988,10 +995,14 @@ constexpr uint32_t kEdTile0 = 4;   // tile0[0..nq]: the batches' first tiles wit
 constexpr uint32_t kEdQueue = 9;   // + 8 q: bytes, bytes_len, off, len, seed, out, status, n
 // ctl words (pinned): each on its own 64-byte line
 constexpr uint32_t kEcPublished = 0, kEcStop = 8, kEcError = 16, kEcDone = 24;  // done[s] at 24 + 8 s
+// mirror words (device): published tiles, steps copied, stop seen, poll token
+constexpr uint32_t kMpTiles = 0, kMpSteps = 8, kMpStop = 16, kMpToken = 24, kMirrorWords = 32;
 
 struct EngineArgs {
-    const uint64_t* ring;   // descriptors, kEngineSlotWords words per step (device view of pinned memory)
+    const uint64_t* hring;  // descriptors as the host writes them, kEngineSlotWords words per step (pinned)
+    uint64_t* dring;        // the same descriptors, copied by the polling wave (device)
     uint64_t* ctl;          // control words (device view of pinned memory)
+    uint64_t* mirror;       // kMirrorWords (device)
     uint32_t* claims;       // kGroups claim counters, kHeadStride apart (device)
     uint32_t* counts;       // kEngineCountSlots x kGroups completion counters, kHeadStride apart (device)
     uint32_t* gdone;        // kEngineCountSlots groups-done counters, kHeadStride apart (device)
@@ -1014,7 +1025,7 @@ struct EngineSrc {
     const EngineArgs& E;
     const bool wt;                                     // results written through (kFlagEngineWT)
     uint32_t lane = 0, grp = 0;
-    uint64_t pub = 0;                                  // published_tiles as last read
+    uint64_t pub = 0;                                  // published tiles, as the mirror last said
     uint64_t step = ~0ull, sfirst = 0, slast = 0;      // the cursor: step `step` holds tiles [sfirst, slast)
     uint64_t dw = 0;                                   // lane i: word i of the cursor's descriptor
 #ifdef SCCSUM_AB_TIMELINE
@@ -1044,17 +1055,62 @@ struct EngineSrc {
         d = __builtin_amdgcn_readfirstlane(d);
         return grp + static_cast<uint64_t>(kGroups) * d;
     }
-    __device__ uint64_t ctl_load(uint32_t w) {
+    __device__ uint64_t ctl_load(uint32_t w) {  // host memory (PCIe): the poll token's holder only
         uint64_t v = 0;
         if (lane == 0) v = __hip_atomic_load(E.ctl + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return rfl64(v);
+    }
+    __device__ uint64_t mload(uint32_t w) {
+        uint64_t v = 0;
+        if (lane == 0) v = __hip_atomic_load(E.mirror + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return rfl64(v);
+    }
+    // Take the poll token if it is free; then bring the host's new steps into
+    // the device ring and raise the mirror (tiles and steps, then stop: a
+    // wave that sees stop then sees every step).
+    __device__ void poll() {
+        uint32_t got = 0;
+        if (lane == 0 && __hip_atomic_load(E.mirror + kMpToken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            uint64_t expect = 0;
+            got = __hip_atomic_compare_exchange_strong(E.mirror + kMpToken, &expect, 1ull, __ATOMIC_RELAXED,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      ? 1u
+                      : 0u;
+        }
+        if (!__builtin_amdgcn_readfirstlane(got)) return;
+#ifdef SCCSUM_AB_TIMELINE
+        ++ab[7];
+#endif
+        const uint64_t stop = ctl_load(kEcStop);  // before the steps: the host raises it after its last step
+        const uint64_t hs = ctl_load(kEcPublished);
+        uint64_t ms = mload(kMpSteps);
+        uint64_t tiles = mload(kMpTiles);
+        for (; ms < hs; ++ms) {
+            const uint64_t w = __hip_atomic_load(E.hring + ms * kEngineSlotWords + lane, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(E.dring + ms * kEngineSlotWords + lane, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tiles = rl64(w, kEdFirst) + static_cast<uint32_t>(rl64(w, kEdTiles));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the descriptors are in the device ring
+        if (lane == 0) {
+            __hip_atomic_store(E.mirror + kMpTiles, tiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(E.mirror + kMpSteps, hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            if (stop) __hip_atomic_store(E.mirror + kMpStop, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(E.mirror + kMpToken, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     __device__ bool ready(uint64_t v) {
         if (v < pub) return true;
 #ifdef SCCSUM_AB_TIMELINE
         ++ab[2];
 #endif
-        pub = ctl_load(kEcPublished);
+        pub = mload(kMpTiles);
+        if (v < pub) return true;
+        poll();
+        pub = mload(kMpTiles);
         return v < pub;
     }
     __device__ bool wait_ready(uint64_t v) {
@@ -1070,8 +1126,8 @@ struct EngineSrc {
         } slept{ab, t0};
 #endif
         for (;;) {
-            __builtin_amdgcn_s_sleep(127);  // ~3.4 us: an idle grid polls host memory gently
-            const uint64_t stop = ctl_load(kEcStop);  // read before published_tiles: the host raises it after the last step
+            __builtin_amdgcn_s_sleep(127);  // ~3.4 us
+            const uint64_t stop = mload(kMpStop);  // read before the tiles (the poller raises it after them)
             if (ready(v)) return true;
             if (stop) return false;  // stopped, and v lies past every published step
             if (static_cast<uint64_t>(wall_clock64()) - t0 > E.idle_ticks) {
@@ -1095,8 +1151,8 @@ struct EngineSrc {
             ++ab[3];
 #endif
             step = step + 1;  // (~0 + 1 = step 0)
-            dw = __hip_atomic_load(E.ring + step * kEngineSlotWords + lane, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            dw = __hip_atomic_load(E.dring + step * kEngineSlotWords + lane, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             sfirst = rl64(dw, kEdFirst);
             slast = sfirst + static_cast<uint32_t>(rl64(dw, kEdTiles));
         }
@@ -2593,7 +2649,8 @@ struct sccsum_engine {
     uint64_t* ctl_h = nullptr;   // pinned control words (host view)
     sccsum::EngineArgs args{};   // device views + device counters
     hipStream_t stream = nullptr;
-    bool running = false;
+    hipEvent_t left = nullptr;   // recorded after the last run's grid: it has left once this completes
+    bool running = false, launched = false, left_recorded = false;
     uint64_t waves = 0;          // the running grid's waves (tile sizing)
     uint64_t next_step = 0, next_first = 0;
 };
@@ -2622,7 +2679,8 @@ int engine_wait_done(sccsum_engine* e, uint64_t s, uint64_t timeout_ns) {
 extern "C" {
 
 int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, sccsum_engine** out) {
-    if (!out || (mode != SCCSUM_PIPE_IPV4 && mode != SCCSUM_PIPE_SPANS) || max_steps == 0 || max_steps > (1u << 20) ||
+    if (!out || (mode != SCCSUM_PIPE_IPV4 && mode != SCCSUM_PIPE_SPANS) || max_steps == 0 ||
+        max_steps > sccsum::kEngineMaxSteps ||
         max_in_flight == 0 || max_in_flight > sccsum::kEngineCountSlots) {
         return SCCSUM_EINVAL;
     }
@@ -2641,7 +2699,8 @@ int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_
     const uint64_t ring_bytes = uint64_t(max_steps) * sccsum::kEngineSlotWords * 8u;
     const uint64_t ctl_bytes = (sccsum::kEcDone + 8u * uint64_t(max_steps)) * 8u;
     const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
-    void *rh = nullptr, *ch = nullptr, *rd = nullptr, *cd = nullptr, *cl = nullptr, *co = nullptr, *gd = nullptr;
+    void *rh = nullptr, *ch = nullptr, *rd = nullptr, *cd = nullptr, *cl = nullptr, *co = nullptr, *gd = nullptr,
+         *dr = nullptr, *mi = nullptr;
     hipError_t r = hipHostMalloc(&rh, ring_bytes, fl);
     if (r == hipSuccess) r = hipHostMalloc(&ch, ctl_bytes, fl);
     if (r == hipSuccess) r = hipHostGetDevicePointer(&rd, rh, 0);
@@ -2652,9 +2711,12 @@ int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_
     if (r == hipSuccess) r = hipMalloc(&cl, claims_b);
     if (r == hipSuccess) r = hipMalloc(&co, counts_b);
     if (r == hipSuccess) r = hipMalloc(&gd, gdone_b);
+    if (r == hipSuccess) r = hipMalloc(&dr, ring_bytes);
+    if (r == hipSuccess) r = hipMalloc(&mi, sccsum::kMirrorWords * 8u);
+    if (r == hipSuccess) r = hipEventCreateWithFlags(&e->left, hipEventDisableTiming);
     if (r != hipSuccess) {
         for (void* p : {rh, ch}) if (p) (void)hipHostFree(p);
-        for (void* p : {cl, co, gd}) if (p) (void)hipFree(p);
+        for (void* p : {cl, co, gd, dr, mi}) if (p) (void)hipFree(p);
         delete e;
         return static_cast<int>(r);
     }
@@ -2662,7 +2724,9 @@ int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_
     std::memset(ch, 0, ctl_bytes);
     e->ring_h = static_cast<uint64_t*>(rh);
     e->ctl_h = static_cast<uint64_t*>(ch);
-    e->args.ring = static_cast<const uint64_t*>(rd);
+    e->args.hring = static_cast<const uint64_t*>(rd);
+    e->args.dring = static_cast<uint64_t*>(dr);
+    e->args.mirror = static_cast<uint64_t*>(mi);
     e->args.ctl = static_cast<uint64_t*>(cd);
     e->args.claims = static_cast<uint32_t*>(cl);
     e->args.counts = static_cast<uint32_t*>(co);
@@ -2678,6 +2742,11 @@ int sccsum_engine_start(sccsum_engine* e, void* stream) {
     int dev = 0;
     if (const int rc = sccsum::launch_device(s, &dev); rc != SCCSUM_OK) return rc;
     if (dev != e->device) return SCCSUM_EINVAL;
+    // the last run's grid has left (stop only asks it to): its control words are ours again
+    if (e->launched) {
+        const hipError_t w = e->left_recorded ? hipEventSynchronize(e->left) : hipStreamSynchronize(e->stream);
+        if (w != hipSuccess) return static_cast<int>(w);
+    }
     // a new run: no step published, none done, counters zero (stream-ordered before the grid)
     std::memset(e->ctl_h, 0, (sccsum::kEcDone + 8u * uint64_t(e->max_steps)) * 8u);
     std::atomic_thread_fence(std::memory_order_seq_cst);
@@ -2687,6 +2756,7 @@ int sccsum_engine_start(sccsum_engine* e, void* stream) {
     hipError_t r = hipMemsetAsync(e->args.claims, 0, claims_b, s);
     if (r == hipSuccess) r = hipMemsetAsync(e->args.counts, 0, counts_b, s);
     if (r == hipSuccess) r = hipMemsetAsync(e->args.gdone, 0, gdone_b, s);
+    if (r == hipSuccess) r = hipMemsetAsync(e->args.mirror, 0, sccsum::kMirrorWords * 8u, s);
     if (r != hipSuccess) return static_cast<int>(r);
     const sccsum::Knobs& K = sccsum::t_knobs;
     uint32_t flags = static_cast<uint32_t>(K.out_policy) << sccsum::kOutPolicyShift;
@@ -2696,6 +2766,8 @@ int sccsum_engine_start(sccsum_engine* e, void* stream) {
     r = e->frames ? sccsum::launch_engine<true>(s, dev, e->args, flags, &e->waves)
                   : sccsum::launch_engine<false>(s, dev, e->args, flags, &e->waves);
     if (r != hipSuccess) return static_cast<int>(r);
+    e->left_recorded = hipEventRecord(e->left, s) == hipSuccess;  // else the next start syncs the stream
+    e->launched = true;
     e->stream = s;
     e->running = true;
     e->next_step = 0;
@@ -2765,8 +2837,8 @@ int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t
     }
     e->next_first += ntiles;
     e->next_step = s + 1;
-    // publish: the descriptor is complete before any of its tiles is claimable
-    __atomic_store_n(e->ctl_h + sccsum::kEcPublished, e->next_first, __ATOMIC_SEQ_CST);
+    // publish: the descriptor is complete before the grid's poller can see the step
+    __atomic_store_n(e->ctl_h + sccsum::kEcPublished, e->next_step, __ATOMIC_SEQ_CST);
     *step = s;
     return SCCSUM_OK;
 }
@@ -2797,6 +2869,9 @@ int sccsum_engine_destroy(sccsum_engine* e) {
     (void)hipFree(e->args.claims);
     (void)hipFree(e->args.counts);
     (void)hipFree(e->args.gdone);
+    (void)hipFree(e->args.dring);
+    (void)hipFree(e->args.mirror);
+    if (e->left) (void)hipEventDestroy(e->left);
     delete e;
     return rc;
 }

@@ -103,6 +103,22 @@ static void checks() {
     EXPECT(sccsum_burst_poll(nullptr, nullptr) == SCCSUM_EINVAL);
     EXPECT(sccsum_burst_drain(nullptr) == SCCSUM_EINVAL);
     EXPECT(sccsum_burst_destroy(nullptr) == SCCSUM_OK);
+    // resident engine: arguments are checked before any runtime call
+    sccsum_engine* eng = nullptr;
+    EXPECT(sccsum_engine_create(0, 7, 16, 2, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, 0, 2, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, 65537, 2, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_SPANS, 16, 0, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_SPANS, 16, 65, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, 16, 2, nullptr) == SCCSUM_EINVAL);
+    EXPECT(eng == nullptr);
+    EXPECT(sccsum_engine_start(nullptr, nullptr) == SCCSUM_EINVAL);
+    uint64_t step = 0;
+    EXPECT(sccsum_engine_submit(nullptr, nullptr, 1, 0, 0, &step) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_wait(nullptr, 0, 0) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_stop(nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_destroy(nullptr) == SCCSUM_OK);
+    EXPECT(sccsum_set_engine_write_through(0) == SCCSUM_OK && sccsum_set_engine_write_through(1) == SCCSUM_OK);
     // host pipeline
     sccsum_pipeline* p = nullptr;
     EXPECT(sccsum_pipeline_create(0, 1 << 20, 1024, 0, &p) == SCCSUM_EINVAL);
