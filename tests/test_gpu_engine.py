@@ -206,3 +206,31 @@ def test_engine_large_steps_property(dev):
         assert torch.equal(outs[r].view(-1, 2), ref[r])
         assert int(((sts[r] & 2) == 0).sum()) == bad.numel()
     eng.close()
+
+
+def test_engine_results_readable_while_the_grid_runs(dev):
+    """The header's promise: a step's results may be read as soon as its wait
+    returns, while the grid still runs (a host copy on another stream goes
+    through a copy engine, not a kernel that would queue behind the grid)."""
+    rng = np.random.default_rng(0xE5)
+    items = []
+    for _ in range(3):
+        b, want, want_st = _frames_step(rng, dev, 0)
+        items.append((b, torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev), want))
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, max_steps=8, max_in_flight=2)
+    stream = torch.cuda.Stream(device=dev)
+    side = torch.cuda.Stream(device=dev)
+    eng.start(stream)
+    ids = [eng.submit([(b, out, None)]) for b, out, _ in items]
+    got = []
+    for i, (b, out, want) in zip(ids, items):
+        eng.wait(i)
+        with torch.cuda.stream(side):
+            host = out.to("cpu", non_blocking=False)
+        got.append((host, want))
+    eng.stop()  # raises SccsumError(EIDLE) if a copy had queued behind the grid past its idle limit
+    stream.synchronize()
+    for host, want in got:
+        assert np.array_equal(host.numpy().view(np.uint16).reshape(-1, 2), want)
+    eng.close()

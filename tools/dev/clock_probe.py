@@ -38,8 +38,14 @@ def read_int(path):
 def main():
     bdf, hw = hwmon_dir()
     files = {k: os.path.join(hw, f) for k, f in (("sclk_hz", "freq1_input"), ("mclk_hz", "freq2_input"),
-                                                  ("power_uw", "power1_average"), ("power_in_uw", "power1_input"),
-                                                  ("temp_mc", "temp1_input"))} if hw else {}
+                                                  ("power_uw", "power1_average"), ("power_in_uw", "power1_input"))} if hw else {}
+    for t in sorted(glob.glob(os.path.join(hw, "temp*_input"))) if hw else []:  # every readable sensor, by label
+        lab = os.path.join(os.path.dirname(t), os.path.basename(t).replace("_input", "_label"))
+        try:
+            name = open(lab).read().strip()
+        except OSError:
+            name = os.path.basename(t)
+        files[f"temp_{name}_mc"] = t
     print(json.dumps({"bdf": bdf, "hwmon": hw, "readable": {k: read_int(v) for k, v in files.items()}}), flush=True)
     dev = torch.device("cuda:0")
     n, R, K = 1 << 20, 4, 4000
@@ -68,12 +74,15 @@ def main():
             for k in range(K):
                 pre[k % R](s)
                 if (k + 1) % 100 == 0:
-                    e = torch.cuda.Event()
+                    e = torch.cuda.Event(enable_timing=True)
                     e.record(s)
                     ev.append((k + 1, e))
-            for k1, e in ev:  # completion times of every 100th launch, from the host
-                e.synchronize()
-                marks.append((time.perf_counter(), k1))
+            torch.cuda.synchronize()
+            t_end = time.perf_counter()
+            # GPU time of each 100-launch block from the events; host times placed back from the run's end
+            gpu = [0.0] + [ev[0][1].elapsed_time(e) / 1e3 for _, e in ev[1:]]
+            span = gpu[-1]
+            marks = [(t_end - (span - g), k1) for g, (k1, _) in zip(gpu, ev)]
         else:
             eng = batch.Engine(0, frames=True, max_steps=K + 4, max_in_flight=8)
             pe = [eng.prepare([(txs[r], o_tx, None), (rxs[r], None, sts[r])]) for r in range(R)]
@@ -97,7 +106,7 @@ def main():
             for key in files:
                 vals = [w[key] for w in win if w[key] is not None]
                 if vals:
-                    row[key] = round(float(np.mean(vals)) / (1e6 if key.endswith("hz") else 1e6 if key.endswith("uw") else 1e3), 1)
+                    row[key] = round(float(np.mean(vals)) / (1e3 if key.endswith("_mc") else 1e6), 1)
             rows.append(row)
         print(json.dumps({"form": form, "steps": K, "rows_every_100_steps": rows}), flush=True)
 
