@@ -217,6 +217,10 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  *       publish one step; waits (spinning, up to timeout_ns) while
  *       max_in_flight steps are pending.  SCCSUM_EBUSY: the run already took
  *       max_steps steps (stop and start a new run) or the wait timed out.
+ *       max_len is taken for symmetry with the _multi calls and not used:
+ *       the engine always runs the flat kernel, so sparse layouts give exact
+ *       results but belong on the launches, whose row kernel reads them
+ *       faster.  Frames take no seeds.
  *   sccsum_engine_wait(e, step, timeout_ns)   0 once the step is done
  *   sccsum_engine_stop(e)               no more steps: the grid leaves once the
  *       published steps are done (synchronise `stream` to wait for it)
