@@ -465,9 +465,8 @@ class Engine:
         if not items or len(items) > native.ENGINE_MAX_BATCHES:
             raise ValueError(f"1..{native.ENGINE_MAX_BATCHES} batches per step")
         width = 2 if self.frames else 1
-        arr = (native.Batch * len(items))()
-        ml = 0
-        for i, it in enumerate(items):
+        parts = []
+        for i, it in enumerate(items):  # every item is checked before any is built
             b, out, status = it[0], it[1], it[2]
             seeds = it[3] if len(it) > 3 else None
             if self.frames and seeds is not None:
@@ -477,10 +476,12 @@ class Engine:
             _need(out, width * b.n, torch.int16, f"batch {i} out", b.device)
             _need(status, b.n, torch.uint8, f"batch {i} status", b.device)
             _need(seeds, b.n, torch.int32, f"batch {i} seeds", b.device)
+            parts.append((b, out, status, seeds))
+        arr = (native.Batch * len(items))()
+        for i, (b, out, status, seeds) in enumerate(parts):
             arr[i] = native.Batch(ctypes_ptr(b.data), b.bytes_len, ctypes_ptr(b.off), ctypes_ptr(b.length),
                                   _ptr(seeds), _ptr(out), _ptr(status), b.n)
-            ml = max(ml, b.max_len)
-        return (arr, len(items), ml, items)
+        return (arr, len(items), max(b.max_len for b, _, _, _ in parts), items)
 
     def submit_prepared(self, prep, timeout_s: float = 10.0) -> int:
         arr, nb, ml, items = prep
