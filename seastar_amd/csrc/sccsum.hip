@@ -800,6 +800,12 @@ __device__ unsigned long long g_timeline[kTimelineWaves][4];
 // engine runs: per wave, [waits that slept, ticks asleep, mirror reloads,
 // descriptor walks, ticks in walks, flushes, ticks in flushes, host polls]
 __device__ unsigned long long g_engine_stats[kTimelineWaves][8];
+// engine runs, per step of the run (the first kStepRec): the latest tile
+// retire of each dequeue group, and per XCD the latest and (complemented, so a
+// max keeps the earliest) first tile retire
+constexpr uint32_t kStepRec = 1024;
+__device__ unsigned long long g_step_grp[kStepRec][64];
+__device__ unsigned long long g_step_xcd[kStepRec][8][2];
 #endif
 
 constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B) between packets
@@ -854,6 +860,18 @@ struct Queues {
 // grid fed steps through a ring, csum_engine_kernel, §5.11 of DESIGN.md).
 // Both give the same body (flat_body) a tile's batch and packet range (Ref),
 // the next tile number to work on, and what to do once a tile is stored.
+// A wave's dequeue group.  Each aligned run of 64 waves holds one wave of
+// every group (a launch's per-group dequeue counts rely on it), shifted by one
+// per run, so group g holds waves of every slot in their workgroup on every
+// XCD; g = wglob % 64 gave a group waves of one slot only.  Waves are not
+// equally fast and a group's are fixed, so in a long engine run the groups
+// drift apart (the grid then works on several steps at once, its step time
+// rising with the spread); this composition halves the drift rate
+// (profiles/r04_engine_groups.log).
+__device__ __forceinline__ uint32_t group_of(uint64_t wglob) {
+    return static_cast<uint32_t>((wglob + wglob / kGroups) % kGroups);
+}
+
 struct QueueSrc {
     static constexpr bool kEngine = false;
     const Queues& Q;
@@ -876,7 +894,7 @@ struct QueueSrc {
         nwaves = nwaves_;
         wglob = wglob_;
         lane = lane_;
-        grp = static_cast<uint32_t>(wglob % kGroups);
+        grp = group_of(wglob);
         const uint64_t rest = ntiles > nwaves ? ntiles - nwaves : 0;
         tiles_g = rest > grp ? static_cast<uint32_t>((rest - grp + kGroups - 1) / kGroups) : 0u;
         waves_g = static_cast<uint32_t>(nwaves / kGroups);
@@ -914,7 +932,7 @@ struct QueueSrc {
     // Tile order.  Wave w first takes tile w (static: no start-up contention).
     // With `heads`, the remaining tiles [W, ntiles) are split over kGroups
     // counters (each on its own line) and dequeued: wave w pulls
-    // tile W + g + kGroups * atomicAdd(heads[g], 1) with g = w % kGroups, so
+    // tile W + g + kGroups * atomicAdd(heads[g], 1) with g = group_of(w), so
     // waves that drew short tiles take more (Zipf batches).  Each group's
     // dequeue count is known — one per remaining tile of the group plus one
     // failing dequeue per wave of the group — so the wave that draws the last
@@ -1045,7 +1063,7 @@ struct EngineSrc {
     __device__ EngineSrc(const EngineArgs& e, uint32_t flags) : E(e), wt((flags & kFlagEngineWT) != 0) {}
     __device__ void init(uint64_t wglob, uint64_t, uint32_t lane_) {
         lane = lane_;
-        grp = static_cast<uint32_t>(wglob % kGroups);
+        grp = group_of(wglob);
     }
     __device__ uint64_t end() const { return ~0ull; }
     __device__ uint64_t claim(uint64_t) {
@@ -1198,6 +1216,9 @@ struct EngineSrc {
     // the counters and reports the step done.
     uint64_t pend_step = ~0ull, pend_first = 0, pend_last = 0;
     uint32_t pend = 0;
+#ifdef SCCSUM_AB_TIMELINE
+    unsigned long long pend_t0 = 0, pend_t1 = 0;
+#endif
     __device__ void flush() {
         if (pend == 0) return;
         const uint32_t k = pend;
@@ -1209,6 +1230,13 @@ struct EngineSrc {
             uint64_t t0;
             __device__ ~Flushed() { a[6] += static_cast<uint64_t>(wall_clock64()) - t0; }
         } flushed{ab, static_cast<uint64_t>(wall_clock64())};
+#endif
+#ifdef SCCSUM_AB_TIMELINE
+        if (lane == 0 && pend_step < kStepRec) {
+            atomicMax(&g_step_grp[pend_step][grp], pend_t1);
+            atomicMax(&g_step_xcd[pend_step][blockIdx.x & 7u][0], pend_t1);
+            atomicMax(&g_step_xcd[pend_step][blockIdx.x & 7u][1], ~pend_t0);
+        }
 #endif
         if (lane != 0) return;
         if (wt) {
@@ -1246,8 +1274,14 @@ struct EngineSrc {
             pend_step = r.step;
             pend_first = r.first;
             pend_last = r.last;
+#ifdef SCCSUM_AB_TIMELINE
+            pend_t0 = static_cast<uint64_t>(wall_clock64());
+#endif
         }
         ++pend;
+#ifdef SCCSUM_AB_TIMELINE
+        pend_t1 = static_cast<uint64_t>(wall_clock64());
+#endif
     }
 };
 
@@ -3170,6 +3204,22 @@ int sccsum_ab_timeline(void* host, uint64_t bytes) {
 int sccsum_ab_engine_stats(void* host, uint64_t bytes) {
     const uint64_t n = bytes < sizeof(sccsum::g_engine_stats) ? bytes : sizeof(sccsum::g_engine_stats);
     return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(sccsum::g_engine_stats), n, 0, hipMemcpyDeviceToHost));
+}
+// and the per-step group / XCD retire times of the last engine run (then cleared):
+// kStepRec x 64 u64, then kStepRec x 8 x 2 u64
+int sccsum_ab_step_times(void* host, uint64_t bytes) {
+    const uint64_t a = sizeof(sccsum::g_step_grp), b = sizeof(sccsum::g_step_xcd);
+    if (bytes < a + b) return SCCSUM_EINVAL;
+    hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(sccsum::g_step_grp), a, 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(static_cast<char*>(host) + a, HIP_SYMBOL(sccsum::g_step_xcd), b, 0, hipMemcpyDeviceToHost);
+    void* pa = nullptr;
+    void* pb = nullptr;
+    if (e == hipSuccess) e = hipGetSymbolAddress(&pa, HIP_SYMBOL(sccsum::g_step_grp));
+    if (e == hipSuccess) e = hipGetSymbolAddress(&pb, HIP_SYMBOL(sccsum::g_step_xcd));
+    if (e == hipSuccess) e = hipMemset(pa, 0, a);
+    if (e == hipSuccess) e = hipMemset(pb, 0, b);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    return static_cast<int>(e);
 }
 #endif
 

@@ -24,21 +24,64 @@ from seastar_amd import batch, devsynth, native  # noqa: E402
 TICK_US = 0.01  # 100 MHz
 
 
+def step_spread(rec, K):
+    """Per step of the run: how far apart its 64 dequeue groups and 8 XCDs
+    finished, how many later steps had begun on some XCD when it completed,
+    and each XCD's lag behind the step's first XCD to finish (us), by tenths."""
+    grp = rec[:1024 * 64].reshape(1024, 64)[:K].astype(np.float64)
+    xcd = rec[1024 * 64:].reshape(1024, 8, 2)[:K]
+    fin = xcd[:, :, 0].astype(np.float64)
+    first = (~xcd[:, :, 1]).astype(np.float64)  # stored complemented
+    ok = (grp.min(axis=1) > 0) & (fin.min(axis=1) > 0)
+    done = grp.max(axis=1)
+    ahead = []
+    for k in range(K):
+        later = first[k + 1:k + 17].min(axis=1) if k + 1 < K else np.array([])
+        ahead.append(int((later < done[k]).sum()))
+    tenth = lambda a: [round(float(np.mean(c)), 1) for c in np.array_split(np.asarray(a, dtype=np.float64), 10)]
+    gs = (grp.max(axis=1) - grp.min(axis=1)) * TICK_US
+    xs = (fin.max(axis=1) - fin.min(axis=1)) * TICK_US
+    lag = (fin - fin.min(axis=1, keepdims=True)) * TICK_US
+    glag = ((grp - grp.min(axis=1, keepdims=True)) * TICK_US)[ok]
+    return {"steps_recorded": int(ok.sum()),
+            "group_finish_spread_us_by_tenth": tenth(gs[ok]),
+            "xcd_finish_spread_us_by_tenth": tenth(xs[ok]),
+            "later_steps_begun_at_completion_by_tenth": tenth(np.asarray(ahead)[ok]),
+            "step_interval_us_by_tenth": tenth(np.diff(done[ok]) * TICK_US),
+            "group_lag_us_last_tenth_by_g_mod_4": [round(float(v), 1) for v in
+                glag[-max(1, K // 10):].mean(axis=0).reshape(16, 4).mean(axis=0)],
+            "slowest_groups_last_tenth": [int(g) for g in np.argsort(-glag[-max(1, K // 10):].mean(axis=0))[:6]],
+            "fastest_groups_last_tenth": [int(g) for g in np.argsort(glag[-max(1, K // 10):].mean(axis=0))[:6]],
+            "xcd_lag_us_first_tenth": [round(float(v), 1) for v in lag[ok][:max(1, K // 10)].mean(axis=0)],
+            "xcd_lag_us_last_tenth": [round(float(v), 1) for v in lag[ok][-max(1, K // 10):].mean(axis=0)]}
+
+
 def main():
     lib = native.load()
     fn = getattr(lib, "sccsum_ab_engine_stats", None)  # timeline builds only
     if fn is not None:
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    st_fn = getattr(lib, "sccsum_ab_step_times", None)  # per-step group / XCD retire times
+    if st_fn is not None:
+        st_fn.restype = ctypes.c_int
+        st_fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     dev = torch.device("cuda:0")
     flights = [int(x) for x in os.environ.get("ENGINE_IN_FLIGHT", "2").split(",")]
     sizes = [int(x) for x in os.environ.get("ENGINE_FRAMES", f"{1 << 18},{1 << 20}").split(",")]
     K = int(os.environ.get("ENGINE_STEPS", "20"))
     for n, in_flight in [(n, f) for n in sizes for f in flights]:
         R = 4
-        txs = [devsynth.udp_frames(n, 1500, seed=11 + r, device=dev) for r in range(R)]
-        rxs = [devsynth.udp_frames(n, 1500, seed=31 + r, device=dev) for r in range(R)]
         o_tx = torch.empty(2 * n, dtype=torch.int16, device=dev)
+        if os.environ.get("ENGINE_BENCH_DATA"):  # bench.py's cfg 2 batches: rx = tx with its checksums stored
+            txs, rxs = [], []
+            for r in range(R):
+                txs.append(devsynth.udp_frames(n, 1500, seed=11 + r, device=dev))
+                first = batch.ipv4_frames(txs[-1], out2=o_tx)
+                rxs.append(devsynth.store_checksums(txs[-1], first))
+        else:
+            txs = [devsynth.udp_frames(n, 1500, seed=11 + r, device=dev) for r in range(R)]
+            rxs = [devsynth.udp_frames(n, 1500, seed=31 + r, device=dev) for r in range(R)]
         sts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(R)]
         eng = batch.Engine(0, frames=True, max_steps=K + 8, max_in_flight=in_flight)
         preps = [eng.prepare([(txs[r], o_tx, None), (rxs[r], None, sts[r])]) for r in range(R)]
@@ -47,6 +90,9 @@ def main():
         for rep in range(2):  # the first run warms
             stats = np.zeros((16384, 8), dtype=np.uint64)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            steps_rec = np.zeros(1024 * 64 + 1024 * 16, dtype=np.uint64)
+            if st_fn is not None:  # clear the last run's records
+                native.check(st_fn(steps_rec.ctypes.data, steps_rec.nbytes), "sccsum_ab_step_times")
             e0.record(s)
             eng.start(s)
             blocked, ret = [], []
@@ -60,6 +106,8 @@ def main():
             torch.cuda.synchronize()
             if fn is not None:
                 native.check(fn(stats.ctypes.data, stats.nbytes), "sccsum_ab_engine_stats")
+            if st_fn is not None:
+                native.check(st_fn(steps_rec.ctypes.data, steps_rec.nbytes), "sccsum_ab_step_times")
         # submit k returns when step k - in_flight is done: the spacing of the returns is the
         # grid's step time, here in 10 quantiles of the run
         gaps = np.diff(np.array(ret[in_flight:])) * 1e6
@@ -86,6 +134,8 @@ def main():
                 "flushes_per_wave": round(float(w[:, 5].mean()), 2),
                 "flush_us_per_wave": round(float(w[:, 6].mean()) * TICK_US, 1),
                 "host_polls_total": int(w[:, 7].sum())})
+        if st_fn is not None:
+            d.update(step_spread(steps_rec, min(K, 1024)))
         print(json.dumps(d), flush=True)
         eng.close()
         del txs, rxs
