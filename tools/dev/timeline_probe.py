@@ -58,7 +58,15 @@ def main():
     o_tx = torch.empty(2 * n, dtype=torch.int16, device=dev)
     sts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(R)]
     s = torch.cuda.current_stream()
+    from seastar_amd import synth
+    nz = 3_400_000  # cfg 3: Zipf frames packed at odd offsets, one sccsum_ipv4_frames launch (bench.py's single form)
+    lens = synth.zipf_lengths(nz, seed=0x5EA57A2C)
+    zs = [devsynth.mixed_frames(lens, seed=7 * r + 1, device=dev) for r in range(R)]
+    o_z = torch.empty(2 * nz, dtype=torch.int16, device=dev)
     cases = {
+        "cfg3_step (3.4 M Zipf frames, one batch)":
+            [batch.prepare_call("sccsum_ipv4_frames", z.data, z.bytes_len, z.off, z.length, o_z, None, z.n, z.max_len)
+             for z in zs],
         "cfg2_step (tx + verify-only rx, 2 M frames)":
             [batch.prepare_ipv4_frames_multi([(txs[r], o_tx, None), (rxs[r], None, sts[r])]) for r in range(R)],
         "one 1 M-frame batch":
