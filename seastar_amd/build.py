@@ -13,12 +13,17 @@ SOURCES = [
     os.path.join(PKG_DIR, "csrc", "burst.cc"),
 ]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# The AMDGPU atomic optimizer rewrites the kernels' lane-0 atomics into
+# wave-wide ones whose result it reads back where they are issued; the flat
+# kernel's LATE form reads its tile claim back a tile later (sccsum.hip,
+# flat_body).  No kernel has an atomic it would help: each is one lane's.
+DEVICE_FLAGS = ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
 
 
 def hipcc_cmd(out: str = LIB_PATH) -> list[str]:
     return [
         HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared",
-        "-Wall", "-Wno-unused-command-line-argument",
+        "-Wall", "-Wno-unused-command-line-argument", *DEVICE_FLAGS,
         "-I", os.path.join(REPO_DIR, "include"),
         *SOURCES, "-o", out,
     ]

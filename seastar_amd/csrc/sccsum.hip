@@ -940,32 +940,43 @@ struct QueueSrc {
     // the last group to do so stores this launch's ticket to `done` (pinned
     // host memory): the host may then hand the slot to another launch
     // (acquire_heads).  Without `heads`: static round robin.
-    __device__ uint64_t claim(uint64_t prev) {
-        if (heads == nullptr) return prev + nwaves;
-        uint32_t d = 0;
-        if (lane == 0) {
+    // A claim in two halves, the atomic (claim_issue) and its read-back
+    // (claim_resolve); claim() does both at once (the flat body's LATE form
+    // issues after a tile's last loads and reads back after the tile).
+    struct Claim {
+        uint32_t raw;
+        uint64_t prev;
+    };
+    __device__ Claim claim_issue(uint64_t prev) {
+        Claim c{0u, prev};
+        if (heads != nullptr && lane == 0)
+            c.raw = __hip_atomic_fetch_add(heads + grp * kHeadStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return c;
+    }
+    __device__ uint64_t claim_resolve(const Claim& c) {
+        if (heads == nullptr) return c.prev + nwaves;
+        uint32_t d = c.raw;
+        if (lane == 0 && d == tiles_g + waves_g - 1) {
             uint32_t* h = heads + grp * kHeadStride;
-            d = __hip_atomic_fetch_add(h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (d == tiles_g + waves_g - 1) {
-                // The slot's words are only ever touched by agent-scope atomics,
-                // which are performed at the device's coherence point; waiting
-                // for each to complete (s_waitcnt) orders reset -> count ->
-                // report without the L2 write-backs a release fence costs
-                // (profiles/r03_ab_pool_rows.log).
-                __hip_atomic_store(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // The slot's words are only ever touched by agent-scope atomics,
+            // which are performed at the device's coherence point; waiting
+            // for each to complete (s_waitcnt) orders reset -> count ->
+            // report without the L2 write-backs a release fence costs
+            // (profiles/r03_ab_pool_rows.log).
+            __hip_atomic_store(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint32_t* const groups_done = heads + kGroups * kHeadStride;
+            const uint32_t gd = __hip_atomic_fetch_add(groups_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (gd == kGroups - 1) {  // every group has reset: the slot is free for another launch
+                __hip_atomic_store(groups_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                uint32_t* const groups_done = heads + kGroups * kHeadStride;
-                const uint32_t gd = __hip_atomic_fetch_add(groups_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (gd == kGroups - 1) {  // every group has reset: the slot is free for another launch
-                    __hip_atomic_store(groups_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_store(done, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
+                __hip_atomic_store(done, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         d = __builtin_amdgcn_readfirstlane(d);
         return d < tiles_g ? nwaves + grp + static_cast<uint64_t>(kGroups) * d : ntiles;
     }
+    __device__ uint64_t claim(uint64_t prev) { return claim_resolve(claim_issue(prev)); }
     __device__ uint64_t first() {
         uint64_t t = wglob;
         if (t >= ntiles && heads != nullptr) t = claim(t);
@@ -1066,13 +1077,20 @@ struct EngineSrc {
         grp = group_of(wglob);
     }
     __device__ uint64_t end() const { return ~0ull; }
-    __device__ uint64_t claim(uint64_t) {
-        uint32_t d = 0;
-        if (lane == 0) d = __hip_atomic_fetch_add(E.claims + grp * kHeadStride, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        d = __builtin_amdgcn_readfirstlane(d);
+    struct Claim {
+        uint32_t raw;
+    };
+    __device__ Claim claim_issue(uint64_t) {
+        Claim c{0u};
+        if (lane == 0) c.raw = __hip_atomic_fetch_add(E.claims + grp * kHeadStride, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+        return c;
+    }
+    __device__ uint64_t claim_resolve(const Claim& c) {
+        const uint32_t d = __builtin_amdgcn_readfirstlane(c.raw);
         return grp + static_cast<uint64_t>(kGroups) * d;
     }
+    __device__ uint64_t claim(uint64_t prev) { return claim_resolve(claim_issue(prev)); }
     __device__ uint64_t ctl_load(uint32_t w) {  // host memory (PCIe): the poll token's holder only
         uint64_t v = 0;
         if (lane == 0) v = __hip_atomic_load(E.ctl + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1285,7 +1303,7 @@ struct EngineSrc {
     }
 };
 
-template <int U, bool IPV4, bool FILL, bool PIPE, class Src>
+template <int U, bool IPV4, bool FILL, bool PIPE, bool LATE, class Src>
 __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const RssParams& rss) {
     static_assert(!FILL || IPV4, "in-place generate is a frames mode");
     static_assert(!FILL || !Src::kEngine, "the engine does not fill in place");
@@ -1426,7 +1444,24 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
 #ifdef SCCSUM_AB_TIMELINE
         ++tl_tiles;
 #endif
-        uint64_t t2 = t1 < ntiles ? next_tile(t1) : ntiles;
+        // The claim of the tile after next.  Read back at once: its round trip
+        // stalls the wave here, before the tile's first loads.  LATE (tiles of
+        // one packet of 48 KiB or more): issued after the tile's last loads and
+        // read back after the tile, so the round trip overlaps the last chunk's:
+        // cfg 4 1.2 % faster, but Zipf tiles ran 8 % slower in steady state
+        // (profiles/r04_engine_groups.log, r04zf-r04zk).  The atomic optimizer is
+        // off (build.py): it would read the atomic back right where it is issued.
+        const bool claiming = t1 < ntiles;
+        bool issued = false;
+        typename Src::Claim c2{};
+        uint64_t t2 = ntiles;
+        if (!LATE && claiming) t2 = next_tile(t1);
+        auto issue = [&]() {
+            if (LATE && claiming && !issued) {
+                c2 = src.claim_issue(t1);
+                issued = true;
+            }
+        };
         cur = derive(r_n, o_n, L_n, sd_n);
         // an engine's next tile may belong to a step not published yet: its plan
         // then waits until this tile is done (a wave never waits holding work)
@@ -1457,6 +1492,7 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
             const int rf = cap ? static_cast<int>(static_cast<uint32_t>(cur.fu - F)) : -0x40000000;
             const int rl = cap ? static_cast<int>(static_cast<uint32_t>(cur.lu - F)) : -0x40000000;
             uint32_t carry = 0;
+            const bool last_run = rem == 0;
             // one chunk = R <= U rows of 64 units: unit sums, scanned, parked
             // in LDS with the units; packet lanes pick up what falls in it
             auto chunk = [&](uint32_t g, const auto& v) {
@@ -1509,26 +1545,32 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
                 // profiles/r02_ab_short_chunks.log)
                 for (uint32_t g = 0; g < ext; g += C) {
                     const uint32_t left = ext - g;
+                    const bool last = LATE && last_run && left <= C;  // the tile's last loads
                     if (!short_chunks || left > C / 2) {
                         u32x4 v[U];
                         load(r, g, v);
+                        if (last) issue();
                         chunk(g, v);
                     } else if (left > C / 4) {
                         u32x4 v[U / 2];
                         load(r, g, v);
+                        if (last) issue();
                         chunk(g, v);
                     } else if (U < 8 || left > C / 8) {
                         u32x4 v[U / 4];
                         load(r, g, v);
+                        if (last) issue();
                         chunk(g, v);
                     } else {
                         u32x4 v[U >= 8 ? U / 8 : 1];
                         load(r, g, v);
+                        if (last) issue();
                         chunk(g, v);
                     }
                 }
             }
         }
+        issue();  // (LATE: a tile with nothing streamed)
         const uint32_t res = pend - pst;  // sum of the packet's units, mod 2^32
         if (IPV4 && huge && mine && !range_bad) {  // not streamed (phase D redoes its sum): head units from the frame
             const auto* hu = gld(reinterpret_cast<const u32x4*>(a0));
@@ -1700,6 +1742,7 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
             }
             if (status) tile_store(status + base, lane, static_cast<uint8_t>(st), pol_st);
         }
+        if (LATE && claiming) t2 = src.claim_resolve(c2);
         src.retire(cur.ref);
         if (Src::kEngine && t1 < ntiles && !planned) {
             if (src.wait_ready(t1)) {
@@ -1723,19 +1766,19 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
 #endif
 }
 
-template <int U, bool IPV4, bool FILL, bool PIPE>
+template <int U, bool IPV4, bool FILL, bool PIPE, bool LATE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 ? 2 : 3))) void csum_flat_kernel(
     const Queues Q, uint32_t B, uint32_t* __restrict__ heads, uint32_t* __restrict__ done, uint32_t ticket,
     uint32_t flags, const RssParams rss) {
     QueueSrc src(Q, B, heads, done, ticket);
-    flat_body<U, IPV4, FILL, PIPE>(src, flags, rss);
+    flat_body<U, IPV4, FILL, PIPE, LATE>(src, flags, rss);
 }
 
 template <int U, bool IPV4>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 ? 2 : 3))) void csum_engine_kernel(
     const EngineArgs E, uint32_t flags) {
     EngineSrc src(E, flags);
-    flat_body<U, IPV4, false, false>(src, flags, RssParams{});
+    flat_body<U, IPV4, false, false, false>(src, flags, RssParams{});
 }
 
 // Fragment lists (checksummer::sum(const packet&), src/net/ip_checksum.cc:64-68):
@@ -2143,6 +2186,7 @@ int units_class(uint32_t max_len) {
 // every wave's static first tile starts at launch; tiles hold B packets (one
 // per lane, B <= 64, about tile_bytes of packets when that knob is set),
 // numbered across the queue set.
+constexpr uint64_t kLateClaimBytes = 49152;  // mean packet size from which a launch takes the LATE form
 using FlatKernel = void (*)(const Queues, uint32_t, uint32_t*, uint32_t*, uint32_t, uint32_t, const RssParams);
 
 // Resident 256-thread blocks per CU of a kernel (from its VGPR and LDS use),
@@ -2261,10 +2305,15 @@ hipError_t launch_flat_variant(int variant, hipStream_t s, int dev, Queues& Q, u
     auto go = [&](auto kern) { return launch_flat(kern, s, dev, Q, n_total, bytes_total, flags, rss); };
     constexpr bool F = IPV4;
     const bool fill = IPV4 && (flags & kFillFlags);
+    // packets of 48 KiB or more, one per tile: the claim read back a tile late
+    // (flat_body, LATE)
+    const bool late = n_total != 0 && bytes_total / n_total >= kLateClaimBytes;
     switch (variant) {
         case 14: return fill ? go(csum_flat_kernel<8, IPV4, F, false>) : go(csum_flat_kernel<8, IPV4, false, false>);
         case 15: return fill ? go(csum_flat_kernel<8, IPV4, F, true>) : go(csum_flat_kernel<8, IPV4, false, true>);
-        default: return fill ? go(csum_flat_kernel<16, IPV4, F, false>) : go(csum_flat_kernel<16, IPV4, false, false>);
+        default:
+            if (fill) return go(csum_flat_kernel<16, IPV4, F, false>);
+            return late ? go(csum_flat_kernel<16, IPV4, false, false, true>) : go(csum_flat_kernel<16, IPV4, false, false>);
     }
 }
 

@@ -7,7 +7,7 @@ set -e
 cd "$(dirname "$0")/.."
 mkdir -p seastar_amd/lib/ab
 SRC="seastar_amd/csrc/sccsum.hip seastar_amd/csrc/checksummer.cc seastar_amd/csrc/pipeline.cc seastar_amd/csrc/burst.cc"
-FL="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -Wall -Wno-unused-command-line-argument -I include ${AB_FLAGS:-}"
+FL="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -Wall -Wno-unused-command-line-argument -I include ${AB_FLAGS--mllvm -amdgpu-atomic-optimizer-strategy=None}"  # (build.py's device flags unless AB_FLAGS is set)
 pids=()
 for spec in "$@"; do
     name=${spec%%=*}
