@@ -1402,3 +1402,48 @@ def test_scratch_on_a_side_stream(dev, kernel_variant):
     want_buf, _, _ = oracle.batch_ipv4_fill(buf, off, length, m)
     assert np.array_equal(b.data.cpu().numpy()[: buf.size], want_buf)
     assert np.array_equal(batch.as_u16(got), oracle.batch_fragments(fb, fo, fl, first))
+
+
+@pytest.mark.parametrize("bpc,dynamic", [(8, 1), (1, 1), (2, 0)], ids=["grid", "one_block_per_cu", "static"])
+def test_late_claim_form_matches_oracle(dev, kernel_variant, bpc, dynamic):
+    """The U = 16 form reads its tile claims back a tile late for launches
+    whose mean packet is 48 KiB or more (sccsum.hip flat_body LATE, cfg 4).
+    Big spans and frames with tiny, empty, out-of-range and over-128 KiB
+    packets among them (tiles that stream nothing claim after the run loop),
+    seeds and status, on the full grid, one block per CU (more tiles per wave)
+    and static tile order; and a launch with fewer tiles than waves."""
+    if kernel_variant != 16:
+        pytest.skip("the LATE form is the U = 16 flat kernel's")
+    lib = native.load()
+    native.check(lib.sccsum_set_blocks_per_cu(bpc), "blocks_per_cu")
+    native.check(lib.sccsum_set_dynamic_tiles(dynamic), "dynamic")
+    try:
+        rng = np.random.default_rng(4000 + bpc)
+        n = 1500
+        lens = rng.integers(49152, 65537, n).astype(np.uint32)
+        lens[rng.choice(n, 40, replace=False)] = rng.choice([0, 1, 2, 7, 19, 20, 64], 40)
+        lens[rng.choice(n, 5, replace=False)] = [131_073, 140_000, 65_535, 200_001, 131_072]
+        assert lens.mean() >= 49152
+        off, total = synth.pack(lens, seed=4010 + bpc, max_gap=5)
+        buf = rng.integers(0, 256, size=int(total), dtype=np.uint8)
+        seeds = rng.integers(0, 65536, n).astype(np.uint32)
+        bad = [3, 700]
+        bad_off = off.copy()
+        bad_off[bad] = total + 1  # out of range (the oracle has no buffer length: those two are checked apart)
+        got, st = _spans(dev, buf, bad_off, lens, seeds, with_status=True)
+        want = oracle.batch_spans(buf, off, lens, seeds)
+        assert np.array_equal(np.delete(got, bad), np.delete(want, bad))
+        assert np.array_equal(np.delete(st, bad), np.delete((want == 0).astype(np.uint8), bad))
+        assert np.all(got[bad] == 0) and np.all(st[bad] == native.ST_RANGE)
+        flens = np.clip(lens, 28, 65535).astype(np.uint32)  # (UDP frames: 28 B at least)
+        fbuf, foff, flens, _ = synth.mixed_udp_frames(n, seed=4020 + bpc, max_gap=3, lengths=flens)
+        got, st = _frames(dev, fbuf, foff, flens)
+        want, want_st = oracle.batch_ipv4(fbuf, foff, flens)
+        assert np.array_equal(got, want) and np.array_equal(st, want_st)
+        small = lens[:37]  # fewer tiles than waves
+        o2, t2 = synth.pack(small, seed=4030, max_gap=1)
+        b2 = rng.integers(0, 256, size=int(t2), dtype=np.uint8)
+        assert np.array_equal(_spans(dev, b2, o2, small), oracle.batch_spans(b2, o2, small))
+    finally:
+        native.check(lib.sccsum_set_blocks_per_cu(8), "blocks_per_cu")
+        native.check(lib.sccsum_set_dynamic_tiles(1), "dynamic")
