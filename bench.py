@@ -53,9 +53,7 @@ def flat_kernel(ipv4: bool, fill: bool, n: int, nbytes: int) -> str:
     the next chunk in flight), as rocprofv3 names it."""
     big = n >= (512 << 10) and nbytes >= (256 << 20)
     u, pipe = (16, "false") if big else (8, "true")
-    # the U = 16 form reads its tile claims back late for packets of 48 KiB or more (flat_body, LATE)
-    late = big and not fill and nbytes // n >= 49152
-    return f"csum_flat_kernel<{u}, {str(ipv4).lower()}, {str(fill).lower()}, {pipe}, {str(late).lower()}>"
+    return f"csum_flat_kernel<{u}, {str(ipv4).lower()}, {str(fill).lower()}, {pipe}>"
 
 
 def sparse_kernel(args, ipv4: bool, max_len: int) -> str:

@@ -941,8 +941,9 @@ struct QueueSrc {
     // host memory): the host may then hand the slot to another launch
     // (acquire_heads).  Without `heads`: static round robin.
     // A claim in two halves, the atomic (claim_issue) and its read-back
-    // (claim_resolve); claim() does both at once (the flat body's LATE form
-    // issues after a tile's last loads and reads back after the tile).
+    // (claim_resolve): the flat body issues a tile's claim after the previous
+    // tile's last loads and reads it back after that tile; claim() does both
+    // at once (a wave's first claims).
     struct Claim {
         uint32_t raw;
         uint64_t prev;
@@ -1303,7 +1304,7 @@ struct EngineSrc {
     }
 };
 
-template <int U, bool IPV4, bool FILL, bool PIPE, bool LATE, class Src>
+template <int U, bool IPV4, bool FILL, bool PIPE, class Src>
 __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const RssParams& rss) {
     static_assert(!FILL || IPV4, "in-place generate is a frames mode");
     static_assert(!FILL || !Src::kEngine, "the engine does not fill in place");
@@ -1444,20 +1445,23 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
 #ifdef SCCSUM_AB_TIMELINE
         ++tl_tiles;
 #endif
-        // The claim of the tile after next.  Read back at once: its round trip
-        // stalls the wave here, before the tile's first loads.  LATE (tiles of
-        // one packet of 48 KiB or more): issued after the tile's last loads and
-        // read back after the tile, so the round trip overlaps the last chunk's:
-        // cfg 4 1.2 % faster, but Zipf tiles ran 8 % slower in steady state
-        // (profiles/r04_engine_groups.log, r04zf-r04zk).  The atomic optimizer is
-        // off (build.py): it would read the atomic back right where it is issued.
+        // The claim of the tile after next: issued after this tile's last loads
+        // (below) and read back after the tile, so its round trip overlaps the
+        // last chunk's.  Read back at once, where it is issued, it stalled the
+        // wave before every tile's first loads: cfg 2 +0.5 %, cfg 3 +1.3 %,
+        // cfg 4 +0.6-2.3 % this way (profiles/r04_engine_groups.log).  The
+        // atomic optimizer is off (build.py): it would read the atomic back
+        // where it is issued.
+        // (The chunk-in-flight forms, PIPE, read it back at once: their loads
+        // run a chunk ahead of the sums, so there is no last load to follow;
+        // issued after the run loop it ran small launches 2 % slower.)
         const bool claiming = t1 < ntiles;
         bool issued = false;
         typename Src::Claim c2{};
         uint64_t t2 = ntiles;
-        if (!LATE && claiming) t2 = next_tile(t1);
+        if (PIPE && claiming) t2 = next_tile(t1);
         auto issue = [&]() {
-            if (LATE && claiming && !issued) {
+            if (!PIPE && claiming && !issued) {
                 c2 = src.claim_issue(t1);
                 issued = true;
             }
@@ -1545,7 +1549,7 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
                 // profiles/r02_ab_short_chunks.log)
                 for (uint32_t g = 0; g < ext; g += C) {
                     const uint32_t left = ext - g;
-                    const bool last = LATE && last_run && left <= C;  // the tile's last loads
+                    const bool last = last_run && left <= C;  // the tile's last loads: then the claim
                     if (!short_chunks || left > C / 2) {
                         u32x4 v[U];
                         load(r, g, v);
@@ -1570,7 +1574,7 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
                 }
             }
         }
-        issue();  // (LATE: a tile with nothing streamed)
+        issue();  // (a tile that streamed nothing, or the chunk-in-flight forms)
         const uint32_t res = pend - pst;  // sum of the packet's units, mod 2^32
         if (IPV4 && huge && mine && !range_bad) {  // not streamed (phase D redoes its sum): head units from the frame
             const auto* hu = gld(reinterpret_cast<const u32x4*>(a0));
@@ -1742,7 +1746,10 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
             }
             if (status) tile_store(status + base, lane, static_cast<uint8_t>(st), pol_st);
         }
-        if (LATE && claiming) t2 = src.claim_resolve(c2);
+        // (readfirstlane: the compiler otherwise loses the tile number's
+        // uniformity across the issue branches and reads the next tile's queue
+        // fields with vector loads, 8 more per tile)
+        if (!PIPE && claiming) t2 = rfl64(src.claim_resolve(c2));
         src.retire(cur.ref);
         if (Src::kEngine && t1 < ntiles && !planned) {
             if (src.wait_ready(t1)) {
@@ -1766,19 +1773,19 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
 #endif
 }
 
-template <int U, bool IPV4, bool FILL, bool PIPE, bool LATE = false>
+template <int U, bool IPV4, bool FILL, bool PIPE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 ? 2 : 3))) void csum_flat_kernel(
     const Queues Q, uint32_t B, uint32_t* __restrict__ heads, uint32_t* __restrict__ done, uint32_t ticket,
     uint32_t flags, const RssParams rss) {
     QueueSrc src(Q, B, heads, done, ticket);
-    flat_body<U, IPV4, FILL, PIPE, LATE>(src, flags, rss);
+    flat_body<U, IPV4, FILL, PIPE>(src, flags, rss);
 }
 
 template <int U, bool IPV4>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 ? 2 : 3))) void csum_engine_kernel(
     const EngineArgs E, uint32_t flags) {
     EngineSrc src(E, flags);
-    flat_body<U, IPV4, false, false, false>(src, flags, RssParams{});
+    flat_body<U, IPV4, false, false>(src, flags, RssParams{});
 }
 
 // Fragment lists (checksummer::sum(const packet&), src/net/ip_checksum.cc:64-68):
@@ -2186,7 +2193,6 @@ int units_class(uint32_t max_len) {
 // every wave's static first tile starts at launch; tiles hold B packets (one
 // per lane, B <= 64, about tile_bytes of packets when that knob is set),
 // numbered across the queue set.
-constexpr uint64_t kLateClaimBytes = 49152;  // mean packet size from which a launch takes the LATE form
 using FlatKernel = void (*)(const Queues, uint32_t, uint32_t*, uint32_t*, uint32_t, uint32_t, const RssParams);
 
 // Resident 256-thread blocks per CU of a kernel (from its VGPR and LDS use),
@@ -2305,15 +2311,10 @@ hipError_t launch_flat_variant(int variant, hipStream_t s, int dev, Queues& Q, u
     auto go = [&](auto kern) { return launch_flat(kern, s, dev, Q, n_total, bytes_total, flags, rss); };
     constexpr bool F = IPV4;
     const bool fill = IPV4 && (flags & kFillFlags);
-    // packets of 48 KiB or more, one per tile: the claim read back a tile late
-    // (flat_body, LATE)
-    const bool late = n_total != 0 && bytes_total / n_total >= kLateClaimBytes;
     switch (variant) {
         case 14: return fill ? go(csum_flat_kernel<8, IPV4, F, false>) : go(csum_flat_kernel<8, IPV4, false, false>);
         case 15: return fill ? go(csum_flat_kernel<8, IPV4, F, true>) : go(csum_flat_kernel<8, IPV4, false, true>);
-        default:
-            if (fill) return go(csum_flat_kernel<16, IPV4, F, false>);
-            return late ? go(csum_flat_kernel<16, IPV4, false, false, true>) : go(csum_flat_kernel<16, IPV4, false, false>);
+        default: return fill ? go(csum_flat_kernel<16, IPV4, F, false>) : go(csum_flat_kernel<16, IPV4, false, false>);
     }
 }
 
