@@ -86,6 +86,8 @@ def parse():
                          "slots = cfg 2 frames in DPDK-mbuf-shaped slots in HBM (a sparse layout); frags = 9000 B "
                          "jumbo packets as 5-fragment mbuf chains in HBM (checksummer::sum(const packet&))")
     ap.add_argument("--tile-bytes", type=int, default=None, help="A/B: flat-kernel tile target (sccsum_diag.h)")
+    ap.add_argument("--tile-packets", type=int, default=None,
+                    help="A/B: flat-kernel packets-per-tile cap, <= 64 (sccsum_set_tile_packets)")
     ap.add_argument("--variant", type=int, default=None, help="A/B: kernel form (sccsum_set_kernel_variant)")
     ap.add_argument("--blocks-per-cu", type=int, default=None,
                     help="A/B: grid cap in workgroups per CU (sccsum_set_blocks_per_cu)")
@@ -1240,6 +1242,8 @@ def main():
         dev = torch.device("cuda", local)
         if args.tile_bytes is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_tile_bytes(args.tile_bytes), "sccsum_set_tile_bytes")
+        if args.tile_packets is not None:  # A/B only (sccsum_diag.h)
+            native.check(native.load().sccsum_set_tile_packets(args.tile_packets), "sccsum_set_tile_packets")
         if args.variant is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_kernel_variant(args.variant), "sccsum_set_kernel_variant")
         if args.blocks_per_cu is not None:  # A/B only (sccsum_diag.h)
