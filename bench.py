@@ -53,7 +53,9 @@ def flat_kernel(ipv4: bool, fill: bool, n: int, nbytes: int) -> str:
     the next chunk in flight), as rocprofv3 names it."""
     big = n >= (512 << 10) and nbytes >= (256 << 20)
     u, pipe = (16, "false") if big else (8, "true")
-    return f"csum_flat_kernel<{u}, {str(ipv4).lower()}, {str(fill).lower()}, {pipe}>"
+    # the chunk-in-flight (U = 8) form reads its claims back late for packets of 1 KiB+ in 256 MiB+ (PLATE)
+    plate = not big and nbytes // max(n, 1) >= 1024 and nbytes >= (256 << 20)
+    return f"csum_flat_kernel<{u}, {str(ipv4).lower()}, {str(fill).lower()}, {pipe}, {str(plate).lower()}>"
 
 
 def sparse_kernel(args, ipv4: bool, max_len: int) -> str:

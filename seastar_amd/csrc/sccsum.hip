@@ -1306,7 +1306,7 @@ struct EngineSrc {
     }
 };
 
-template <int U, bool IPV4, bool FILL, bool PIPE, class Src>
+template <int U, bool IPV4, bool FILL, bool PIPE, bool PLATE, class Src>
 __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const RssParams& rss) {
     static_assert(!FILL || IPV4, "in-place generate is a frames mode");
     static_assert(!FILL || !Src::kEngine, "the engine does not fill in place");
@@ -1454,16 +1454,20 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
         // cfg 4 +0.6-2.3 % this way (profiles/r04_engine_groups.log).  The
         // atomic optimizer is off (build.py): it would read the atomic back
         // where it is issued.
-        // (The chunk-in-flight forms, PIPE, read it back at once: their loads
-        // run a chunk ahead of the sums, so there is no last load to follow;
-        // issued after the run loop it ran small launches 2 % slower.)
+        // The chunk-in-flight forms (PIPE, small launches) issue it after their
+        // last real chunk load (PLATE) only for launches of 1 KiB+ packets and
+        // 256 MiB+: 2 x 131 072 x 1500 B frames ran 5.5-6 % faster that way,
+        // 262 144 Zipf frames 4.7 % and 2 x 32 768 frames 3.5 % slower
+        // (profiles/r04_engine_groups.log, r05e-r05f).  Otherwise they read it
+        // back at once.
+        constexpr bool kLate = !PIPE || PLATE;
         const bool claiming = t1 < ntiles;
         bool issued = false;
         typename Src::Claim c2{};
         uint64_t t2 = ntiles;
-        if (PIPE && claiming) t2 = next_tile(t1);
+        if (!kLate && claiming) t2 = next_tile(t1);
         auto issue = [&]() {
-            if (!PIPE && claiming && !issued) {
+            if (kLate && claiming && !issued) {
                 c2 = src.claim_issue(t1);
                 issued = true;
             }
@@ -1537,11 +1541,15 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
             };
             if (PIPE) {
                 u32x4 va[U], vb[U];
+                const uint32_t lastg = last_run ? ((ext - 1u) / C) * C : ~0u;  // the run's last real chunk
                 load(r, 0, va);
+                if (lastg == 0u) issue();
                 for (uint32_t g = 0; g < ext; g += 2 * C) {
                     load(r, g + C, vb);
+                    if (g + C == lastg) issue();
                     chunk(g, va);
                     load(r, g + 2 * C, va);
+                    if (g + 2 * C == lastg) issue();
                     chunk(g + C, vb);
                 }
             } else {
@@ -1751,7 +1759,7 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
         // (readfirstlane: the compiler otherwise loses the tile number's
         // uniformity across the issue branches and reads the next tile's queue
         // fields with vector loads, 8 more per tile)
-        if (!PIPE && claiming) t2 = rfl64(src.claim_resolve(c2));
+        if (kLate && claiming) t2 = rfl64(src.claim_resolve(c2));
         src.retire(cur.ref);
         if (Src::kEngine && t1 < ntiles && !planned) {
             if (src.wait_ready(t1)) {
@@ -1775,19 +1783,19 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
 #endif
 }
 
-template <int U, bool IPV4, bool FILL, bool PIPE>
+template <int U, bool IPV4, bool FILL, bool PIPE, bool PLATE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 ? 2 : 3))) void csum_flat_kernel(
     const Queues Q, uint32_t B, uint32_t* __restrict__ heads, uint32_t* __restrict__ done, uint32_t ticket,
     uint32_t flags, const RssParams rss) {
     QueueSrc src(Q, B, heads, done, ticket);
-    flat_body<U, IPV4, FILL, PIPE>(src, flags, rss);
+    flat_body<U, IPV4, FILL, PIPE, PLATE>(src, flags, rss);
 }
 
 template <int U, bool IPV4>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 ? 2 : 3))) void csum_engine_kernel(
     const EngineArgs E, uint32_t flags) {
     EngineSrc src(E, flags);
-    flat_body<U, IPV4, false, false>(src, flags, RssParams{});
+    flat_body<U, IPV4, false, false, false>(src, flags, RssParams{});
 }
 
 // Fragment lists (checksummer::sum(const packet&), src/net/ip_checksum.cc:64-68):
@@ -2315,9 +2323,16 @@ hipError_t launch_flat_variant(int variant, hipStream_t s, int dev, Queues& Q, u
     auto go = [&](auto kern) { return launch_flat(kern, s, dev, Q, n_total, bytes_total, flags, rss); };
     constexpr bool F = IPV4;
     const bool fill = IPV4 && (flags & kFillFlags);
+    // the chunk-in-flight form's late claim pays for packets of 1 KiB or more in
+    // launches of several tiles per wave (flat_body, PLATE): one tile per wave
+    // (2 x 32 768 frames) ran 3.5 % slower with it, the launch's last atomic
+    // then waited on at the wave's end
+    const bool plate = n_total != 0 && bytes_total / n_total >= 1024u && bytes_total >= (uint64_t(256) << 20);
     switch (variant) {
         case 14: return fill ? go(csum_flat_kernel<8, IPV4, F, false>) : go(csum_flat_kernel<8, IPV4, false, false>);
-        case 15: return fill ? go(csum_flat_kernel<8, IPV4, F, true>) : go(csum_flat_kernel<8, IPV4, false, true>);
+        case 15:
+            if (fill) return plate ? go(csum_flat_kernel<8, IPV4, F, true, true>) : go(csum_flat_kernel<8, IPV4, F, true>);
+            return plate ? go(csum_flat_kernel<8, IPV4, false, true, true>) : go(csum_flat_kernel<8, IPV4, false, true>);
         default: return fill ? go(csum_flat_kernel<16, IPV4, F, false>) : go(csum_flat_kernel<16, IPV4, false, false>);
     }
 }

@@ -44,8 +44,8 @@ def test_bench_line_has_the_contract_fields():
     assert cpu["physical_cores"]["l3_domains_host"] >= 1 and "one_l3_domain" in cpu
     args = argparse.Namespace(pmc=None, steps=200, warmup=5)
     alg = 3_176_136_704
-    roof = bench.roofline(alg, 460e-6, "udp1500", "csum_flat_kernel<16, true, false, false>",
-                          {"kernel": "csum_flat_kernel<16, true, false, false>", "skip": 9, "count": 200}, args)
+    roof = bench.roofline(alg, 460e-6, "udp1500", "csum_flat_kernel<16, true, false, false, false>",
+                          {"kernel": "csum_flat_kernel<16, true, false, false, false>", "skip": 9, "count": 200}, args)
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in roof, k
     assert roof["bound"] == "hbm" and roof["unit"] == "GB/s" and roof["peak"] == bench.HBM_PEAK_GBPS
