@@ -88,3 +88,21 @@ def test_e2e_line_names_the_slowest_rank():
         r["variants"]["C_strided_dma"]["GiBps_packet_bytes"] = float(r["variants"]["C_strided_dma"]["GiBps_packet_bytes"])
     check_e2e_line({"n_gpus": 8, "best_variant": "C_strided_dma", "variants": {"C_strided_dma": {}}, "per_rank": ranks,
                     "ranks_summary": s}, 8)
+
+
+def test_flat_kernel_names_follow_the_library_choice():
+    """bench.py names the flat-kernel instantiation rocprofv3 will report,
+    which selects the timed dispatches from a trace: U = 16 for launches of
+    512 Ki+ packets and 256 MiB+, else U = 8 with a chunk in flight, whose
+    late-claim form (PLATE) the library picks for 1 KiB+ packets in 256 MiB+
+    (sccsum.hip launch_flat_variant)."""
+    bench = _bench()
+    mi, kb = 1 << 20, 1 << 10
+    assert bench.flat_kernel(True, False, 2 * mi, 2 * mi * 1500) == "csum_flat_kernel<16, true, false, false, false>"
+    assert bench.flat_kernel(True, True, mi, mi * 1500) == "csum_flat_kernel<16, true, true, false, false>"
+    assert bench.flat_kernel(False, False, 2 * mi, 2 * mi * 65536) == "csum_flat_kernel<16, false, false, false, false>"
+    # small launches: 2 x 131 072 x 1500 B (393 MB) late, Zipf and 196 MB batches read back at once
+    assert bench.flat_kernel(True, False, 256 * kb, 256 * kb * 1500) == "csum_flat_kernel<8, true, false, true, true>"
+    assert bench.flat_kernel(True, False, 128 * kb, 128 * kb * 1500) == "csum_flat_kernel<8, true, false, true, false>"
+    assert bench.flat_kernel(True, False, 262144, 262144 * 442) == "csum_flat_kernel<8, true, false, true, false>"
+    assert bench.flat_kernel(True, True, 256 * kb, 256 * kb * 1500) == "csum_flat_kernel<8, true, true, true, true>"
