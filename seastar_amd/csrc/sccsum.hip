@@ -1341,7 +1341,12 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
     // Every wave still makes exactly one failing dequeue (the counter reset
     // relies on it).  (One tile ahead instead lost: profiles/r04_ab_dequeue_depth.log.)
     uint64_t t = src.first();
-    uint64_t t1 = t < ntiles ? next_tile(t) : ntiles;
+    // A launch's first claim (tile t1) is issued after the first tile's plan
+    // loads and read back after its derive, so the two round trips of a
+    // wave's start overlap (the late-claim forms; see the tile loop).
+    constexpr bool kLate = !PIPE || PLATE;
+    constexpr bool kLateStart = kLate && !Src::kEngine;
+    uint64_t t1 = (!kLateStart && t < ntiles) ? next_tile(t) : ntiles;
     auto plan_load = [&](const Ref& tr, bool valid, uint64_t& o_, uint32_t& L_, uint32_t& sd_) {
         const uint32_t c_ = valid ? tr.cnt : 0u;
         const uint64_t q_ = tr.base + (lane < c_ ? lane : 0);
@@ -1438,6 +1443,12 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
         r_n = src.ref(t < ntiles ? t : 0);
         plan_load(r_n, t < ntiles, o_n, L_n, sd_n);
     }
+    typename Src::Claim c1{};
+    bool c1p = false;
+    if (kLateStart && t < ntiles) {
+        c1 = src.claim_issue(t);
+        c1p = true;
+    }
     Tile cur{};
 #ifdef SCCSUM_AB_TIMELINE
     const unsigned long long tl_start = wall_clock64();
@@ -1460,19 +1471,22 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
         // 262 144 Zipf frames 4.7 % and 2 x 32 768 frames 3.5 % slower
         // (profiles/r04_engine_groups.log, r05e-r05f).  Otherwise they read it
         // back at once.
-        constexpr bool kLate = !PIPE || PLATE;
+        uint64_t t2 = ntiles;
+        if (!kLate && t1 < ntiles) t2 = next_tile(t1);
+        cur = derive(r_n, o_n, L_n, sd_n);
+        if (kLateStart && c1p) {  // the launch's first claim (above)
+            t1 = rfl64(src.claim_resolve(c1));
+            c1p = false;
+        }
         const bool claiming = t1 < ntiles;
         bool issued = false;
         typename Src::Claim c2{};
-        uint64_t t2 = ntiles;
-        if (!kLate && claiming) t2 = next_tile(t1);
         auto issue = [&]() {
             if (kLate && claiming && !issued) {
                 c2 = src.claim_issue(t1);
                 issued = true;
             }
         };
-        cur = derive(r_n, o_n, L_n, sd_n);
         // an engine's next tile may belong to a step not published yet: its plan
         // then waits until this tile is done (a wave never waits holding work)
         bool planned = false;
