@@ -114,7 +114,8 @@ def parse():
                          "(multi; udp1500's default) or one sccsum_ipv4_frames launch per batch (single; mixed: "
                          "the rx batch only, mixed's default — its multi step measured 1-2 %% slower on three "
                          "boxes, DESIGN.md §5.3); engine = one resident grid per timed run, the steps submitted "
-                         "into it as they go, at most 2 in flight (sccsum_engine_*, DESIGN.md §5.11)")
+                         "into it as they go, at most --engine-in-flight in flight (sccsum_engine_*, DESIGN.md "
+                         "§5.11; fill: sccsum_engine_submit_fill)")
     ap.add_argument("--rx-out2", action="store_true",
                     help="udp1500 / mixed: the verify (rx) half also writes both checksums per frame (default: status "
                          "bits only, what the reference's verify keeps: ip.cc:121-127, tcp.hh:876-883)")
@@ -621,7 +622,7 @@ def run_udp1500(args, world, rank, dev):
     if multi:  # the tx and rx batches of a step form ONE launch of 2 * n frames
         kern = flat_kernel(True, False, 2 * n, 2 * n * FRAME)
     if engine:  # one resident grid per run; each step (tx + rx batch) submitted into it
-        kern = "csum_engine_kernel<16, true>"
+        kern = "csum_engine_kernel<16, true, false>"
         streams = streams[:1]
         ns = 1
 
@@ -805,7 +806,7 @@ def run_mixed(args, world, rank, dev):
     warm = max(args.warmup, R)
     step, begin, end, eng = (lambda k: pre[(k % R, k % ns)](streams[k % ns])), None, None, None
     if engine:  # the single form's steps, submitted into one resident grid per run
-        kern = "csum_engine_kernel<16, true>"
+        kern = "csum_engine_kernel<16, true, false>"
         eng = batch.Engine(dev.index or 0, frames=True, max_steps=max(warm, args.steps) + 4,
                            max_in_flight=args.engine_in_flight)
         pre_e = {r: eng.prepare([(rxs[r], outs[0][1], None)]) for r in range(R)}
@@ -989,9 +990,14 @@ def run_fill(args, world, rank, dev):
     """cfg 2 tx side with in-place write-back: IPv4 header +
     UDP checksums generated and stored into the frames (wire-ready), over R
     rotated 1 M x 1500 B batches (generate ignores the fields' old contents,
-    so repeated steps are identical work)."""
+    so repeated steps are identical work).  A step is one sccsum_ipv4_fill
+    call (generate launch + store launch; --launch single, the default) or one
+    fill submitted into a resident engine grid per timed run (--launch engine:
+    sccsum_engine_submit_fill, a generate step and the store step that waits
+    for it)."""
     n = args.packets
     R = max(1, args.rotate)
+    engine = args.launch == "engine"
     bs = [devsynth.udp_frames(n, FRAME, seed=SEED + 7 * rank + 13 * r, device=dev) for r in range(R)]
     mode = native.FILL_IP | native.FILL_L4
     st = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -1003,20 +1009,49 @@ def run_fill(args, world, rank, dev):
     kern = flat_kernel(True, True, n, n * FRAME)
     LAUNCHES.add(kern, R)
     streams = make_streams(args, dev)
-    if R % len(streams):  # a batch filled in place must always come back to the same stream
+    if R % len(streams) or engine:  # a batch filled in place must always come back to the same stream
         streams = streams[:1]
     ns = len(streams)
     warm = max(args.warmup, R)
-    LAUNCHES.add(kern, warm)
-    sel = LAUNCHES.select(kern, args.steps)
     # prebuilt launches; the caller's out2 (the values stored) carries the generate pass's
     # words to the store pass, so no per-call scratch allocation is timed
     outs2 = [torch.empty(2 * n, dtype=torch.int16, device=dev) for _ in range(ns)]
-    pre = {(r, i): batch.prepare_call("sccsum_ipv4_fill", bs[r].data, bs[r].bytes_len, bs[r].off, bs[r].length,
-                                      outs2[i], None, bs[r].n, bs[r].max_len, mode)
-           for r in range(R) for i in range(ns)}
-    wall, launch_s = timed(lambda k: pre[(k % R, k % ns)](streams[k % ns]), args.steps, warm, world, streams)
+    begin = end = eng = None
+    if engine:  # one resident grid per timed run; each step = one fill (generate step + store step)
+        kern = "csum_engine_kernel<16, true, true>"
+        eng = batch.Engine(dev.index or 0, frames=True, fill=True, max_steps=2 * max(warm, args.steps) + 4,
+                           max_in_flight=max(2, args.engine_in_flight))
+        # one out2 per batch: a fill's store step reads its generate step's values from out2 while
+        # the next fills run (sccsum.h: no other step may write a fill's d_out until it is done)
+        outs2 = [torch.empty(2 * n, dtype=torch.int16, device=dev) for _ in range(R)]
+        pre_e = {r: eng.prepare([(bs[r], outs2[r], None)], fill_mode=mode) for r in range(R)}
+
+        def step(k):
+            eng.submit_prepared(pre_e[k % R])
+
+        def begin():
+            eng.start(streams[0])
+
+        end = eng.stop
+    else:
+        pre = {(r, i): batch.prepare_call("sccsum_ipv4_fill", bs[r].data, bs[r].bytes_len, bs[r].off,
+                                          bs[r].length, outs2[i], None, bs[r].n, bs[r].max_len, mode)
+               for r in range(R) for i in range(ns)}
+
+        def step(k):
+            pre[(k % R, k % ns)](streams[k % ns])
+    LAUNCHES.add(kern, 1 if engine else warm)
+    sel = LAUNCHES.select(kern, 1 if engine else args.steps)
+    wall, launch_s = timed(step, args.steps, warm, world, streams, begin, end)
     alg = n * (FRAME + META_BYTES + 4)  # read every byte + metadata, write the two 2-byte fields
+    roof_alg, roof_s = alg, launch_s
+    if engine:  # the launch is the run: every step's bytes over the run's time (the same ratio)
+        roof_alg, roof_s = alg * args.steps, launch_s * args.steps
+        eng.close()
+        for b in bs:  # the engine's fills verify too
+            batch.ipv4_frames(b, status=st)
+            torch.cuda.synchronize()
+            assert args.no_check or int((st != 3).sum()) == 0, "engine-filled frames do not verify"
     ranks = per_rank(world, rank, dev, **rank_rate(n * FRAME, args.steps), avg_launch_us=launch_s * 1e6,
                      frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS)
     if rank == 0:
@@ -1024,11 +1059,18 @@ def run_fill(args, world, rank, dev):
              world * n * FRAME * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": "cfg2 tx: 1500 B IPv4/UDP frames, IP + UDP checksums generated and stored in place",
               "packets_per_gpu": n, "rotation": f"{R} distinct batches launched in turn",
+              "launch": (f"one resident engine grid per timed run (sccsum_engine_submit_fill): each step's fill "
+                         f"= a generate step + the store step that waits for it, at most "
+                         f"{max(2, args.engine_in_flight)} steps in flight" if engine
+                         else "one sccsum_ipv4_fill call per step (generate launch + store launch)"),
               "streams": f"{ns} (step k on stream k % {ns})", "parallelism": f"{world} independent shards"},
-             roofline(alg, launch_s, "fill", kern + " + fill_store_kernel (sccsum_ipv4_fill: generate pass, "
-                                                    "then the field-store pass)", sel, args,
-                      {"trace_select_extra": [{"kernel": "fill_store_kernel", "skip": sel["skip"],
-                                               "count": sel["count"]}]}), extra={"per_rank": ranks})
+             roofline(roof_alg, roof_s, "fill_engine" if engine else "fill",
+                      kern + (" (sccsum_engine_submit_fill: generate + store steps; one launch = the timed run)"
+                              if engine else " + fill_store_kernel (sccsum_ipv4_fill: generate pass, "
+                                             "then the field-store pass)"), sel, args,
+                      None if engine else {"trace_select_extra": [{"kernel": "fill_store_kernel",
+                                                                   "skip": sel["skip"], "count": sel["count"]}]}),
+             extra={"per_rank": ranks})
 
 
 def run_sweep(args, world, rank, dev):

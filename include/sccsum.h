@@ -84,13 +84,20 @@ extern "C" {
 
 /* 2 (round 3): frames leave IP fragments' L4 alone (SCCSUM_ST_IPFRAG), L4
  * values of protocols other than TCP / UDP carry no pseudo-header, fill gained
- * SCCSUM_FILL_ICMP_ECHO ("Migration from ABI 1"). */
-#define SCCSUM_ABI_VERSION 2
+ * SCCSUM_FILL_ICMP_ECHO ("Migration from ABI 1").
+ * 3 (round 5): a launch on a stream of another device is SCCSUM_EINVAL and a
+ * pending HIP error is left pending (round 4, unversioned then); the engine
+ * gained SCCSUM_EIDLE, fill steps (SCCSUM_ENGINE_FILL,
+ * sccsum_engine_submit_fill), one running engine per device
+ * (sccsum_engine_start: SCCSUM_EBUSY), and sccsum_engine_create no longer
+ * changes the caller's current device. */
+#define SCCSUM_ABI_VERSION 3
 
 #define SCCSUM_OK 0
 #define SCCSUM_EINVAL (-1)   /* bad argument (null pointer, misalignment) */
 #define SCCSUM_ENODEV (-2)   /* no HIP device / device index out of range */
-#define SCCSUM_EBUSY  (-3)   /* burst queue: every batch slot is in flight; poll and retry */
+#define SCCSUM_EBUSY  (-3)   /* burst queue: every batch slot is in flight; poll and retry.  engine: the
+                                run's steps are used up, a wait timed out, or another engine runs on the device */
 #define SCCSUM_EIDLE  (-4)   /* engine: its grid gave up waiting for steps (idle limit); start a new run */
 
 /* per-packet status bits (d_status) */
@@ -204,15 +211,25 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  * batches (a step's tx and rx halves, a shard's rx queues), computed exactly
  * as sccsum_*_multi would compute them, and its tiles flow into the same
  * grid without a boundary.  Per step the engine reports completion; its
- * results are written through to device memory, so they may be read (any
- * stream, hipMemcpy) as soon as sccsum_engine_wait returns for it.
+ * results are written through to device memory, so a DEVICE-TO-HOST copy
+ * (hipMemcpy / hipMemcpyAsync to host memory, which a copy engine runs) may
+ * read them as soon as sccsum_engine_wait returns for the step.  Anything
+ * that runs as a kernel on the device — another library launch, a torch op,
+ * a device-to-device copy that HIP runs as a blit kernel — waits for the run
+ * to stop (see "Sharing the device" below).
  *
  *   sccsum_engine_create(device, mode, max_steps, max_in_flight, &e)
- *       mode SCCSUM_PIPE_IPV4 (frames) or SCCSUM_PIPE_SPANS; at most
- *       max_steps (1..65536) steps per run (descriptors are never reused
- *       within a run: max_steps x 512 B of pinned memory and as much device
- *       memory), at most max_in_flight (1..64) submitted and not yet done.
- *   sccsum_engine_start(e, stream)      launch the grid on `stream` (a run)
+ *       mode SCCSUM_PIPE_IPV4 (frames) or SCCSUM_PIPE_SPANS, frames may add
+ *       SCCSUM_ENGINE_FILL (the run also takes fill steps; max_in_flight >= 2);
+ *       at most max_steps (1..65536) steps per run (descriptors are never
+ *       reused within a run: max_steps x 512 B of pinned memory and as much
+ *       device memory), at most max_in_flight (1..64) submitted and not yet
+ *       done.  Allocates on `device`; the calling thread's current device is
+ *       left as it was.
+ *   sccsum_engine_start(e, stream)      launch the grid on `stream` (a run);
+ *       `stream` belongs to the engine's device, which must be the calling
+ *       thread's current device (sccsum_init(device)).  SCCSUM_EBUSY when
+ *       another engine of this process runs on the device.
  *   sccsum_engine_submit(e, batches, nbatch, max_len, timeout_ns, &step)
  *       publish one step; waits (spinning, up to timeout_ns) while
  *       max_in_flight steps are pending.  SCCSUM_EBUSY: the run already took
@@ -221,22 +238,43 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  *       the engine always runs the flat kernel, so sparse layouts give exact
  *       results but belong on the launches, whose row kernel reads them
  *       faster.  Frames take no seeds.
+ *   sccsum_engine_submit_fill(e, batches, nbatch, mode, timeout_ns, &step)
+ *       an in-place fill (sccsum_ipv4_fill's SCCSUM_FILL_L4 and/or
+ *       SCCSUM_FILL_ICMP_ECHO, optionally | SCCSUM_FILL_IP) of every batch,
+ *       as two steps: a generate step (the flat kernel's fill values into each
+ *       batch's d_out, required here, and the status bits into d_status) and a
+ *       store step whose tiles wait for the generate step and write the values
+ *       into the frames' fields (d_bytes is written).  *step = the store step:
+ *       once it is done the frames are wire-ready in device memory and d_out
+ *       holds the values stored.  Both steps or neither are published (a
+ *       fill takes 2 of the run's max_steps).  The store step reads the values
+ *       from d_out: no other step may write a fill's d_out (nor its frames)
+ *       before the fill is done.
  *   sccsum_engine_wait(e, step, timeout_ns)   0 once the step is done
  *   sccsum_engine_stop(e)               no more steps: the grid leaves once the
  *       published steps are done (synchronise `stream` to wait for it)
  *   sccsum_engine_destroy(e)            stops and synchronises a running engine
  *
- * The grid holds the device's compute units while it runs (every CU, all of
- * their LDS): other kernels on the device wait for the run to stop.  A grid
- * left without steps and without a stop for 1 s leaves on its own, and every
- * later call on that run returns SCCSUM_EIDLE.  One engine belongs to one host
- * thread, like a burst queue. */
+ * Sharing the device.  The grid holds the device's compute units while it
+ * runs (every CU, all of their LDS): kernels that other threads or streams
+ * launch on the device — this library's launches included — queue until the
+ * run stops, and then complete.  So one engine runs per device at a time
+ * (per process: a second start returns SCCSUM_EBUSY until the first run's
+ * stop), and a shard that shares its GPU with other shards should use
+ * launches, or own the engine's device for the run.  A grid given no new step
+ * (and no stop) for 1 s leaves on its own, and every later call on that run
+ * returns SCCSUM_EIDLE: the limit counts from the last step the grid
+ * received, so steady light traffic never trips it.  One engine belongs to
+ * one host thread, like a burst queue. */
 #define SCCSUM_ENGINE_MAX_BATCHES 4
+#define SCCSUM_ENGINE_FILL 0x100 /* sccsum_engine_create mode flag: the run takes fill steps too */
 typedef struct sccsum_engine sccsum_engine;
 int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, sccsum_engine** out);
 int sccsum_engine_start(sccsum_engine* e, void* stream);
 int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
                          uint64_t timeout_ns, uint64_t* step);
+int sccsum_engine_submit_fill(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t mode,
+                              uint64_t timeout_ns, uint64_t* step);
 int sccsum_engine_wait(sccsum_engine* e, uint64_t step, uint64_t timeout_ns);
 int sccsum_engine_stop(sccsum_engine* e);
 int sccsum_engine_destroy(sccsum_engine* e);

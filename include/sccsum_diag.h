@@ -62,6 +62,10 @@ int sccsum_set_out_policy(int policy);
  * launch stores them (out_policy and the 128-byte rule) with an agent-scope
  * release before each step's completion count (0).  A/B only. */
 int sccsum_set_engine_write_through(int on);
+/* Engine runs started later by this thread: how long the grid may go without
+ * a new step before its waiting waves give up and the run reports
+ * SCCSUM_EIDLE (default 1000 ms; 1 .. 3 600 000).  Tests shorten it. */
+int sccsum_set_engine_idle_ms(int ms);
 
 /* Flat kernel forms without a chunk in flight (U 8 form 14, U 16): a run's
  * last chunk loads and scans only the rows its units reach, U / 8 .. U (1, the

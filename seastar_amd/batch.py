@@ -434,20 +434,29 @@ class Engine:
         eng = Engine(device=0, frames=True, max_steps=1024, max_in_flight=2)
         eng.start(stream)
         step = eng.submit([(tx, out2, None), (rx, None, status)])   # like prepare_ipv4_frames_multi's items
-        eng.wait(step)                                               # results readable on any stream
+        eng.wait(step)                                               # results readable by a D2H copy
         eng.stop(); stream.synchronize()
 
-    A step's tensors must stay alive (and unmodified) until its wait returns;
-    submit keeps a reference until then."""
+    fill=True (frames): the run also takes in-place fills, each as a generate
+    step and a store step (sccsum_engine_submit_fill):
+        step = eng.submit_fill([(frames, out2, status)], FILL_IP | FILL_L4)
 
-    def __init__(self, device: int = 0, frames: bool = True, max_steps: int = 1024, max_in_flight: int = 2):
+    A step's tensors must stay alive (and unmodified) until its wait returns;
+    submit keeps a reference until then.  One engine runs per device at a time
+    (start raises SccsumError(SCCSUM_EBUSY) while another engine's run holds
+    it); while it runs, every other kernel on the device waits for its stop."""
+
+    def __init__(self, device: int = 0, frames: bool = True, max_steps: int = 1024, max_in_flight: int = 2,
+                 fill: bool = False):
         self._lib = native.load()
         h = ctypes.c_void_p()
-        native.check(self._lib.sccsum_engine_create(int(device), native.PIPE_IPV4 if frames else native.PIPE_SPANS,
-                                                     int(max_steps), int(max_in_flight), ctypes.byref(h)),
+        mode = (native.PIPE_IPV4 if frames else native.PIPE_SPANS) | (native.ENGINE_FILL if fill else 0)
+        native.check(self._lib.sccsum_engine_create(int(device), mode, int(max_steps), int(max_in_flight),
+                                                     ctypes.byref(h)),
                      "sccsum_engine_create")
         self._h = h
         self.frames = frames
+        self.fill = fill
         self.max_in_flight = int(max_in_flight)
         self._keep: dict[int, tuple] = {}
         self._stream = None
@@ -458,12 +467,15 @@ class Engine:
         self._stream = s
         self._keep.clear()
 
-    def prepare(self, items):
+    def prepare(self, items, fill_mode: int = 0):
         """A step's descriptor array, checked once (items as for
         prepare_ipv4_frames_multi: (PacketBatch, out | None, status | None
-        [, seeds])); submit_prepared(prep) then only crosses the C-ABI."""
+        [, seeds])); submit_prepared(prep) then only crosses the C-ABI.
+        fill_mode != 0: an in-place fill of the items (out2 required)."""
         if not items or len(items) > native.ENGINE_MAX_BATCHES:
             raise ValueError(f"1..{native.ENGINE_MAX_BATCHES} batches per step")
+        if fill_mode and not self.fill:
+            raise ValueError("fill steps need Engine(..., fill=True)")
         width = 2 if self.frames else 1
         parts = []
         for i, it in enumerate(items):  # every item is checked before any is built
@@ -471,6 +483,8 @@ class Engine:
             seeds = it[3] if len(it) > 3 else None
             if self.frames and seeds is not None:
                 raise ValueError("frames take no seeds")
+            if fill_mode and out is None:
+                raise ValueError(f"batch {i}: a fill step needs out2 (the values pass through it)")
             if out is None and status is None:
                 raise ValueError(f"batch {i}: give out, status or both")
             _need(out, width * b.n, torch.int16, f"batch {i} out", b.device)
@@ -481,14 +495,19 @@ class Engine:
         for i, (b, out, status, seeds) in enumerate(parts):
             arr[i] = native.Batch(ctypes_ptr(b.data), b.bytes_len, ctypes_ptr(b.off), ctypes_ptr(b.length),
                                   _ptr(seeds), _ptr(out), _ptr(status), b.n)
-        return (arr, len(items), max(b.max_len for b, _, _, _ in parts), items)
+        return (arr, len(items), max(b.max_len for b, _, _, _ in parts), items, int(fill_mode))
 
     def submit_prepared(self, prep, timeout_s: float = 10.0) -> int:
-        arr, nb, ml, items = prep
+        arr, nb, ml, items, fill_mode = prep
         step = ctypes.c_uint64()
-        native.check(self._lib.sccsum_engine_submit(self._h, ctypes.cast(arr, ctypes.c_void_p), nb, ml,
-                                                     int(timeout_s * 1e9), ctypes.byref(step)),
-                     "sccsum_engine_submit")
+        if fill_mode:
+            native.check(self._lib.sccsum_engine_submit_fill(self._h, ctypes.cast(arr, ctypes.c_void_p), nb,
+                                                              fill_mode, int(timeout_s * 1e9), ctypes.byref(step)),
+                         "sccsum_engine_submit_fill")
+        else:
+            native.check(self._lib.sccsum_engine_submit(self._h, ctypes.cast(arr, ctypes.c_void_p), nb, ml,
+                                                         int(timeout_s * 1e9), ctypes.byref(step)),
+                         "sccsum_engine_submit")
         self._keep[step.value] = prep
         for s in [k for k in self._keep if k + self.max_in_flight < step.value]:
             del self._keep[s]  # done: submit waited for it
@@ -496,6 +515,11 @@ class Engine:
 
     def submit(self, items, timeout_s: float = 10.0) -> int:
         return self.submit_prepared(self.prepare(items), timeout_s)
+
+    def submit_fill(self, items, mode: int = native.FILL_IP | native.FILL_L4, timeout_s: float = 10.0) -> int:
+        """In-place fill of items [(PacketBatch, out2, status | None), ...]:
+        returns the store step, done once the frames hold their checksums."""
+        return self.submit_prepared(self.prepare(items, fill_mode=mode), timeout_s)
 
     def wait(self, step: int, timeout_s: float = 10.0) -> None:
         native.check(self._lib.sccsum_engine_wait(self._h, int(step), int(timeout_s * 1e9)), "sccsum_engine_wait")

@@ -930,6 +930,10 @@ struct QueueSrc {
     __device__ uint16_t* out(const Ref& r) const { return Q.out[r.q]; }
     __device__ uint8_t* status(const Ref& r) const { return Q.status[r.q]; }
     __device__ uint32_t tile_packets(const Ref&) const { return B; }
+    // a launch's tiles are all of one kind, its fill flags the kernel's
+    __device__ bool is_store(const Ref&) const { return false; }
+    __device__ uint32_t fill_flags(const Ref&, uint32_t flags) const { return flags; }
+    __device__ uint32_t store_mode(const Ref&) const { return 0u; }
 
     // Tile order.  Wave w first takes tile w (static: no start-up contention).
     // With `heads`, the remaining tiles [W, ntiles) are split over kGroups
@@ -1012,9 +1016,20 @@ struct QueueSrc {
 // are written through (sc0 sc1) and counted per step and group; the last count
 // of a step stores the step's ticket into its pinned done word.  Exit: the
 // host sets stop (ctl[8]); a wave that needs a tile past every published step
-// then leaves — and so does one that has waited `idle_ticks` with no stop (it
-// raises ctl[16] first).
-constexpr uint32_t kEngineQueues = 4;
+// then leaves — and so does one that finds the grid given no step for
+// `idle_ticks` (the poller stamps the time it last saw a new step), raising
+// ctl[16] first.
+//
+// In-place fill through the engine (sccsum_engine_submit_fill): a fill is two
+// steps.  The GENERATE step runs the flat body's FILL phase C (values into the
+// caller's out2, nothing stored in the frames); the STORE step that follows it
+// has lane-per-frame tiles that store those values into the frames' fields.
+// The store step depends on its generate step: a wave whose next tile lies in
+// it waits (after finishing what it holds) until the generate step's count is
+// complete, read from a device copy of the steps' done words.  No wave can
+// wait on itself: a store tile is only ever waited on by a wave that holds
+// nothing older, and every generate tile precedes it in its group's claim
+// order, so the chain of waits runs to strictly older tiles and ends.
 constexpr uint32_t kEngineSlotWords = 64;  // 512-byte descriptors
 constexpr uint32_t kEngineCountSlots = 64;  // completion counters: steps in flight at most
 constexpr uint32_t kEngineMaxSteps = 1u << 16;  // steps per run (2 x 32 MiB of descriptor rings at most)
@@ -1024,11 +1039,29 @@ constexpr uint32_t kEdTiles = 1;   // tiles | B (packets per tile) << 32
 constexpr uint32_t kEdStep = 2;    // the step's index in the run
 constexpr uint32_t kEdNq = 3;      // batches in the step (1..kEngineQueues)
 constexpr uint32_t kEdTile0 = 4;   // tile0[0..nq]: the batches' first tiles within the step
-constexpr uint32_t kEdQueue = 9;   // + 8 q: bytes, bytes_len, off, len, seed, out, status, n
+constexpr uint32_t kEdQueue = 9;   // + 8 q: bytes, bytes_len, off, len, seed, out, status, n (q < 4: words 9-40)
+constexpr uint32_t kEdKind = 41;   // kind | flat-body fill flags << 8 | public fill mode << 16
+constexpr uint32_t kEdDep = 42;    // 0, or 1 + the step whose completion this step's tiles wait for
+// step kinds
+constexpr uint32_t kStepSum = 0;        // checksums into out / status (sccsum_engine_submit)
+constexpr uint32_t kStepFillGen = 1;    // fill, generate half: values into out2, status; frames untouched
+constexpr uint32_t kStepFillStore = 2;  // fill, store half: out2's values into the frames' fields
+constexpr uint32_t kStoreTilePackets = 256;  // store tiles: 4 frames per lane
+// Store tiles write each field through (sc0 sc1).  Stored plain (the L2
+// merging a frame's two fields) with one system-scope release per wave at the
+// step's flush instead, a fill step took 408 us against 328 (the releases'
+// L2 write-backs, 2 048 per step, stall every wave; profiles/r05_engine_fill.log).
+#if defined(SCCSUM_AB_FILLSTORE_PLAIN) || defined(SCCSUM_AB_FILLSTORE_NORELEASE)
+constexpr bool kStoreWT = false;  // A/B only (NORELEASE: not even the release; results unsafe until the run ends)
+#else
+constexpr bool kStoreWT = true;
+#endif
 // ctl words (pinned): each on its own 64-byte line
 constexpr uint32_t kEcPublished = 0, kEcStop = 8, kEcError = 16, kEcDone = 24;  // done[s] at 24 + 8 s
-// mirror words (device): published tiles, steps copied, stop seen, poll token
-constexpr uint32_t kMpTiles = 0, kMpSteps = 8, kMpStop = 16, kMpToken = 24, kMirrorWords = 32;
+// kEcError values: the grid gave up waiting for a step (idle), or on a dependency (a fault: never expected)
+constexpr uint64_t kErrIdle = 1, kErrDepWait = 2;
+// mirror words (device): published tiles, steps copied, stop seen, poll token, time of the last new step
+constexpr uint32_t kMpTiles = 0, kMpSteps = 8, kMpStop = 16, kMpToken = 24, kMpStamp = 32, kMirrorWords = 40;
 
 struct EngineArgs {
     const uint64_t* hring;  // descriptors as the host writes them, kEngineSlotWords words per step (pinned)
@@ -1038,7 +1071,9 @@ struct EngineArgs {
     uint32_t* claims;       // kGroups claim counters, kHeadStride apart (device)
     uint32_t* counts;       // kEngineCountSlots x kGroups completion counters, kHeadStride apart (device)
     uint32_t* gdone;        // kEngineCountSlots groups-done counters, kHeadStride apart (device)
-    uint64_t idle_ticks;    // 100 MHz ticks a wave waits for a step before it gives up
+    uint64_t* sdone;        // kEngineCountSlots words, 8 apart: 1 + the latest step done in each count slot (device)
+    uint64_t idle_ticks;    // 100 MHz ticks the grid may go without a new step before a waiting wave gives up
+    uint64_t dep_ticks;     // safety limit of a wait on a dependency (never reached by a correct run)
 };
 
 __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
@@ -1060,11 +1095,13 @@ struct EngineSrc {
     uint64_t pub = 0;                                  // published tiles, as the mirror last said
     uint64_t step = ~0ull, sfirst = 0, slast = 0;      // the cursor: step `step` holds tiles [sfirst, slast)
     uint64_t dw = 0;                                   // lane i: word i of the cursor's descriptor
+    uint64_t skind = 0, sdep = 0;                      // the cursor step's kind word and dependency
+    uint64_t dep_seen = 0;                             // the latest dependency (1 + step) found done
 #ifdef SCCSUM_AB_TIMELINE
     unsigned long long ab[8] = {};
 #endif
     struct Ref {
-        uint32_t cnt, B;
+        uint32_t cnt, B, kind;
         uint64_t base, step, first, last;
         const uint8_t* bytes;
         uint64_t bytes_len;
@@ -1123,6 +1160,7 @@ struct EngineSrc {
         const uint64_t stop = ctl_load(kEcStop);  // before the steps: the host raises it after its last step
         const uint64_t hs = ctl_load(kEcPublished);
         uint64_t ms = mload(kMpSteps);
+        const uint64_t ms0 = ms;
         uint64_t tiles = mload(kMpTiles);
         for (; ms < hs; ++ms) {
             const uint64_t w = __hip_atomic_load(E.hring + ms * kEngineSlotWords + lane, __ATOMIC_RELAXED,
@@ -1134,6 +1172,14 @@ struct EngineSrc {
         if (lane == 0) {
             __hip_atomic_store(E.mirror + kMpTiles, tiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(E.mirror + kMpSteps, hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the grid's progress clock: waiting waves give up only when no new
+            // step arrived for idle_ticks (timing each wave's own
+            // wait let a wave holding a claim far ahead leave under steady light
+            // traffic, stranding its tile)
+            if (ms0 < hs) {
+                __hip_atomic_store(E.mirror + kMpStamp, static_cast<uint64_t>(wall_clock64()), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) {
@@ -1141,7 +1187,7 @@ struct EngineSrc {
             __hip_atomic_store(E.mirror + kMpToken, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    __device__ bool ready(uint64_t v) {
+    __device__ bool published(uint64_t v) {
         if (v < pub) return true;
 #ifdef SCCSUM_AB_TIMELINE
         ++ab[2];
@@ -1152,6 +1198,20 @@ struct EngineSrc {
         pub = mload(kMpTiles);
         return v < pub;
     }
+    // tile v (published) may start: its step has no dependency, or the step it
+    // depends on is done (device copy of the done words; each slot only rises)
+    __device__ bool dep_ready(uint64_t v) {
+        walk(v);
+        if (sdep == 0 || sdep <= dep_seen) return true;
+        const uint32_t slot = static_cast<uint32_t>((sdep - 1) % kEngineCountSlots);
+        uint64_t d = 0;
+        if (lane == 0) d = __hip_atomic_load(E.sdone + 8u * slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        d = rfl64(d);
+        if (d < sdep) return false;
+        dep_seen = sdep;
+        return true;
+    }
+    __device__ bool ready(uint64_t v) { return published(v) && dep_ready(v); }
     __device__ bool wait_ready(uint64_t v) {
         if (ready(v)) return true;
         flush();  // never wait holding counts: a step's completion may hang on them
@@ -1165,14 +1225,33 @@ struct EngineSrc {
         } slept{ab, t0};
 #endif
         for (;;) {
-            __builtin_amdgcn_s_sleep(127);  // ~3.4 us
             const uint64_t stop = mload(kMpStop);  // read before the tiles (the poller raises it after them)
-            if (ready(v)) return true;
+            const bool pubd = published(v);
+            if (pubd) {
+                // v's step waits on an older step: that always completes (its
+                // tiles come before v in every group's claim order); the limit
+                // only keeps a fault from hanging the device
+                if (dep_ready(v)) return true;
+                if (static_cast<uint64_t>(wall_clock64()) - t0 > E.dep_ticks) {
+                    if (lane == 0) __hip_atomic_store(E.ctl + kEcError, kErrDepWait, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM);
+                    return false;
+                }
+                __builtin_amdgcn_s_sleep(32);  // ~0.9 us: a dependency ends with a step's last tiles
+                continue;
+            }
             if (stop) return false;  // stopped, and v lies past every published step
-            if (static_cast<uint64_t>(wall_clock64()) - t0 > E.idle_ticks) {
-                if (lane == 0) __hip_atomic_store(E.ctl + kEcError, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // idle: no new step for idle_ticks, counted from this wait's start or
+            // the poller's last new step, whichever is later
+            const uint64_t now = static_cast<uint64_t>(wall_clock64());
+            const uint64_t stamp = mload(kMpStamp);
+            const uint64_t since = stamp > t0 ? stamp : t0;
+            if (now > since && now - since > E.idle_ticks) {
+                if (lane == 0) __hip_atomic_store(E.ctl + kEcError, kErrIdle, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM);
                 return false;
             }
+            __builtin_amdgcn_s_sleep(127);  // ~3.4 us
         }
     }
     __device__ uint64_t first() {
@@ -1181,7 +1260,7 @@ struct EngineSrc {
     }
     // tile v (published) -> its step, batch and packets.  Steps are walked in
     // order: a run never reuses a descriptor, so a step passed over stays valid.
-    __device__ Ref ref(uint64_t v) {
+    __device__ void walk(uint64_t v) {
 #ifdef SCCSUM_AB_TIMELINE
         const uint64_t w0 = (step == ~0ull || v >= slast) ? static_cast<uint64_t>(wall_clock64()) : 0;
 #endif
@@ -1194,11 +1273,17 @@ struct EngineSrc {
                                    __HIP_MEMORY_SCOPE_AGENT);
             sfirst = rl64(dw, kEdFirst);
             slast = sfirst + static_cast<uint32_t>(rl64(dw, kEdTiles));
+            skind = rl64(dw, kEdKind);
+            sdep = rl64(dw, kEdDep);
         }
 #ifdef SCCSUM_AB_TIMELINE
         if (w0) ab[4] += static_cast<uint64_t>(wall_clock64()) - w0;
 #endif
+    }
+    __device__ Ref ref(uint64_t v) {
+        walk(v);
         Ref r;
+        r.kind = static_cast<uint32_t>(skind);
         const uint64_t t_in = v - sfirst;
         const uint32_t nq = static_cast<uint32_t>(rl64(dw, kEdNq));
         uint32_t q = 0;
@@ -1228,6 +1313,9 @@ struct EngineSrc {
     __device__ uint16_t* out(const Ref& r) const { return r.out; }
     __device__ uint8_t* status(const Ref& r) const { return r.status; }
     __device__ uint32_t tile_packets(const Ref& r) const { return r.B; }
+    __device__ bool is_store(const Ref& r) const { return (r.kind & 0xffu) == kStepFillStore; }
+    __device__ uint32_t fill_flags(const Ref& r, uint32_t) const { return (r.kind >> 8) & 0xffu; }
+    __device__ uint32_t store_mode(const Ref& r) const { return r.kind >> 16; }
     // A tile's results are stored: count it for its step, per group (so no
     // counter sees more than its group's share).  A wave's tiles of one step
     // come in a row (claims rise), so it counts them itself and adds the count
@@ -1236,7 +1324,7 @@ struct EngineSrc {
     // cost 18 % of cfg 2's step: profiles/r04g).  The step's last count resets
     // the counters and reports the step done.
     uint64_t pend_step = ~0ull, pend_first = 0, pend_last = 0;
-    uint32_t pend = 0;
+    uint32_t pend = 0, pend_kind = 0;
 #ifdef SCCSUM_AB_TIMELINE
     unsigned long long pend_t0 = 0, pend_t1 = 0;
 #endif
@@ -1260,7 +1348,15 @@ struct EngineSrc {
         }
 #endif
         if (lane != 0) return;
-        if (wt) {
+#ifdef SCCSUM_AB_FILLSTORE_NORELEASE
+        if (false) {
+#else
+        if ((pend_kind & 0xffu) == kStepFillStore && !kStoreWT) {
+#endif
+            // the fields were stored plain: write them back from this XCD's L2
+            // before the step can report (the host copies the frames out then)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        } else if (wt) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the counted tiles' write-through result stores are done
         } else {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // their stores leave this XCD's L2 first
@@ -1279,6 +1375,8 @@ struct EngineSrc {
         const uint32_t y = __hip_atomic_fetch_add(gd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (y + 1 != groups) return;
         __hip_atomic_store(gd, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the device's copy first (steps that depend on this one read it), then the host's
+        __hip_atomic_store(E.sdone + 8u * slot, pend_step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(E.ctl + kEcDone + 8u * pend_step, pend_step + 1, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1295,6 +1393,7 @@ struct EngineSrc {
             pend_step = r.step;
             pend_first = r.first;
             pend_last = r.last;
+            pend_kind = r.kind;
 #ifdef SCCSUM_AB_TIMELINE
             pend_t0 = static_cast<uint64_t>(wall_clock64());
 #endif
@@ -1306,10 +1405,105 @@ struct EngineSrc {
     }
 };
 
+// In-place fill, store half, for one frame of length L >= 20 at p: the values
+// the generate half made (FILL phase C, *wp = IP | L4 << 16) go into the
+// frame's fields.  Which fields is decided from the frame's own (unmodified)
+// header exactly as the generate half decided it.  Field bytes of different
+// frames never overlap, so the 2-byte stores need no coordination.
+// kCoherent (the engine's store tiles, which share a running grid with the
+// generate tiles that wrote *wp on other XCDs): the value and the header are
+// read at agent scope, past this XCD's L2, and the fields are written through
+// (sc0 sc1), so the host may copy the frames out once the step reports.
+template <bool kCoherent>
+__device__ __forceinline__ uint32_t fill_ld32(const uint32_t* q) {
+    if constexpr (kCoherent) {
+        return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        return *gld(q);
+    }
+}
+template <bool kWriteThrough>
+__device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {
+    if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0u) {
+        if constexpr (kWriteThrough) {
+            __hip_atomic_store(reinterpret_cast<uint16_t*>(p), static_cast<uint16_t>(v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            *gst(reinterpret_cast<uint16_t*>(p)) = static_cast<uint16_t>(v);
+        }
+    } else if constexpr (kWriteThrough) {
+        __hip_atomic_store(p, static_cast<uint8_t>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(p + 1, static_cast<uint8_t>(v >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        gst(p)[0] = static_cast<uint8_t>(v);
+        gst(p)[1] = static_cast<uint8_t>(v >> 8);
+    }
+}
+// What the store half reads of one frame: its value word and header bytes
+// 0..9 from the four dwords at the dword-aligned address at or below p (one
+// 16-byte request instead of four byte loads).  (Issuing the offset, length
+// and words loads together, two round trips instead of the three the compiler
+// makes of this, ran the fill 0.8 % slower: r04zz.)  Loads and stores are two
+// calls so a caller with several frames per lane issues every load first.
+struct FillHead {
+    uint32_t w, d0, d1, d2, d3;
+};
+template <bool kCoherent>
+__device__ __forceinline__ FillHead fill_load(const uint8_t* p, const uint32_t* wp) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    FillHead h;
+    h.w = fill_ld32<kCoherent>(wp);
+    h.d0 = fill_ld32<kCoherent>(d);
+    h.d1 = fill_ld32<kCoherent>(d + 1);
+    h.d2 = fill_ld32<kCoherent>(d + 2);
+    h.d3 = fill_ld32<kCoherent>(d + 3);
+    return h;
+}
+// kCoherent: the ICMP type byte is read at agent scope; kWriteThrough: the
+// fields are stored sc0 sc1 (else plain: the L2 merges a frame's two fields
+// into one line write, and the engine releases a store step's fields once per
+// wave, in flush)
+template <bool kCoherent, bool kWriteThrough = false>
+__device__ __forceinline__ void fill_apply(uint8_t* p, uint32_t L, const FillHead& h, uint32_t mode) {
+    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p) & 3u);
+    const uint32_t w = h.w, d0 = h.d0, d1 = h.d1, d2 = h.d2, d3 = h.d3;
+    auto hbyte = [&](uint32_t k) {
+        const uint32_t b = sh + k;
+        const uint32_t dw = b < 4u ? d0 : (b < 8u ? d1 : (b < 12u ? d2 : d3));
+        return (dw >> (8u * (b & 3u))) & 0xffu;
+    };
+    const uint32_t ihl = hbyte(0) & 0xfu;
+    const uint32_t ip_len = (hbyte(2) << 8) | hbyte(3);
+    const uint32_t fragw = (hbyte(6) << 8) | hbyte(7);
+    const uint32_t proto = hbyte(9);
+    const uint32_t l4_off = 4u * ihl;
+    const uint32_t l4_end = ip_len < L ? ip_len : L;
+    // as frame_decode: malformed, or an IP fragment -> no L4 write
+    const bool atomic = !(L < ip_len || l4_off > l4_end || (fragw & 0x1fffu) * 8u + l4_end > 65535u ||
+                          (fragw & 0x3fffu) != 0u);
+    const uint32_t l4_len = l4_off > l4_end ? 0u : l4_end - l4_off;
+    if (mode & SCCSUM_FILL_IP) store_field<kWriteThrough>(p + 10, w);
+    if (!atomic) return;
+    if (mode & SCCSUM_FILL_L4) {
+        const uint32_t fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
+        if (fo != 0u && l4_len >= fo + 2u) store_field<kWriteThrough>(p + l4_off + fo, w >> 16);
+    }
+    if ((mode & SCCSUM_FILL_ICMP_ECHO) && proto == 1u && l4_len >= 8u) {
+        uint8_t* ih = p + l4_off;
+        const uintptr_t ia = reinterpret_cast<uintptr_t>(ih);
+        const uint32_t type = (fill_ld32<kCoherent>(reinterpret_cast<const uint32_t*>(ia & ~uintptr_t(3))) >>
+                               (8u * static_cast<uint32_t>(ia & 3u))) & 0xffu;
+        if (type == 8u) {  // echo_request -> echo_reply, code 0, checksum (ip.cc:469-474)
+            store_field<kWriteThrough>(ih, 0u);
+            store_field<kWriteThrough>(ih + 2, w >> 16);
+        }
+    }
+}
+
 template <int U, bool IPV4, bool FILL, bool PIPE, bool PLATE, class Src>
 __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const RssParams& rss) {
     static_assert(!FILL || IPV4, "in-place generate is a frames mode");
-    static_assert(!FILL || !Src::kEngine, "the engine does not fill in place");
     constexpr uint32_t C = kWave * U;  // units per chunk
     constexpr uint32_t kLdsUnits = C;
     constexpr int kHead = FILL ? 4 : (IPV4 ? 3 : 1);
@@ -1320,9 +1514,6 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
     const uint32_t ra_code = (flags >> kRunAlignShift) & 3u;
     const uint64_t ra_mask = ra_code == 0 ? 0ull : (ra_code == 1 ? 3ull : 7ull);
     const bool raw = !IPV4 && (flags & kFlagRaw);
-    const bool fill_ip = FILL && (flags & kFlagFillIp);
-    const bool fill_l4 = FILL && (flags & kFlagFillL4);
-    const bool fill_icmp = FILL && (flags & kFlagFillIcmp);
     __shared__ u32x4 ubuf_all[kWavesPerBlock][kLdsUnits];
     __shared__ uint32_t pbuf_all[kWavesPerBlock][kLdsUnits];
     const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -1501,6 +1692,55 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
         const uint64_t a0 = cur.a0;
         const bool range_bad = cur.range_bad, short_frame = cur.short_frame, huge = cur.huge, fast = cur.fast;
 
+        // the tile's fill flags: a launch's are the kernel's; an engine's come
+        // with its step (a FILL engine runs verify and generate steps too)
+        const uint32_t ff = FILL ? src.fill_flags(cur.ref, flags) : 0u;
+        const bool fill_tile = FILL && (ff & kFillFlags) != 0u;
+        const bool fill_ip = fill_tile && (ff & kFlagFillIp);
+        const bool fill_l4 = fill_tile && (ff & kFlagFillL4);
+        const bool fill_icmp = fill_tile && (ff & kFlagFillIcmp);
+        // an engine fill's store tile: one frame per lane, nothing streamed
+        const bool store_tile = Src::kEngine && FILL && src.is_store(cur.ref);
+#ifdef SCCSUM_AB_NOFILLSTORE
+        if (store_tile) {  // A/B only (tools/build_ab.sh): a store tile does nothing (the step's barrier alone)
+            issue();
+        } else
+#endif
+        if (store_tile) {
+            issue();  // the claim of the tile after next
+            // frames base + lane + 64 j, j < J: every load of the tile issues
+            // before its first store (one frame per lane left the store phase
+            // with a quarter of the frames in flight that the launch's store
+            // pass keeps, 8 waves per SIMD against the engine's 2)
+            constexpr int J = static_cast<int>(kStoreTilePackets) / kWave;
+            uint8_t* const sb = const_cast<uint8_t*>(src.bytes(cur.ref));
+            const uint64_t slen = src.bytes_len(cur.ref);
+            const uint64_t* const soffs = src.off(cur.ref);
+            const uint32_t* const slens = src.len(cur.ref);
+            const uint32_t* const swords = reinterpret_cast<const uint32_t*>(src.out(cur.ref));
+            uint64_t so[J];
+            uint32_t sl[J];
+            bool sv[J];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const uint32_t k = lane + static_cast<uint32_t>(kWave * j);
+                sv[j] = k < cur.cnt;
+                const uint64_t q = base + (sv[j] ? k : 0u);
+                so[j] = gld(soffs)[q];
+                sl[j] = sv[j] ? gld(slens)[q] : 0u;
+            }
+            FillHead fh[J];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                sv[j] = sv[j] && so[j] <= slen && sl[j] <= slen - so[j] && sl[j] >= 20u;
+                if (sv[j]) fh[j] = fill_load<true>(sb + so[j], swords + base + lane + kWave * j);
+            }
+            const uint32_t smode = src.store_mode(cur.ref);
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                if (sv[j]) fill_apply<true, kStoreWT>(sb + so[j], sl[j], fh[j], smode);
+            }
+        } else {
         // ---- B: stream each run's extent
         u32x4 hs[4] = {u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}};
         u32x4 hl = u32x4{0, 0, 0, 0};
@@ -1635,7 +1875,7 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
             const uint32_t h2 = header_dword(hs, head, 2), h3 = header_dword(hs, head, 3);
             const uint32_t h4 = header_dword(hs, head, 4);
             const FrameDecode D = frame_decode(h0, h1, h2, h3, h4, L);
-            ipc = ~fold16(static_cast<uint64_t>(h0) + h1 + (FILL ? h2 & 0xffffu : h2) + h3 + h4) & 0xffffu;
+            ipc = ~fold16(static_cast<uint64_t>(h0) + h1 + (fill_tile ? h2 & 0xffffu : h2) + h3 + h4) & 0xffffu;
             const uint32_t ihl = D.ihl, l4_off = D.l4_off, l4_len = D.l4_len;
             st = D.st;
             pseudo = D.pseudo;
@@ -1654,7 +1894,7 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
                 rss_ipv4(rss, h0, h1, h2, h3, h4, h5, pl, L, hv);
                 if (mine) rss.hash[base + lane] = (range_bad || short_frame) ? 0u : hv;  // one queue with RSS
             }
-            if (FILL) {
+            if (fill_tile) {
                 // L4 writers never touch an IP fragment or a malformed frame
                 const bool atomic = (st & (SCCSUM_ST_MALFORMED | SCCSUM_ST_IPFRAG)) == 0u;
                 uint32_t fo = 0;
@@ -1722,7 +1962,7 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
             uint32_t SJ = exact_range_sum(ja0, rs, re, lane);
             if (jhead & 1u) SJ = swap16(SJ);
             if (lane == j) {
-                if (IPV4 && FILL) {
+                if (IPV4 && fill_tile) {
                     uint32_t rr = ~SJ & 0xffffu;  // ICMP echo: the message after type, code, checksum
                     if (!icmp_lane) {
                         const uint8_t* fp = reinterpret_cast<const uint8_t*>(a0) + fpos;
@@ -1773,6 +2013,7 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
         // (readfirstlane: the compiler otherwise loses the tile number's
         // uniformity across the issue branches and reads the next tile's queue
         // fields with vector loads, 8 more per tile)
+        }  // (not a store tile)
         if (kLate && claiming) t2 = rfl64(src.claim_resolve(c2));
         src.retire(cur.ref);
         if (Src::kEngine && t1 < ntiles && !planned) {
@@ -1805,11 +2046,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 
     flat_body<U, IPV4, FILL, PIPE, PLATE>(src, flags, rss);
 }
 
-template <int U, bool IPV4>
+// FILL: an engine that also takes fill steps (sccsum_engine_submit_fill)
+template <int U, bool IPV4, bool FILL = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U >= 16 ? 2 : 3))) void csum_engine_kernel(
     const EngineArgs E, uint32_t flags) {
     EngineSrc src(E, flags);
-    flat_body<U, IPV4, false, false, false>(src, flags, RssParams{});
+    flat_body<U, IPV4, FILL, false, false>(src, flags, RssParams{});
 }
 
 // Fragment lists (checksummer::sum(const packet&), src/net/ip_checksum.cc:64-68):
@@ -1857,15 +2099,6 @@ __global__ __launch_bounds__(kBlock) void frag_combine_kernel(const uint32_t* __
 // ~70-90 us (HBM read/write turnarounds; tools/dev/store_probe.hip,
 // DESIGN.md §5.6).  Field bytes of different frames never overlap, so the
 // 2-byte stores need no coordination.
-__device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {
-    if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0u) {
-        *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(v);
-    } else {
-        p[0] = static_cast<uint8_t>(v);
-        p[1] = static_cast<uint8_t>(v >> 8);
-    }
-}
-
 __global__ __launch_bounds__(kBlock) void fill_store_kernel(uint8_t* __restrict__ bytes, uint64_t bytes_len,
                                                             const uint64_t* __restrict__ off,
                                                             const uint32_t* __restrict__ len,
@@ -1876,44 +2109,7 @@ __global__ __launch_bounds__(kBlock) void fill_store_kernel(uint8_t* __restrict_
     const uint64_t o = off[i];
     const uint32_t L = len[i];
     if (o > bytes_len || L > bytes_len - o || L < 20u) return;
-    uint8_t* p = bytes + o;
-    const uint32_t w = words[i];
-    // header bytes 0..9 from the four dwords at the dword-aligned address at or
-    // below p (one 16-byte request instead of four byte loads).  (Issuing the
-    // offset, length and words loads together, two round trips instead of the
-    // three the compiler makes of this, ran the fill 0.8 % slower: r04zz.)
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t sh = static_cast<uint32_t>(a & 3u);
-    const uint32_t* d = reinterpret_cast<const uint32_t*>(a - sh);
-    const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
-    auto hbyte = [&](uint32_t k) {
-        const uint32_t b = sh + k;
-        const uint32_t dw = b < 4u ? d0 : (b < 8u ? d1 : (b < 12u ? d2 : d3));
-        return (dw >> (8u * (b & 3u))) & 0xffu;
-    };
-    const uint32_t ihl = hbyte(0) & 0xfu;
-    const uint32_t ip_len = (hbyte(2) << 8) | hbyte(3);
-    const uint32_t fragw = (hbyte(6) << 8) | hbyte(7);
-    const uint32_t proto = hbyte(9);
-    const uint32_t l4_off = 4u * ihl;
-    const uint32_t l4_end = ip_len < L ? ip_len : L;
-    // as frame_decode: malformed, or an IP fragment -> no L4 write
-    const bool atomic = !(L < ip_len || l4_off > l4_end || (fragw & 0x1fffu) * 8u + l4_end > 65535u ||
-                          (fragw & 0x3fffu) != 0u);
-    const uint32_t l4_len = l4_off > l4_end ? 0u : l4_end - l4_off;
-    if (mode & SCCSUM_FILL_IP) store_field(p + 10, w);
-    if (!atomic) return;
-    if (mode & SCCSUM_FILL_L4) {
-        const uint32_t fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
-        if (fo != 0u && l4_len >= fo + 2u) store_field(p + l4_off + fo, w >> 16);
-    }
-    if ((mode & SCCSUM_FILL_ICMP_ECHO) && proto == 1u && l4_len >= 8u) {
-        uint8_t* ih = p + l4_off;
-        if (ih[0] == 8u) {  // echo_request -> echo_reply, code 0, checksum (ip.cc:469-474)
-            store_field(ih, 0u);
-            store_field(ih + 2, w >> 16);
-        }
-    }
+    fill_apply<false>(bytes + o, L, fill_load<false>(bytes + o, words + i), mode);
 }
 
 // Header-only generate (no payload bytes read): the IPv4 header checksum
@@ -2092,6 +2288,7 @@ struct Knobs {
     int short_chunks = 1;            // flat kernel (no chunk in flight): a run's last chunk covers only its rows
     int run_align = kRunAlign;       // flat kernel: run extents start on 1 / 4 / 8-unit (16 / 64 / 128 B) boundaries
     int engine_wt = 1;               // engine: results written through (1) or stored as a launch stores them (0)
+    int engine_idle_ms = 1000;       // engine: a run given no new step for this long gives up (SCCSUM_EIDLE)
 };
 thread_local Knobs t_knobs;
 
@@ -2742,9 +2939,9 @@ int launch_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const
 
 // Engine launch: the grid is what the chip holds at once (every wave's tiles
 // come from the claim counters, so no block waits for another to finish).
-template <bool IPV4>
+template <bool IPV4, bool FILL = false>
 hipError_t launch_engine(hipStream_t s, int dev, const EngineArgs& E, uint32_t flags, uint64_t* waves) {
-    auto kern = csum_engine_kernel<16, IPV4>;
+    auto kern = csum_engine_kernel<16, IPV4, FILL>;
     const int occ = kernel_occupancy(reinterpret_cast<const void*>(kern));
     const uint64_t bpc = static_cast<uint64_t>(occ < t_knobs.blocks_per_cu ? occ : t_knobs.blocks_per_cu);
     uint64_t blocks = static_cast<uint64_t>(cu_count(dev)) * bpc;
@@ -2760,7 +2957,7 @@ hipError_t launch_engine(hipStream_t s, int dev, const EngineArgs& E, uint32_t f
 // ---- resident engine, host side (sccsum.h "Resident engine")
 struct sccsum_engine {
     int device = 0;
-    bool frames = true;
+    bool frames = true, fill = false;
     uint32_t max_steps = 0, max_in_flight = 0;
     uint64_t* ring_h = nullptr;  // pinned descriptors (host view)
     uint64_t* ctl_h = nullptr;   // pinned control words (host view)
@@ -2773,6 +2970,33 @@ struct sccsum_engine {
 };
 
 namespace {
+
+// One running engine per device in this process.  A grid holds every CU of
+// its device and all of their LDS while it runs, so a second grid there could
+// only queue behind it (and a step submitted to it would wait on the first
+// run's stop): sccsum_engine_start refuses it with SCCSUM_EBUSY.  (Seastar
+// runs one process with a reactor thread per core, src/core/reactor.cc:4163,
+// so shards sharing a GPU meet here.)
+std::mutex g_live_mu;
+sccsum_engine* g_live[sccsum::kMaxDevices] = {};
+
+void release_live(sccsum_engine* e) {
+    std::lock_guard<std::mutex> g(g_live_mu);
+    if (g_live[e->device] == e) g_live[e->device] = nullptr;
+}
+
+// The calling thread's current device, put back on scope exit (create must
+// not leave a shard thread bound to another device: its later launches on its
+// own streams would then be refused).
+struct CurrentDevice {
+    int dev = -1;
+    CurrentDevice() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~CurrentDevice() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
 
 uint64_t now_ns() {
     return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -2791,140 +3015,56 @@ int engine_wait_done(sccsum_engine* e, uint64_t s, uint64_t timeout_ns) {
     }
 }
 
-}  // namespace
-
-extern "C" {
-
-int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, sccsum_engine** out) {
-    if (!out || (mode != SCCSUM_PIPE_IPV4 && mode != SCCSUM_PIPE_SPANS) || max_steps == 0 ||
-        max_steps > sccsum::kEngineMaxSteps ||
-        max_in_flight == 0 || max_in_flight > sccsum::kEngineCountSlots) {
-        return SCCSUM_EINVAL;
-    }
-    *out = nullptr;
-    int n = 0;
-    hipError_t e0 = hipGetDeviceCount(&n);
-    if (e0 != hipSuccess) return static_cast<int>(e0);
-    if (device < 0 || device >= n) return SCCSUM_ENODEV;
-    if ((e0 = hipSetDevice(device)) != hipSuccess) return static_cast<int>(e0);
-    auto* e = new (std::nothrow) sccsum_engine;
-    if (!e) return static_cast<int>(hipErrorOutOfMemory);
-    e->device = device;
-    e->frames = mode == SCCSUM_PIPE_IPV4;
-    e->max_steps = max_steps;
-    e->max_in_flight = max_in_flight;
-    const uint64_t ring_bytes = uint64_t(max_steps) * sccsum::kEngineSlotWords * 8u;
-    const uint64_t ctl_bytes = (sccsum::kEcDone + 8u * uint64_t(max_steps)) * 8u;
-    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
-    void *rh = nullptr, *ch = nullptr, *rd = nullptr, *cd = nullptr, *cl = nullptr, *co = nullptr, *gd = nullptr,
-         *dr = nullptr, *mi = nullptr;
-    hipError_t r = hipHostMalloc(&rh, ring_bytes, fl);
-    if (r == hipSuccess) r = hipHostMalloc(&ch, ctl_bytes, fl);
-    if (r == hipSuccess) r = hipHostGetDevicePointer(&rd, rh, 0);
-    if (r == hipSuccess) r = hipHostGetDevicePointer(&cd, ch, 0);
-    const size_t claims_b = size_t(sccsum::kGroups) * sccsum::kHeadStride * 4u;
-    const size_t counts_b = size_t(sccsum::kEngineCountSlots) * sccsum::kGroups * sccsum::kHeadStride * 4u;
-    const size_t gdone_b = size_t(sccsum::kEngineCountSlots) * sccsum::kHeadStride * 4u;
-    if (r == hipSuccess) r = hipMalloc(&cl, claims_b);
-    if (r == hipSuccess) r = hipMalloc(&co, counts_b);
-    if (r == hipSuccess) r = hipMalloc(&gd, gdone_b);
-    if (r == hipSuccess) r = hipMalloc(&dr, ring_bytes);
-    if (r == hipSuccess) r = hipMalloc(&mi, sccsum::kMirrorWords * 8u);
-    if (r == hipSuccess) r = hipEventCreateWithFlags(&e->left, hipEventDisableTiming);
-    if (r != hipSuccess) {
-        for (void* p : {rh, ch}) if (p) (void)hipHostFree(p);
-        for (void* p : {cl, co, gd, dr, mi}) if (p) (void)hipFree(p);
-        delete e;
-        return static_cast<int>(r);
-    }
-    std::memset(rh, 0, ring_bytes);
-    std::memset(ch, 0, ctl_bytes);
-    e->ring_h = static_cast<uint64_t*>(rh);
-    e->ctl_h = static_cast<uint64_t*>(ch);
-    e->args.hring = static_cast<const uint64_t*>(rd);
-    e->args.dring = static_cast<uint64_t*>(dr);
-    e->args.mirror = static_cast<uint64_t*>(mi);
-    e->args.ctl = static_cast<uint64_t*>(cd);
-    e->args.claims = static_cast<uint32_t*>(cl);
-    e->args.counts = static_cast<uint32_t*>(co);
-    e->args.gdone = static_cast<uint32_t*>(gd);
-    e->args.idle_ticks = 100000000ull;  // 1 s at the constant 100 MHz clock
-    *out = e;
-    return SCCSUM_OK;
-}
-
-int sccsum_engine_start(sccsum_engine* e, void* stream) {
-    if (!e || e->running) return SCCSUM_EINVAL;
-    const hipStream_t s = static_cast<hipStream_t>(stream);
-    int dev = 0;
-    if (const int rc = sccsum::launch_device(s, &dev); rc != SCCSUM_OK) return rc;
-    if (dev != e->device) return SCCSUM_EINVAL;
-    // the last run's grid has left (stop only asks it to): its control words are ours again
-    if (e->launched) {
-        const hipError_t w = e->left_recorded ? hipEventSynchronize(e->left) : hipStreamSynchronize(e->stream);
-        if (w != hipSuccess) return static_cast<int>(w);
-    }
-    // a new run: no step published, none done, counters zero (stream-ordered before the grid)
-    std::memset(e->ctl_h, 0, (sccsum::kEcDone + 8u * uint64_t(e->max_steps)) * 8u);
-    std::atomic_thread_fence(std::memory_order_seq_cst);
-    const size_t claims_b = size_t(sccsum::kGroups) * sccsum::kHeadStride * 4u;
-    const size_t counts_b = size_t(sccsum::kEngineCountSlots) * sccsum::kGroups * sccsum::kHeadStride * 4u;
-    const size_t gdone_b = size_t(sccsum::kEngineCountSlots) * sccsum::kHeadStride * 4u;
-    hipError_t r = hipMemsetAsync(e->args.claims, 0, claims_b, s);
-    if (r == hipSuccess) r = hipMemsetAsync(e->args.counts, 0, counts_b, s);
-    if (r == hipSuccess) r = hipMemsetAsync(e->args.gdone, 0, gdone_b, s);
-    if (r == hipSuccess) r = hipMemsetAsync(e->args.mirror, 0, sccsum::kMirrorWords * 8u, s);
-    if (r != hipSuccess) return static_cast<int>(r);
-    const sccsum::Knobs& K = sccsum::t_knobs;
-    uint32_t flags = static_cast<uint32_t>(K.out_policy) << sccsum::kOutPolicyShift;
-    if (K.engine_wt) flags |= sccsum::kFlagEngineWT;
-    if (!K.short_chunks) flags |= sccsum::kFlagFullChunks;
-    flags |= static_cast<uint32_t>(K.run_align == 8 ? 2 : (K.run_align == 4 ? 1 : 0)) << sccsum::kRunAlignShift;
-    r = e->frames ? sccsum::launch_engine<true>(s, dev, e->args, flags, &e->waves)
-                  : sccsum::launch_engine<false>(s, dev, e->args, flags, &e->waves);
-    if (r != hipSuccess) return static_cast<int>(r);
-    e->left_recorded = hipEventRecord(e->left, s) == hipSuccess;  // else the next start syncs the stream
-    e->launched = true;
-    e->stream = s;
-    e->running = true;
-    e->next_step = 0;
-    e->next_first = 0;
-    return SCCSUM_OK;
-}
-
-int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
-                         uint64_t timeout_ns, uint64_t* step) {
-    if (!e || !e->running || !step || nbatch == 0 || nbatch > SCCSUM_ENGINE_MAX_BATCHES || !batches) {
-        return SCCSUM_EINVAL;
-    }
-    uint64_t n_total = 0, bytes_total = 0;
+// The batches of one step, checked as the launches check them.
+int engine_check(const sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, bool fill) {
+    if (nbatch == 0 || nbatch > SCCSUM_ENGINE_MAX_BATCHES || !batches) return SCCSUM_EINVAL;
     for (uint32_t i = 0; i < nbatch; ++i) {
         const sccsum_batch& x = batches[i];
+        if (e->frames && x.d_seed) return SCCSUM_EINVAL;  // frames derive their pseudo-header in-kernel
+        if (!x.n) continue;
         const bool ok = e->frames
                             ? sccsum::batch_ok<true>(x.d_bytes, x.d_off, x.d_len, nullptr, x.d_out, x.d_status, 0)
                             : sccsum::batch_ok<false>(x.d_bytes, x.d_off, x.d_len, x.d_seed, x.d_out, x.d_status, 0);
-        if (x.n && !ok) return SCCSUM_EINVAL;
-        if (e->frames && x.d_seed) return SCCSUM_EINVAL;  // frames derive their pseudo-header in-kernel
-        n_total += x.n;
-        bytes_total += x.n ? x.bytes_len : 0;
+        if (!ok) return SCCSUM_EINVAL;
+        if (fill && !x.d_out) return SCCSUM_EINVAL;  // a fill's values pass from its generate to its store step
     }
+    return SCCSUM_OK;
+}
+
+// Room to publish k more steps now: pacing by max_in_flight (waits for the
+// step max_in_flight before the last of them), max_steps, a live grid.
+int engine_room(sccsum_engine* e, uint32_t k, uint64_t timeout_ns) {
     if (__atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE)) return SCCSUM_EIDLE;
+    const uint64_t last = e->next_step + k - 1;
+    if (last >= e->max_steps) return SCCSUM_EBUSY;  // the run's descriptors are used up: stop, start again
+    if (last >= e->max_in_flight) return engine_wait_done(e, last - e->max_in_flight, timeout_ns);
+    return SCCSUM_OK;
+}
+
+// Write one step's descriptor over checked batches (nbatch 0: an empty step,
+// done at once) and publish it; engine_room made the room.  kind = the
+// descriptor's kind word, dep = 0 or 1 + the step its tiles wait for.
+uint64_t engine_put(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint64_t kind, uint64_t dep) {
+    uint64_t n_total = 0, bytes_total = 0;
+    for (uint32_t i = 0; i < nbatch; ++i) {
+        n_total += batches[i].n;
+        bytes_total += batches[i].n ? batches[i].bytes_len : 0;
+    }
+    uint64_t B = sccsum::kStoreTilePackets;  // store tiles: four frames per lane
+    if ((kind & 0xffu) != sccsum::kStepFillStore) {
+        // tile size as a launch would pick it (launch_flat): ~tile_bytes of packets, at most 64
+        const sccsum::Knobs& K = sccsum::t_knobs;
+        uint64_t bmax = static_cast<uint64_t>(K.tile_packets);
+        if (K.tile_bytes && n_total) {
+            const uint64_t mean = bytes_total / n_total ? bytes_total / n_total : 1;
+            const uint64_t tb = static_cast<uint64_t>(K.tile_bytes);
+            const uint64_t bb = tb / mean ? tb / mean : 1;
+            bmax = bb < bmax ? bb : bmax;
+        }
+        B = e->waves ? (n_total + e->waves - 1) / e->waves : 1;
+        B = B < 1 ? 1 : (B > bmax ? bmax : B);
+    }
     const uint64_t s = e->next_step;
-    if (s >= e->max_steps) return SCCSUM_EBUSY;  // the run's descriptors are used up: stop, start again
-    if (s >= e->max_in_flight) {
-        const int rc = engine_wait_done(e, s - e->max_in_flight, timeout_ns);
-        if (rc != SCCSUM_OK) return rc;
-    }
-    // tile size as a launch would pick it (launch_flat): ~tile_bytes of packets, at most 64
-    const sccsum::Knobs& K = sccsum::t_knobs;
-    uint64_t bmax = static_cast<uint64_t>(K.tile_packets);
-    if (K.tile_bytes && n_total) {
-        const uint64_t mean = bytes_total / n_total ? bytes_total / n_total : 1;
-        const uint64_t bb = static_cast<uint64_t>(K.tile_bytes) / mean ? static_cast<uint64_t>(K.tile_bytes) / mean : 1;
-        bmax = bb < bmax ? bb : bmax;
-    }
-    uint64_t B = e->waves ? (n_total + e->waves - 1) / e->waves : 1;
-    B = B < 1 ? 1 : (B > bmax ? bmax : B);
     uint64_t* const d = e->ring_h + s * sccsum::kEngineSlotWords;
     uint64_t tile0[SCCSUM_ENGINE_MAX_BATCHES + 1] = {};
     uint32_t nq = 0;
@@ -2949,6 +3089,8 @@ int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t
     d[sccsum::kEdStep] = s;
     d[sccsum::kEdNq] = nq ? nq : 1;
     for (uint32_t q = 0; q <= SCCSUM_ENGINE_MAX_BATCHES; ++q) d[sccsum::kEdTile0 + q] = tile0[q];
+    d[sccsum::kEdKind] = kind;
+    d[sccsum::kEdDep] = dep;
     if (ntiles == 0) {  // nothing to sum: done at once (the descriptor still keeps the walk in order)
         __atomic_store_n(e->ctl_h + sccsum::kEcDone + 8u * s, s + 1, __ATOMIC_RELEASE);
     }
@@ -2956,7 +3098,175 @@ int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t
     e->next_step = s + 1;
     // publish: the descriptor is complete before the grid's poller can see the step
     __atomic_store_n(e->ctl_h + sccsum::kEcPublished, e->next_step, __ATOMIC_SEQ_CST);
-    *step = s;
+    return s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, sccsum_engine** out) {
+    const int base = mode & ~SCCSUM_ENGINE_FILL;
+    const bool fill = (mode & SCCSUM_ENGINE_FILL) != 0;
+    if (!out || (base != SCCSUM_PIPE_IPV4 && base != SCCSUM_PIPE_SPANS) || (fill && base != SCCSUM_PIPE_IPV4) ||
+        max_steps == 0 || max_steps > sccsum::kEngineMaxSteps || max_in_flight == 0 ||
+        max_in_flight > sccsum::kEngineCountSlots || (fill && max_in_flight < 2)) {
+        return SCCSUM_EINVAL;
+    }
+    *out = nullptr;
+    int n = 0;
+    hipError_t e0 = hipGetDeviceCount(&n);
+    if (e0 != hipSuccess) return static_cast<int>(e0);
+    if (device < 0 || device >= n || device >= sccsum::kMaxDevices) return SCCSUM_ENODEV;
+    const CurrentDevice keep;  // the allocations go to `device`; the caller's binding is put back
+    if ((e0 = hipSetDevice(device)) != hipSuccess) return static_cast<int>(e0);
+    auto* e = new (std::nothrow) sccsum_engine;
+    if (!e) return static_cast<int>(hipErrorOutOfMemory);
+    e->device = device;
+    e->frames = base == SCCSUM_PIPE_IPV4;
+    e->fill = fill;
+    e->max_steps = max_steps;
+    e->max_in_flight = max_in_flight;
+    const uint64_t ring_bytes = uint64_t(max_steps) * sccsum::kEngineSlotWords * 8u;
+    const uint64_t ctl_bytes = (sccsum::kEcDone + 8u * uint64_t(max_steps)) * 8u;
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
+    void *rh = nullptr, *ch = nullptr, *rd = nullptr, *cd = nullptr, *cl = nullptr, *co = nullptr, *gd = nullptr,
+         *dr = nullptr, *mi = nullptr, *sd = nullptr;
+    hipError_t r = hipHostMalloc(&rh, ring_bytes, fl);
+    if (r == hipSuccess) r = hipHostMalloc(&ch, ctl_bytes, fl);
+    if (r == hipSuccess) r = hipHostGetDevicePointer(&rd, rh, 0);
+    if (r == hipSuccess) r = hipHostGetDevicePointer(&cd, ch, 0);
+    const size_t claims_b = size_t(sccsum::kGroups) * sccsum::kHeadStride * 4u;
+    const size_t counts_b = size_t(sccsum::kEngineCountSlots) * sccsum::kGroups * sccsum::kHeadStride * 4u;
+    const size_t gdone_b = size_t(sccsum::kEngineCountSlots) * sccsum::kHeadStride * 4u;
+    const size_t sdone_b = size_t(sccsum::kEngineCountSlots) * 8u * 8u;
+    if (r == hipSuccess) r = hipMalloc(&cl, claims_b);
+    if (r == hipSuccess) r = hipMalloc(&co, counts_b);
+    if (r == hipSuccess) r = hipMalloc(&gd, gdone_b);
+    if (r == hipSuccess) r = hipMalloc(&dr, ring_bytes);
+    if (r == hipSuccess) r = hipMalloc(&mi, sccsum::kMirrorWords * 8u);
+    if (r == hipSuccess) r = hipMalloc(&sd, sdone_b);
+    if (r == hipSuccess) r = hipEventCreateWithFlags(&e->left, hipEventDisableTiming);
+    if (r != hipSuccess) {
+        for (void* p : {rh, ch}) if (p) (void)hipHostFree(p);
+        for (void* p : {cl, co, gd, dr, mi, sd}) if (p) (void)hipFree(p);
+        delete e;
+        return static_cast<int>(r);
+    }
+    std::memset(rh, 0, ring_bytes);
+    std::memset(ch, 0, ctl_bytes);
+    e->ring_h = static_cast<uint64_t*>(rh);
+    e->ctl_h = static_cast<uint64_t*>(ch);
+    e->args.hring = static_cast<const uint64_t*>(rd);
+    e->args.dring = static_cast<uint64_t*>(dr);
+    e->args.mirror = static_cast<uint64_t*>(mi);
+    e->args.ctl = static_cast<uint64_t*>(cd);
+    e->args.claims = static_cast<uint32_t*>(cl);
+    e->args.counts = static_cast<uint32_t*>(co);
+    e->args.gdone = static_cast<uint32_t*>(gd);
+    e->args.sdone = static_cast<uint64_t*>(sd);
+    e->args.idle_ticks = 100000000ull;  // 1 s at the constant 100 MHz clock
+    e->args.dep_ticks = 200000000ull;   // 2 s
+    *out = e;
+    return SCCSUM_OK;
+}
+
+int sccsum_engine_start(sccsum_engine* e, void* stream) {
+    if (!e || e->running) return SCCSUM_EINVAL;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    int dev = 0;
+    if (const int rc = sccsum::launch_device(s, &dev); rc != SCCSUM_OK) return rc;
+    if (dev != e->device) return SCCSUM_EINVAL;
+    {
+        std::lock_guard<std::mutex> g(g_live_mu);
+        if (g_live[dev] != nullptr) return SCCSUM_EBUSY;  // another engine's run holds the device
+        g_live[dev] = e;
+    }
+    // the last run's grid has left (stop only asks it to): its control words are ours again
+    if (e->launched) {
+        const hipError_t w = e->left_recorded ? hipEventSynchronize(e->left) : hipStreamSynchronize(e->stream);
+        if (w != hipSuccess) {
+            release_live(e);
+            return static_cast<int>(w);
+        }
+    }
+    // a new run: no step published, none done, counters zero (stream-ordered before the grid)
+    std::memset(e->ctl_h, 0, (sccsum::kEcDone + 8u * uint64_t(e->max_steps)) * 8u);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    const size_t claims_b = size_t(sccsum::kGroups) * sccsum::kHeadStride * 4u;
+    const size_t counts_b = size_t(sccsum::kEngineCountSlots) * sccsum::kGroups * sccsum::kHeadStride * 4u;
+    const size_t gdone_b = size_t(sccsum::kEngineCountSlots) * sccsum::kHeadStride * 4u;
+    const size_t sdone_b = size_t(sccsum::kEngineCountSlots) * 8u * 8u;
+    hipError_t r = hipMemsetAsync(e->args.claims, 0, claims_b, s);
+    if (r == hipSuccess) r = hipMemsetAsync(e->args.counts, 0, counts_b, s);
+    if (r == hipSuccess) r = hipMemsetAsync(e->args.gdone, 0, gdone_b, s);
+    if (r == hipSuccess) r = hipMemsetAsync(e->args.mirror, 0, sccsum::kMirrorWords * 8u, s);
+    if (r == hipSuccess) r = hipMemsetAsync(e->args.sdone, 0, sdone_b, s);
+    if (r != hipSuccess) {
+        release_live(e);
+        return static_cast<int>(r);
+    }
+    const sccsum::Knobs& K = sccsum::t_knobs;
+    uint32_t flags = static_cast<uint32_t>(K.out_policy) << sccsum::kOutPolicyShift;
+    if (K.engine_wt) flags |= sccsum::kFlagEngineWT;
+    if (!K.short_chunks) flags |= sccsum::kFlagFullChunks;
+    flags |= static_cast<uint32_t>(K.run_align == 8 ? 2 : (K.run_align == 4 ? 1 : 0)) << sccsum::kRunAlignShift;
+    e->args.idle_ticks = static_cast<uint64_t>(K.engine_idle_ms) * 100000ull;  // 100 MHz ticks
+    r = e->fill ? sccsum::launch_engine<true, true>(s, dev, e->args, flags, &e->waves)
+                : (e->frames ? sccsum::launch_engine<true>(s, dev, e->args, flags, &e->waves)
+                             : sccsum::launch_engine<false>(s, dev, e->args, flags, &e->waves));
+    if (r != hipSuccess) {
+        release_live(e);
+        return static_cast<int>(r);
+    }
+    e->left_recorded = hipEventRecord(e->left, s) == hipSuccess;  // else the next start syncs the stream
+    e->launched = true;
+    e->stream = s;
+    e->running = true;
+    e->next_step = 0;
+    e->next_first = 0;
+    return SCCSUM_OK;
+}
+
+int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
+                         uint64_t timeout_ns, uint64_t* step) {
+    (void)max_len;
+    if (!e || !e->running || !step) return SCCSUM_EINVAL;
+    if (const int rc = engine_check(e, batches, nbatch, false); rc != SCCSUM_OK) return rc;
+    if (const int rc = engine_room(e, 1, timeout_ns); rc != SCCSUM_OK) return rc;
+    *step = engine_put(e, batches, nbatch, sccsum::kStepSum, 0);
+    return SCCSUM_OK;
+}
+
+// In-place fill as two steps published together: the generate step, then the
+// store step whose tiles wait for it.  Both or neither: the room for two is
+// made first (max_in_flight >= 2 for a fill engine, so that wait never waits
+// on the generate step itself).  The store step right behind its generate
+// step runs as a phase of its own: its waves wait out the generate step's
+// drain (~10-18 us) and then store with few reads beside them.  Deferred
+// behind the next fill's generate step instead (no drain wait), the store
+// tiles of the groups that finished first ran inside the other groups' read
+// stream, and a fill took 354-356 us against 328 (profiles/r05_engine_fill.log).
+int sccsum_engine_submit_fill(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t mode,
+                              uint64_t timeout_ns, uint64_t* step) {
+    constexpr uint32_t kEngineModes = SCCSUM_FILL_IP | SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO;
+    if (!e || !e->running || !step || !e->fill || (mode & ~kEngineModes) ||
+        !(mode & (SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO))) {
+        return SCCSUM_EINVAL;
+    }
+    if (const int rc = engine_check(e, batches, nbatch, true); rc != SCCSUM_OK) return rc;
+    if (const int rc = engine_room(e, 2, timeout_ns); rc != SCCSUM_OK) return rc;
+    const uint64_t kflags = ((mode & SCCSUM_FILL_L4) ? sccsum::kFlagFillL4 : 0u) |
+                            ((mode & SCCSUM_FILL_ICMP_ECHO) ? sccsum::kFlagFillIcmp : 0u) |
+                            ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u);
+    const uint64_t gen = engine_put(e, batches, nbatch, sccsum::kStepFillGen | (kflags << 8) | (uint64_t(mode) << 16), 0);
+    // the store half: no status (the generate half reported it)
+    sccsum_batch st[SCCSUM_ENGINE_MAX_BATCHES];
+    for (uint32_t i = 0; i < nbatch; ++i) {
+        st[i] = batches[i];
+        st[i].d_status = nullptr;
+    }
+    *step = engine_put(e, st, nbatch, sccsum::kStepFillStore | (uint64_t(mode) << 16), gen + 1);
     return SCCSUM_OK;
 }
 
@@ -2969,6 +3279,7 @@ int sccsum_engine_stop(sccsum_engine* e) {
     if (!e || !e->running) return SCCSUM_EINVAL;
     __atomic_store_n(e->ctl_h + sccsum::kEcStop, 1ull, __ATOMIC_SEQ_CST);
     e->running = false;
+    release_live(e);  // the grid leaves once the published steps are done
     return __atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE) ? SCCSUM_EIDLE : SCCSUM_OK;
 }
 
@@ -2988,6 +3299,7 @@ int sccsum_engine_destroy(sccsum_engine* e) {
     (void)hipFree(e->args.gdone);
     (void)hipFree(e->args.dring);
     (void)hipFree(e->args.mirror);
+    (void)hipFree(e->args.sdone);
     if (e->left) (void)hipEventDestroy(e->left);
     delete e;
     return rc;
@@ -2999,7 +3311,7 @@ const char* sccsum_strerror(int err) {
     if (err == SCCSUM_OK) return "success";
     if (err == SCCSUM_EINVAL) return "invalid argument";
     if (err == SCCSUM_ENODEV) return "no such HIP device";
-    if (err == SCCSUM_EBUSY) return "every batch slot is in flight";
+    if (err == SCCSUM_EBUSY) return "busy: every batch slot or engine step is in flight, or the device's engine is running";
     if (err == SCCSUM_EIDLE) return "the engine's grid gave up waiting for steps";
     if (err > 0) return hipGetErrorString(static_cast<hipError_t>(err));
     return "unknown sccsum error";
@@ -3253,6 +3565,12 @@ int sccsum_set_out_policy(int policy) {
 
 int sccsum_set_engine_write_through(int on) {
     sccsum::t_knobs.engine_wt = on ? 1 : 0;
+    return SCCSUM_OK;
+}
+
+int sccsum_set_engine_idle_ms(int ms) {
+    if (ms < 1 || ms > 3600000) return SCCSUM_EINVAL;
+    sccsum::t_knobs.engine_idle_ms = ms;
     return SCCSUM_OK;
 }
 

@@ -32,7 +32,7 @@ FILL_L4 = 0x02
 FILL_L4_PSEUDO = 0x04
 FILL_TSO = 0x08
 FILL_ICMP_ECHO = 0x10
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class SccsumError(RuntimeError):
@@ -103,12 +103,15 @@ _PROTOS = {
     "sccsum_engine_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _u32, _u32, ctypes.POINTER(_vp)]),
     "sccsum_engine_start": (ctypes.c_int, [_vp, _vp]),
     "sccsum_engine_submit": (ctypes.c_int, [_vp, _vp, _u32, _u32, _u64, ctypes.POINTER(_u64)]),
+    "sccsum_engine_submit_fill": (ctypes.c_int, [_vp, _vp, _u32, _u32, _u64, ctypes.POINTER(_u64)]),
+    "sccsum_set_engine_idle_ms": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_engine_wait": (ctypes.c_int, [_vp, _u64, _u64]),
     "sccsum_engine_stop": (ctypes.c_int, [_vp]),
     "sccsum_engine_destroy": (ctypes.c_int, [_vp]),
 }
 PIPE_SPANS = 0
 PIPE_IPV4 = 1
+ENGINE_FILL = 0x100
 GATHER_NONE = 0
 GATHER_HOST = 1
 GATHER_STRIDED = 2

@@ -111,14 +111,22 @@ static void checks() {
     EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_SPANS, 16, 0, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_SPANS, 16, 65, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, 16, 2, nullptr) == SCCSUM_EINVAL);
+    // fill steps: frames only, and at least 2 steps in flight (a fill is two)
+    EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_SPANS | SCCSUM_ENGINE_FILL, 16, 2, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_IPV4 | SCCSUM_ENGINE_FILL, 16, 1, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_IPV4 | 0x200, 16, 2, &eng) == SCCSUM_EINVAL);
     EXPECT(eng == nullptr);
     EXPECT(sccsum_engine_start(nullptr, nullptr) == SCCSUM_EINVAL);
     uint64_t step = 0;
     EXPECT(sccsum_engine_submit(nullptr, nullptr, 1, 0, 0, &step) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_submit_fill(nullptr, nullptr, 1, SCCSUM_FILL_IP | SCCSUM_FILL_L4, 0, &step) ==
+           SCCSUM_EINVAL);
     EXPECT(sccsum_engine_wait(nullptr, 0, 0) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_stop(nullptr) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_destroy(nullptr) == SCCSUM_OK);
     EXPECT(sccsum_set_engine_write_through(0) == SCCSUM_OK && sccsum_set_engine_write_through(1) == SCCSUM_OK);
+    EXPECT(sccsum_set_engine_idle_ms(0) == SCCSUM_EINVAL && sccsum_set_engine_idle_ms(3600001) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_engine_idle_ms(250) == SCCSUM_OK && sccsum_set_engine_idle_ms(1000) == SCCSUM_OK);
     // host pipeline
     sccsum_pipeline* p = nullptr;
     EXPECT(sccsum_pipeline_create(0, 1 << 20, 1024, 0, &p) == SCCSUM_EINVAL);
@@ -168,7 +176,8 @@ static void checks() {
     // host arithmetic and strings
     EXPECT(sccsum_pseudo_seed(1, 2, 17, 8) == 28u);
     EXPECT(sccsum_pseudo_seed(0xffffffffu, 0xffffffffu, 255, 0xffff) <= 0xffffu);
-    EXPECT(std::strcmp(sccsum_strerror(SCCSUM_EBUSY), "every batch slot is in flight") == 0);
+    EXPECT(std::strcmp(sccsum_strerror(SCCSUM_EBUSY),
+                       "busy: every batch slot or engine step is in flight, or the device's engine is running") == 0);
     EXPECT(std::strcmp(sccsum_strerror(-99), "unknown sccsum error") == 0);
     EXPECT(sccsum_abi_version() == SCCSUM_ABI_VERSION);
 }

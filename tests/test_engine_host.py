@@ -8,9 +8,9 @@ import torch
 from seastar_amd import batch, native
 
 
-def _engine(frames: bool) -> batch.Engine:
+def _engine(frames: bool, fill: bool = False) -> batch.Engine:
     e = object.__new__(batch.Engine)  # no device here: skip sccsum_engine_create
-    e.frames, e.max_in_flight, e._keep, e._h = frames, 2, {}, None
+    e.frames, e.fill, e.max_in_flight, e._keep, e._h = frames, fill, 2, {}, None
     return e
 
 
@@ -45,6 +45,17 @@ def test_items_are_checked_before_the_c_abi():
     # well-formed items on host tensors: refused for their memory, not their shape
     with pytest.raises(ValueError, match="device tensors"):
         _engine(True).prepare([(b, torch.zeros(8, dtype=torch.int16), torch.zeros(4, dtype=torch.uint8))])
+
+
+def test_fill_steps_need_a_fill_engine_and_out2():
+    b = _batch()
+    st = torch.zeros(4, dtype=torch.uint8)
+    with pytest.raises(ValueError, match="fill=True"):
+        _engine(True).prepare([(b, torch.zeros(8, dtype=torch.int16), st)], fill_mode=native.FILL_L4)
+    with pytest.raises(ValueError, match="needs out2"):
+        _engine(True, fill=True).prepare([(b, None, st)], fill_mode=native.FILL_L4)
+    with pytest.raises(ValueError, match="device tensors"):  # well-formed: refused for host memory only
+        _engine(True, fill=True).prepare([(b, torch.zeros(8, dtype=torch.int16), st)], fill_mode=native.FILL_L4)
 
 
 def test_close_without_a_handle_is_a_no_op():

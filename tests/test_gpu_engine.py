@@ -234,3 +234,246 @@ def test_engine_results_readable_while_the_grid_runs(dev):
     for host, want in got:
         assert np.array_equal(host.numpy().view(np.uint16).reshape(-1, 2), want)
     eng.close()
+
+
+# ---- in-place fill through the engine (sccsum_engine_submit_fill) ---------------
+
+ENGINE_FILL_MODES = {
+    "ip_l4": native.FILL_IP | native.FILL_L4,
+    "l4": native.FILL_L4,
+    "icmp_echo": native.FILL_ICMP_ECHO,
+    "ip_l4_icmp_echo": native.FILL_IP | native.FILL_L4 | native.FILL_ICMP_ECHO,
+}
+
+
+@pytest.mark.parametrize("mode", list(ENGINE_FILL_MODES))
+def test_engine_fill_steps_match_oracle(dev, mode):
+    """Fill steps (generate, then the store step that waits for it) of the tx
+    generator's odd frames — UDP / TCP / ICMP, options, padding, truncation,
+    runts, IP fragments, garbage checksum fields, odd offsets — among verify
+    steps of other batches, in one run: every filled buffer is byte-exact
+    against the oracle's writers (ip.cc:266-278, udp.cc:184-195,
+    tcp.hh:1656-1694, ip.cc:464-474), with its out2 values and status; each
+    batch is filled again later in the same run, into fresh out2 / status
+    (generate tiles then read bytes that store tiles of the same grid wrote):
+    the oracle's second fill of its own first result — the same bytes (a fill
+    is idempotent), and the values and status bits that second fill reports
+    (an echo request answered by the first fill is a reply the second leaves
+    alone); the verify steps equal the oracle too."""
+    from test_gpu_parity import _tx_frames
+
+    m = ENGINE_FILL_MODES[mode]
+    rng = np.random.default_rng(0xEF00 + m)
+    fills, verifies = [], []
+    for k in range(6):
+        items = []
+        for q in range(int(rng.integers(1, 4))):
+            buf, off, length = _tx_frames(rng, int(rng.integers(100, 1200)))
+            b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+            out2 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+            st = torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev) if q != 1 else None
+            want1 = oracle.batch_ipv4_fill(buf, off, length, m)
+            want2 = oracle.batch_ipv4_fill(want1[0], off, length, m)
+            again = (torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev),
+                     torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev))
+            items.append((b, out2, st, want1, again, want2))
+        fills.append(items)
+        b, want, want_st = _frames_step(rng, dev, int(rng.integers(0, 3)))
+        out = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+        verifies.append((b, out, want))
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, fill=True, max_steps=64, max_in_flight=4)
+    stream = torch.cuda.Stream(device=dev)
+    eng.start(stream)
+    ids = []
+    for items, (vb, vout, _) in zip(fills, verifies):
+        ids.append(eng.submit_fill([(it[0], it[1], it[2]) for it in items], m))
+        ids.append(eng.submit([(vb, vout, None)]))
+    for items in fills:  # again
+        ids.append(eng.submit_fill([(it[0], it[4][0], it[4][1]) for it in items], m))
+    for i in ids:
+        eng.wait(i)
+    eng.stop()
+    stream.synchronize()
+    for items in fills:
+        for b, out2, st, want1, (out2b, stb), want2 in items:
+            got = b.data.cpu().numpy()[: b.bytes_len]
+            assert np.array_equal(want2[0], want1[0])  # the oracle's own fill is idempotent
+            bad = np.nonzero(got != want1[0])[0]
+            assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+            assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want1[1])
+            if st is not None:
+                assert np.array_equal(st.cpu().numpy(), want1[2])
+            assert np.array_equal(batch.as_u16(out2b).reshape(-1, 2), want2[1])
+            assert np.array_equal(stb.cpu().numpy(), want2[2])
+    for b, out, want in verifies:
+        assert np.array_equal(batch.as_u16(out).reshape(-1, 2), want)
+    eng.close()
+
+
+def test_engine_fill_full_scale(dev):
+    """cfg 2 tx at full size through the engine: 4 rotated 1 M x 1500 B batches
+    with garbage checksum fields, filled 3 times each in one run; the fields
+    equal classic generate (on zeroed fields), every frame verifies, and the
+    out2 values are the ones stored."""
+    from seastar_amd import devsynth
+
+    n, R = 1 << 20, 4
+    bs = [devsynth.udp_frames(n, 1500, seed=300 + r, device=dev) for r in range(R)]
+    gens = [batch.ipv4_frames(b).clone() for b in bs]
+    for b in bs:
+        f = b.data[: n * 1500].view(n, 1500)
+        f[:, 10:12] = 0xA5
+        f[:, 26:28] = 0x3C
+    outs = [torch.empty(2 * n, dtype=torch.int16, device=dev) for _ in range(R)]
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, fill=True, max_steps=64, max_in_flight=8)
+    stream = torch.cuda.Stream(device=dev)
+    preps = [eng.prepare([(bs[r], outs[r], None)], fill_mode=native.FILL_IP | native.FILL_L4) for r in range(R)]
+    eng.start(stream)
+    last = [eng.submit_prepared(preps[k % R]) for k in range(3 * R)][-1]
+    eng.wait(last)
+    eng.stop()
+    stream.synchronize()
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    for b, gen, out in zip(bs, gens, outs):
+        f = b.data[: n * 1500].view(n, 1500)
+        got = torch.stack([f[:, 10:12].contiguous().view(torch.int16).view(-1),
+                           f[:, 26:28].contiguous().view(torch.int16).view(-1)], dim=1)
+        assert torch.equal(got, gen)
+        assert torch.equal(out.view(n, 2), gen)
+        batch.ipv4_frames(b, status=st)
+        assert int((st == 3).sum()) == n
+    eng.close()
+
+
+# ---- sharing the device (include/sccsum.h, "Sharing the device") ---------------
+
+def test_second_engine_on_the_device_is_refused(dev):
+    """One engine runs per device: while the first run holds device 0, a second
+    engine's start returns SCCSUM_EBUSY and changes nothing; the first run's
+    results stay exact; after its stop the second engine runs."""
+    rng = np.random.default_rng(0xE6)
+    b, want, _ = _frames_step(rng, dev, 0)
+    o1 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+    o2 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+    torch.cuda.synchronize()
+    e1 = batch.Engine(0, frames=True, max_steps=8, max_in_flight=2)
+    e2 = batch.Engine(0, frames=True, max_steps=8, max_in_flight=2)
+    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    e1.start(s1)
+    with pytest.raises(native.SccsumError) as e:
+        e2.start(s2)
+    assert e.value.code == native.SCCSUM_EBUSY
+    e1.wait(e1.submit([(b, o1, None)]))
+    e1.stop()
+    s1.synchronize()
+    assert np.array_equal(batch.as_u16(o1).reshape(-1, 2), want)
+    e2.start(s2)  # the device is free again
+    e2.wait(e2.submit([(b, o2, None)]))
+    e2.stop()
+    s2.synchronize()
+    assert np.array_equal(batch.as_u16(o2).reshape(-1, 2), want)
+    e1.close()
+    e2.close()
+
+
+def test_launch_from_another_thread_completes_after_stop(dev):
+    """Seastar's shared-device model: one shard runs the engine, another shard
+    thread (its own sccsum_init, its own stream) launches frames meanwhile.
+    The launch queues behind the resident grid and completes after the run's
+    stop, with exact results; the engine's own steps are exact too."""
+    import threading
+
+    rng = np.random.default_rng(0xE7)
+    b, want, _ = _frames_step(rng, dev, 0)
+    b2, want2, want2_st = _frames_step(rng, dev, 1)
+    o_eng = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+    o_thr = torch.full((2 * b2.n,), -1, dtype=torch.int16, device=dev)
+    st_thr = torch.full((b2.n,), 0xEE, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, max_steps=8, max_in_flight=2)
+    stream = torch.cuda.Stream(device=dev)
+    eng.start(stream)
+    eng.wait(eng.submit([(b, o_eng, None)]))
+    errors, launched, finished = [], threading.Event(), threading.Event()
+
+    def shard():
+        try:
+            native.check(native.load().sccsum_init(0), "sccsum_init")
+            s = torch.cuda.Stream(device=dev)
+            batch.ipv4_frames(b2, out2=o_thr, status=st_thr, stream=s)
+            launched.set()
+            s.synchronize()
+            finished.set()
+        except Exception as ex:  # noqa: BLE001 - reported below
+            errors.append(ex)
+            launched.set()
+
+    t = threading.Thread(target=shard)
+    t.start()
+    assert launched.wait(30)
+    eng.wait(eng.submit([(b, o_eng, None)]))  # the engine keeps taking steps meanwhile
+    eng.stop()
+    stream.synchronize()
+    t.join(60)
+    assert not t.is_alive() and not errors, errors
+    assert finished.is_set()
+    assert np.array_equal(batch.as_u16(o_eng).reshape(-1, 2), want)
+    assert np.array_equal(batch.as_u16(o_thr).reshape(-1, 2), want2)
+    assert np.array_equal(st_thr.cpu().numpy(), want2_st)
+    eng.close()
+
+
+def test_engine_create_keeps_the_callers_device(dev):
+    """sccsum_engine_create allocates on its device and leaves the calling
+    thread's current device as it was (it used to switch it)."""
+    import ctypes
+
+    lib = native.load()
+    ndev = ctypes.c_int()
+    native.check(lib.sccsum_device_count(ctypes.byref(ndev)), "device count")
+    target = ndev.value - 1  # another device where there is one
+    torch.cuda.set_device(0)
+    native.check(lib.sccsum_init(0), "sccsum_init")
+    before = torch.cuda.current_device()
+    eng = batch.Engine(target, frames=True, max_steps=4, max_in_flight=1)
+    assert torch.cuda.current_device() == before == 0
+    eng.close()
+
+
+def test_engine_low_rate_steps_all_complete(dev):
+    """small steps at a steady low rate.  With a 300 ms idle
+    limit and one 64-frame step (64 one-frame tiles) every 10 ms, a wave whose
+    claim lies ~4 000 tiles ahead waits ~0.6 s for its step — past the limit
+    when it was timed per wave.  Timed from the grid's last new step, the run
+    never gives up while steps keep coming: every step completes, exact."""
+    import time
+
+    lib = native.load()
+    buf, off, lens, _ = synth.udp_ipv4_frames(64, 256, seed=5)
+    b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+    want, _ = oracle.batch_ipv4(buf, off, lens)
+    steps = 100
+    outs = [torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev) for _ in range(steps)]
+    torch.cuda.synchronize()
+    native.check(lib.sccsum_set_engine_idle_ms(300), "idle")
+    try:
+        eng = batch.Engine(0, frames=True, max_steps=steps + 1, max_in_flight=4)
+        stream = torch.cuda.Stream(device=dev)
+        eng.start(stream)
+        t0 = time.perf_counter()
+        ids = []
+        for k in range(steps):
+            while time.perf_counter() < t0 + 0.01 * k:
+                pass
+            ids.append(eng.submit([(b, outs[k], None)]))
+        for i in ids:
+            eng.wait(i)
+        eng.stop()  # raises SccsumError(EIDLE) if any wave had given up
+        stream.synchronize()
+    finally:
+        lib.sccsum_set_engine_idle_ms(1000)
+    for o in outs:
+        assert np.array_equal(batch.as_u16(o).reshape(-1, 2), want)
+    eng.close()
