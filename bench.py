@@ -104,6 +104,9 @@ def parse():
     ap.add_argument("--sync", default="auto", choices=["auto", "spin", "yield"],
                     help="how the host thread waits on the device (hipSetDeviceFlags schedule)")
     ap.add_argument("--seg-len", type=int, default=65536, help="tcp64k: segment bytes (65536, or 65535: odd offsets)")
+    ap.add_argument("--verify-only", action="store_true",
+                    help="mixed (single / engine form): the step writes the status byte alone, no out2 (the "
+                         "reference's verify keeps only get() != 0, ip.cc:121-127)")
     ap.add_argument("--align", type=int, default=1, help="mixed: frame start alignment (1 = packed, SURVEY §8(d) (i); "
                                                          "64 = layout (ii))")
     ap.add_argument("--streams", type=int, default=1,
@@ -250,7 +253,9 @@ def dist_setup(dry_run=False, args=None):
     if dry_run:
         # the launcher test's stand-ins for the GPUs: PCI ids (one per local rank) and device count
         bdfs = [b for b in os.environ.get("SCCSUM_DRY_RUN_BDFS", "").split(",") if b]
-        check_devices(local_world, int(os.environ.get("SCCSUM_DRY_RUN_NDEV", str(max(len(bdfs), local_world)))), share)
+        ndev_dry = int(os.environ.get("SCCSUM_DRY_RUN_NDEV", str(max(len(bdfs), local_world))))
+        check_devices(local_world, ndev_dry, share)
+        DRY_DEVICE.update(device=local % max(ndev_dry, 1), pci_bus_id=bdfs[local % len(bdfs)] if bdfs else None)
         NUMA.update(place_rank(bdfs[local % len(bdfs)] if bdfs else None, numa_mode))
         if world > 1:
             import torch.distributed as dist
@@ -503,11 +508,14 @@ def _timed(step, steps, warmup, world, streams, s0, begin, end):
     return wall, e0.elapsed_time(e1) / 1e3 / steps
 
 
+DRY_DEVICE = {}  # --dry-run: the stand-in device index and PCI address of this rank
+
+
 def device_id(dev) -> dict:
     """Which GPU a rank ran on: its index and PCI address (so a slow device
     or box shows up by name in a multi-GPU line)."""
     if dev is None:
-        return {"device": None, "pci_bus_id": None}
+        return {"device": DRY_DEVICE.get("device"), "pci_bus_id": DRY_DEVICE.get("pci_bus_id")}
     p = torch.cuda.get_device_properties(dev)
     return {"device": dev.index, "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0",
             "device_name": p.name}
@@ -529,7 +537,29 @@ def per_rank(world, rank, dev, **fields):
 
     out = [None] * world
     dist.all_gather_object(out, me)
+    check_distinct_devices(out, SHARE_DEVICES)
     return out
+
+
+SHARE_DEVICES = False  # --share-devices
+
+
+def check_distinct_devices(pr, share: bool) -> None:
+    """Every rank on a device of its own: no two ranks of one host on the same
+    device index or PCI address, unless --share-devices asked for sharing
+    (a rank -> device mapping that stacked ranks on device 0
+    would pass every other check).  Every rank holds the gathered list, so
+    all of them stop together."""
+    if share:
+        return
+    seen_dev, seen_bdf = {}, {}
+    for r in pr:
+        for key, seen in (((r["host"], r["device"]), seen_dev), ((r["host"], r["pci_bus_id"]), seen_bdf)):
+            if key[1] is None:
+                continue
+            if key in seen:
+                sys.exit(f"bench.py: ranks {seen[key]} and {r['rank']} share {key} without --share-devices")
+            seen[key] = r["rank"]
 
 
 def rank_rate(nbytes_per_step, steps):
@@ -556,6 +586,21 @@ def roofline(alg_bytes_launch: float, launch_s: float, config: str, kernel: str,
     if extra:
         d.update(extra)
     return d
+
+
+def layout_traffic(alg_bytes: float, gap_bytes: int, packet_bytes: int, frac: float) -> dict:
+    """What a layout's gaps cost: frames placed at 64 B
+    boundaries leave gap bytes between them that the stream reads with the
+    frames (memory moves whole lines; a gap is never wider than the line
+    holding its frame's end).  The bytes a launch streams are the algorithmic
+    bytes plus the gaps, so the line's frac, divided by the traffic ratio,
+    is not kernel loss: frac x ratio is the rate per byte actually streamed,
+    the figure to compare with the packed layout's frac."""
+    ratio = (alg_bytes + gap_bytes) / alg_bytes if alg_bytes else 1.0
+    return {"gap_bytes": int(gap_bytes), "gap_per_packet_byte": round(gap_bytes / packet_bytes, 5) if packet_bytes else 0.0,
+            "traffic_ratio": round(ratio, 5), "frac_of_streamed_bytes": round(frac * ratio, 4),
+            "note": "layout (ii)'s ceiling is the packed layout's frac / traffic_ratio: the gaps are read, "
+                    "not counted"}
 
 
 def emit(metric, value, unit, args, world, wall, dtype, config, roof=None, cpu=None, extra=None):
@@ -765,6 +810,7 @@ def run_mixed(args, world, rank, dev):
     n = args.packets if args.packets != (1 << 20) else 3_400_000
     multi = (args.launch or "single") == "multi"
     engine = args.launch == "engine"
+    vonly = args.verify_only and not multi
     lens = synth.zipf_lengths(n, seed=SEED + rank)
     lens_rx = synth.zipf_lengths(n, seed=SEED + 7717 + rank) if multi else lens
     R = max(1, args.rotate)  # distinct batches launched in turn (no cached-line replay)
@@ -799,9 +845,10 @@ def run_mixed(args, world, rank, dev):
                for r in range(R) for i in range(ns)}
     else:
         kern = flat_kernel(True, False, n, rxs[0].bytes_len)
-        # prebuilt launches: a step only crosses the C-ABI
+        # prebuilt launches: a step only crosses the C-ABI (--verify-only: status bits, no out2)
         pre = {(r, i): batch.prepare_call("sccsum_ipv4_frames", rxs[r].data, rxs[r].bytes_len, rxs[r].off,
-                                          rxs[r].length, outs[i][1], None, rxs[r].n, rxs[r].max_len)
+                                          rxs[r].length, None if vonly else outs[i][1], sts[r] if vonly else None,
+                                          rxs[r].n, rxs[r].max_len)
                for r in range(R) for i in range(ns)}
     warm = max(args.warmup, R)
     step, begin, end, eng = (lambda k: pre[(k % R, k % ns)](streams[k % ns])), None, None, None
@@ -809,7 +856,7 @@ def run_mixed(args, world, rank, dev):
         kern = "csum_engine_kernel<16, true, false>"
         eng = batch.Engine(dev.index or 0, frames=True, max_steps=max(warm, args.steps) + 4,
                            max_in_flight=args.engine_in_flight)
-        pre_e = {r: eng.prepare([(rxs[r], outs[0][1], None)]) for r in range(R)}
+        pre_e = {r: eng.prepare([(rxs[r], None, sts[r]) if vonly else (rxs[r], outs[0][1], None)]) for r in range(R)}
 
         def step(k):
             eng.submit_prepared(pre_e[k % R])
@@ -824,7 +871,7 @@ def run_mixed(args, world, rank, dev):
     # per launch: every frame byte + 12 B metadata + the results: 4 B per frame, except a multi step's rx
     # half, which writes 1 B of status bits (+ 4 B with --rx-out2)
     alg = (total + n * (META_BYTES + 4) + n * (META_BYTES + 1 + (4 if args.rx_out2 else 0)) if multi
-           else total + n * (META_BYTES + 4))
+           else total + n * (META_BYTES + (1 if vonly else 4)))
     roof_alg, roof_s = alg, launch_s
     if engine:  # the launch is the run: every step's bytes over the run's time (the same ratio)
         roof_alg, roof_s = alg * args.steps, launch_s * args.steps
@@ -832,13 +879,17 @@ def run_mixed(args, world, rank, dev):
     ceiling = read_ceiling(rxs[0].data, rxs[0].bytes_len, stream)
     ranks = per_rank(world, rank, dev, **rank_rate(nbytes, args.steps), avg_launch_us=launch_s * 1e6,
                      read_ceiling_GBps=ceiling, frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS)
+    # the gap bytes a step's batches hold between their frames (--align 64: layout (ii))
+    gap = (rxs[0].bytes_len + (txs[0].bytes_len if multi else 0)) - total
+    lay = layout_traffic(alg, gap, total, alg / launch_s / 1e9 / HBM_PEAK_GBPS)
     if rank == 0:
         emit("GiB/s device-resident Internet checksum, mixed-MTU Zipf batches (cfg 3)",
              world * nbytes * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
              {"workload": ("cfg3: Zipf(s=1.2) IPv4/UDP frames 64..9000 B, packed back to back (odd offsets)" if align == 1
                            else f"cfg3 (ii): Zipf(s=1.2) IPv4/UDP frames 64..9000 B, each at a {align} B boundary")
                           + ("; step = generate over a tx batch + verify over an rx batch" if multi
-                             else "; step = verify over one batch"),
+                             else ("; step = verify over one batch, status bits only" if vonly
+                                   else "; step = verify over one batch (both checksums written)")),
               "packets_per_gpu": (2 * n if multi else n), "bytes_per_gpu": total,
               "mean_len": round(total / (2 * n if multi else n), 1),
               "launch": ("one sccsum_ipv4_frames_multi launch per step over the tx and rx batches" if multi
@@ -851,7 +902,8 @@ def run_mixed(args, world, rank, dev):
                       kern + (" (sccsum_ipv4_frames_multi, tx + rx)" if multi else
                               (" (sccsum_engine_*; one launch = the timed run)" if engine
                                else " (sccsum_ipv4_frames)")), sel, args,
-                      {"measured_read_ceiling_GBps": round(ceiling, 1)}), extra={"per_rank": ranks})
+                      {"measured_read_ceiling_GBps": round(ceiling, 1), "layout_traffic": lay}),
+             extra={"per_rank": ranks})
 
 
 def run_slots(args, world, rank, dev):
@@ -1274,8 +1326,9 @@ def run_dry(args, world, rank):
 
 def main():
     args = parse()
-    global SYNC_MODE
+    global SYNC_MODE, SHARE_DEVICES
     SYNC_MODE = args.sync
+    SHARE_DEVICES = args.share_devices
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     _imports()

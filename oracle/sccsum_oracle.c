@@ -256,37 +256,54 @@ static void* run_job(void* arg) {
  * With `cpus`, thread t runs pinned to CPU cpus[t] (smp::pin,
  * src/core/reactor.cc:4163 — one shard per core). */
 #define ORACLE_MAX_THREADS 1024
+/* Never fails: an empty or missing cpus list, a CPU id outside cpu_set_t, a
+ * failed allocation or thread creation all fall back to running the work (or
+ * that thread's share of it) on the calling thread, unpinned. */
 static void run_batch(job_t base, uint64_t n, int nthreads, const int* cpus) {
-    if ((nthreads <= 1 && !cpus) || n < 2) {
+    if (nthreads < 1 || n < 2 || (nthreads == 1 && !cpus)) {
         base.lo = 0;
         base.hi = n;
         run_job(&base);
         return;
     }
-    if (nthreads < 1) nthreads = 1;
     if (nthreads > ORACLE_MAX_THREADS) nthreads = ORACLE_MAX_THREADS;
     pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
     job_t* jobs = (job_t*)malloc(sizeof(job_t) * (size_t)nthreads);
+    char* started = (char*)calloc((size_t)nthreads, 1);
+    if (!th || !jobs || !started) {
+        free(th);
+        free(jobs);
+        free(started);
+        base.lo = 0;
+        base.hi = n;
+        run_job(&base);
+        return;
+    }
     for (int t = 0; t < nthreads; ++t) {
         jobs[t] = base;
         jobs[t].lo = n * (uint64_t)t / (uint64_t)nthreads;
         jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)nthreads;
         pthread_attr_t attr;
-        pthread_attr_init(&attr);
-        if (cpus) {
+        if (pthread_attr_init(&attr) != 0) continue; /* run inline below */
+        if (cpus && cpus[t] >= 0 && cpus[t] < CPU_SETSIZE) {
             cpu_set_t set;
             CPU_ZERO(&set);
             CPU_SET(cpus[t], &set);
             pthread_attr_setaffinity_np(&attr, sizeof(set), &set);
         }
-        pthread_create(&th[t], &attr, run_job, &jobs[t]);
+        started[t] = pthread_create(&th[t], &attr, run_job, &jobs[t]) == 0;
         pthread_attr_destroy(&attr);
     }
     for (int t = 0; t < nthreads; ++t) {
-        pthread_join(th[t], 0);
+        if (started[t]) {
+            pthread_join(th[t], 0);
+        } else {
+            run_job(&jobs[t]);
+        }
     }
     free(th);
     free(jobs);
+    free(started);
 }
 
 void oracle_batch_spans(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,

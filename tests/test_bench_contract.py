@@ -106,3 +106,18 @@ def test_flat_kernel_names_follow_the_library_choice():
     assert bench.flat_kernel(True, False, 128 * kb, 128 * kb * 1500) == "csum_flat_kernel<8, true, false, true, false>"
     assert bench.flat_kernel(True, False, 262144, 262144 * 442) == "csum_flat_kernel<8, true, false, true, false>"
     assert bench.flat_kernel(True, True, 256 * kb, 256 * kb * 1500) == "csum_flat_kernel<8, true, true, true, true>"
+
+
+def test_layout_traffic_of_aligned_frames():
+    """cfg 3 (ii) (--align 64) lines carry roofline.layout_traffic: the gap
+    bytes between 64 B-aligned frames, their share of the packet bytes, the
+    traffic ratio they add to the algorithmic bytes and frac x ratio, the
+    rate per streamed byte (74.9 % at 1.08x traffic is
+    the packed layout's rate, not kernel loss)."""
+    bench = _bench()
+    alg, gap, packets = 1.557e9, 116_000_000, 1_503_052_521
+    d = bench.layout_traffic(alg, gap, packets, 0.749)
+    assert d["gap_bytes"] == gap and abs(d["gap_per_packet_byte"] - gap / packets) < 1e-5
+    assert abs(d["traffic_ratio"] - (alg + gap) / alg) < 1e-5
+    assert abs(d["frac_of_streamed_bytes"] - 0.749 * (alg + gap) / alg) < 1e-4
+    assert bench.layout_traffic(alg, 0, packets, 0.8)["traffic_ratio"] == 1.0  # packed: no gaps

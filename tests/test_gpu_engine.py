@@ -477,3 +477,43 @@ def test_engine_low_rate_steps_all_complete(dev):
     for o in outs:
         assert np.array_equal(batch.as_u16(o).reshape(-1, 2), want)
     eng.close()
+
+
+def test_engine_reads_bytes_rewritten_during_the_run(dev):
+    """A shard refills its buffers while the run goes on (a NIC's DMA, a host
+    copy between steps): a step must read the bytes as they are when it is
+    submitted, not lines an earlier step of the same run left in an XCD's L2.
+    One small batch (64 x 1500 B) is rewritten by host-to-device copies (copy
+    engine, pinned memory) between steps; every step equals the oracle on the
+    bytes it was given."""
+    rng = np.random.default_rng(0xE9)
+    contents = []
+    for k in range(8):
+        buf, off, lens, _ = synth.udp_ipv4_frames(64, 1500, seed=int(rng.integers(1 << 30)))
+        buf = buf.copy()
+        for i in range(64):  # random payloads, random checksum fields: each content verifies differently
+            o = int(off[i])
+            buf[o + 28:o + 1500] = rng.integers(0, 256, 1472, dtype=np.uint8)
+            buf[o + 10:o + 12] = rng.integers(0, 256, 2, dtype=np.uint8)
+        contents.append((buf, off, lens, oracle.batch_ipv4(buf, off, lens)))
+    b = batch.PacketBatch.from_host(contents[0][0], contents[0][1], contents[0][2], device=dev)
+    hosts = [torch.from_numpy(np.concatenate([c[0], np.zeros(b.data.numel() - c[0].size, np.uint8)])).pin_memory()
+             for c in contents]
+    outs = [torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev) for _ in contents]
+    sts = [torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev) for _ in contents]
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, max_steps=32, max_in_flight=2)
+    stream, side = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    eng.start(stream)
+    for rep in range(2):
+        for k in range(len(contents)):
+            with torch.cuda.stream(side):
+                b.data.copy_(hosts[k], non_blocking=True)
+            side.synchronize()
+            eng.wait(eng.submit([(b, outs[k], sts[k])]))
+    eng.stop()
+    stream.synchronize()
+    for (buf, off, lens, (want, want_st)), o, st in zip(contents, outs, sts):
+        assert np.array_equal(batch.as_u16(o).reshape(-1, 2), want)
+        assert np.array_equal(st.cpu().numpy(), want_st)
+    eng.close()

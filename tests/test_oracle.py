@@ -323,3 +323,16 @@ def test_fill_driver_icmp_echo_and_fragments():
             assert g[20:] == m and not st[i] & 2
     assert out2[1, 1] == 0xFFFF  # all-zero message
     assert st[len(msgs)] & 16
+
+
+def test_pinned_batch_survives_bad_cpu_lists():
+    """oracle_batch_ipv4_cpus never reads past its list or overflows
+    cpu_set_t: an empty list, CPU ids past CPU_SETSIZE and
+    negative ids still give the single-thread results."""
+    from seastar_amd import synth
+
+    buf, off, lens, _ = synth.mixed_udp_frames(3000, seed=9, max_gap=3)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
+    for cpus in ([], [5000, 70000], [-1, 0, 1 << 20]):
+        got, st = oracle.batch_ipv4(buf, off, lens, cpus=cpus)
+        assert np.array_equal(got, want) and np.array_equal(st, want_st), cpus

@@ -40,15 +40,24 @@ def _free_port():
     return p
 
 
-def _engine_gpu(sbuf, soff, slen):
+def _engine_gpu(sbuf, soff, slen, rank):
+    """Rank r drives device r % ndev (bench.dist_setup's mapping), bound and
+    initialised as a shard thread is (sccsum_init(d)); on the one-GPU box both
+    ranks share device 0."""
     import torch
-    from seastar_amd import batch
+    from seastar_amd import batch, native
 
-    b = batch.PacketBatch.from_host(sbuf, soff, slen, device="cuda:0")
+    ndev = torch.cuda.device_count()
+    d = rank % ndev
+    torch.cuda.set_device(d)
+    native.check(native.load().sccsum_init(d), "sccsum_init")
+    b = batch.PacketBatch.from_host(sbuf, soff, slen, device=f"cuda:{d}")
     status = torch.zeros(max(b.n, 1), dtype=torch.uint8, device=b.device)
     out = batch.ipv4_frames(b, status=status)
-    torch.cuda.synchronize()
-    return out.cpu().numpy().view(np.uint16), status[:b.n].cpu().numpy()
+    torch.cuda.synchronize(d)
+    p = torch.cuda.get_device_properties(d)
+    where = (d, f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0", ndev)
+    return out.cpu().numpy().view(np.uint16), status[:b.n].cpu().numpy(), where
 
 
 def _worker(rank, world, port, q, engine="oracle", n=3000):
@@ -56,17 +65,27 @@ def _worker(rank, world, port, q, engine="oracle", n=3000):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     buf, off, lens, _ = synth.mixed_udp_frames(n, seed=5, max_gap=3)
     sbuf, soff, slen, (lo, hi) = shard.shard(buf, off, lens, rank, world)
+    where = None
     if engine == "gpu":
-        out, st = _engine_gpu(sbuf, soff, slen)
+        out, st, where = _engine_gpu(sbuf, soff, slen, rank)
     else:
         out, st = oracle.batch_ipv4(sbuf, soff, slen)
     parts = [None] * world
-    dist.all_gather_object(parts, (lo, hi, out, st))
+    dist.all_gather_object(parts, (lo, hi, out, st, where))
     if rank == 0:
-        full = shard.assemble([(a, b, o) for a, b, o, _ in parts], lens.size, width=2)
-        full_st = shard.assemble([(a, b, s) for a, b, _, s in parts], lens.size, dtype=np.uint8)
+        full = shard.assemble([(a, b, o) for a, b, o, _, _ in parts], lens.size, width=2)
+        full_st = shard.assemble([(a, b, s) for a, b, _, s, _ in parts], lens.size, dtype=np.uint8)
         want, want_st = oracle.batch_ipv4(buf, off, lens)
-        q.put(bool(np.array_equal(full, want) and np.array_equal(full_st, want_st)))
+        ok = bool(np.array_equal(full, want) and np.array_equal(full_st, want_st))
+        devs = [w for *_, w in parts]
+        if engine == "gpu":
+            ndev = devs[0][2]
+            # one device per rank wherever there are enough: indices and PCI addresses differ
+            if ndev >= world:
+                ok = ok and len({w[0] for w in devs}) == world and len({w[1] for w in devs}) == world
+            else:
+                ok = ok and [w[0] for w in devs] == [r % ndev for r in range(world)]
+        q.put((ok, devs))
     dist.destroy_process_group()
 
 
@@ -77,11 +96,12 @@ def _run(world, engine, n):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q, engine, n)) for r in range(world)]
     for p in procs:
         p.start()
-    ok = q.get(timeout=180)
+    ok, devs = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
-    assert ok
+    assert ok, devs
     assert all(p.exitcode == 0 for p in procs)
+    return devs
 
 
 def test_two_rank_gloo_shards_match_unsharded():
@@ -90,4 +110,7 @@ def test_two_rank_gloo_shards_match_unsharded():
 
 @pytest.mark.gpu
 def test_two_rank_gpu_engine_shards_match_oracle():
-    _run(2, "gpu", 20000)
+    """Two ranks, rank r on device r % ndev: devices 0 and 1 where two are
+    visible, both on device 0 on the one-GPU box (stated in the output)."""
+    devs = _run(2, "gpu", 20000)
+    print("rank devices:", devs)

@@ -1,12 +1,18 @@
 """Per-launch fixed cost of the flat kernel: launches over k = 1, 2, 4, 8
-distinct 1 M x 1500 B batches (one sccsum_ipv4_frames_multi launch over k
-queues), batches rotated so no launch rereads cached lines.  A line fit
-T(k) = a + k * b gives the launch's fixed cost a (ramp, drain, dispatch) and
-the steady-state per-batch time b.
+distinct batches (one sccsum_ipv4_frames_multi launch over k queues), batches
+rotated so no launch rereads cached lines.  A line fit T(k) = a + k * b gives
+the launch's fixed cost a (ramp, drain, dispatch) and the steady-state
+per-batch time b.
 
-usage: python tools/ab_launch_len.py [reps] [tile_packets,...]
-(tile_packets: sccsum_diag.h's per-tile packet cap, one fit per value)
+Batches: cfg 2's 1 M x 1500 B frames (default), or with --mixed cfg 3's
+Zipf(1.2) frames 64..9000 B packed at odd offsets (3.4 M frames, ~1.5 GB per
+batch).  Outputs: both checksums per frame (out2, 4 B; the default), or with
+--verify-only the status byte alone (the reference's verify keeps only
+get() != 0: ip.cc:121-127).
+
+usage: python tools/ab_launch_len.py [--reps R] [--tiles 64,32] [--mixed] [--verify-only] [--ks 1,2,4,8]
 """
+import argparse
 import os
 import sys
 
@@ -14,31 +20,54 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from seastar_amd import batch, devsynth, native  # noqa: E402
+from seastar_amd import batch, devsynth, native, synth  # noqa: E402
 
 FRAME = 1500
 
 
 def main():
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+    ap = argparse.ArgumentParser()
+    ap.add_argument("reps_pos", nargs="?", type=int, default=None)
+    ap.add_argument("tiles_pos", nargs="?", default=None)
+    ap.add_argument("--reps", type=int, default=12)
+    ap.add_argument("--tiles", default="64")
+    ap.add_argument("--mixed", action="store_true")
+    ap.add_argument("--verify-only", action="store_true")
+    ap.add_argument("--ks", default="1,2,4,8")
+    a = ap.parse_args()
+    reps = a.reps_pos or a.reps
+    tiles = a.tiles_pos or a.tiles
     native.check(native.load().sccsum_init(0), "sccsum_init")
     dev = torch.device("cuda:0")
-    n, NB = 1 << 20, 12
-    bs = [devsynth.udp_frames(n, FRAME, seed=101 + r, device=dev) for r in range(NB)]
-    outs = [torch.empty(2 * n, dtype=torch.int16, device=dev) for _ in range(8)]
+    ks = [int(x) for x in a.ks.split(",")]
+    NB = max(12, 2 * max(ks))
+    if a.mixed:
+        n = 3_400_000
+        lens = synth.zipf_lengths(n, seed=0x5EA57A2C)
+        bs = [devsynth.mixed_frames(lens, seed=0x5EA57A2C + 7 * r, device=dev) for r in range(NB)]
+        nbytes = int(lens.sum())
+    else:
+        n = 1 << 20
+        bs = [devsynth.udp_frames(n, FRAME, seed=101 + r, device=dev) for r in range(NB)]
+        nbytes = n * FRAME
+    outs = [torch.empty(2 * n, dtype=torch.int16, device=dev) for _ in range(max(ks))]
+    sts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(max(ks))]
     s = torch.cuda.current_stream()
-    tps = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [64]
-    for tp in tps:
+    print(f"{'cfg 3 Zipf frames' if a.mixed else 'cfg 2 1500 B frames'}: {n} frames, {nbytes} B per batch; "
+          f"{'status only (verify-only)' if a.verify_only else 'out2 (both checksums)'}", flush=True)
+    for tp in [int(x) for x in tiles.split(",")]:
         native.check(native.load().sccsum_set_tile_packets(tp), "tile_packets")
         print(f"tile_packets {tp}", flush=True)
-        fit(bs, outs, s, n, NB, reps)
+        fit(bs, outs, sts, s, n, nbytes, NB, reps, ks, a.verify_only)
 
 
-def fit(bs, outs, s, n, NB, reps):
+def fit(bs, outs, sts, s, n, nbytes, NB, reps, ks, verify_only):
     rows = []
-    for k in (1, 2, 4, 8):
+    per_out = 1 if verify_only else 4
+    for k in ks:
         def launch(j):
-            items = [(bs[(j * k + q) % NB], outs[q], None) for q in range(k)]
+            items = [(bs[(j * k + q) % NB], None if verify_only else outs[q], sts[q] if verify_only else None)
+                     for q in range(k)]
             batch.ipv4_frames_multi(items, stream=s)
 
         for j in range(4):
@@ -51,15 +80,16 @@ def fit(bs, outs, s, n, NB, reps):
         e1.record(s)
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / reps
-        alg = k * n * (FRAME + 12 + 4)
+        alg = k * (nbytes + n * (12 + per_out))
         rows.append((k, us))
         print(f"k={k}: {us:8.1f} us/launch  {alg / us / 1e3:7.1f} GB/s  {alg / us / 1e3 / 8000:.4f} of 8 TB/s",
               flush=True)
-    ks = np.array([r[0] for r in rows], float)
+    kk = np.array([r[0] for r in rows], float)
     ts = np.array([r[1] for r in rows], float)
-    b, a = np.polyfit(ks, ts, 1)
-    print(f"fit: T(k) = {a:.1f} us + k * {b:.1f} us  (steady {n * (FRAME + 16) / b / 1e3:.1f} GB/s = "
-          f"{n * (FRAME + 16) / b / 1e3 / 8000:.4f} of 8 TB/s)")
+    b, a = np.polyfit(kk, ts, 1)
+    alg1 = nbytes + n * (12 + per_out)
+    print(f"fit: T(k) = {a:.1f} us + k * {b:.1f} us  (steady {alg1 / b / 1e3:.1f} GB/s = "
+          f"{alg1 / b / 1e3 / 8000:.4f} of 8 TB/s)", flush=True)
 
 
 if __name__ == "__main__":
