@@ -104,9 +104,6 @@ def parse():
     ap.add_argument("--sync", default="auto", choices=["auto", "spin", "yield"],
                     help="how the host thread waits on the device (hipSetDeviceFlags schedule)")
     ap.add_argument("--seg-len", type=int, default=65536, help="tcp64k: segment bytes (65536, or 65535: odd offsets)")
-    ap.add_argument("--verify-only", action="store_true",
-                    help="mixed (single / engine form): the step writes the status byte alone, no out2 (the "
-                         "reference's verify keeps only get() != 0, ip.cc:121-127)")
     ap.add_argument("--align", type=int, default=1, help="mixed: frame start alignment (1 = packed, SURVEY §8(d) (i); "
                                                          "64 = layout (ii))")
     ap.add_argument("--streams", type=int, default=1,
@@ -120,8 +117,9 @@ def parse():
                          "into it as they go, at most --engine-in-flight in flight (sccsum_engine_*, DESIGN.md "
                          "§5.11; fill: sccsum_engine_submit_fill)")
     ap.add_argument("--rx-out2", action="store_true",
-                    help="udp1500 / mixed: the verify (rx) half also writes both checksums per frame (default: status "
-                         "bits only, what the reference's verify keeps: ip.cc:121-127, tcp.hh:876-883)")
+                    help="udp1500 / mixed: the verify (rx) half — mixed's single form: its one batch — also writes "
+                         "both checksums per frame (default: status bits only, what the reference's verify keeps: "
+                         "ip.cc:121-127, tcp.hh:876-883)")
     ap.add_argument("--dry-run", action="store_true",
                     help="multi-rank plumbing only: launch, rendezvous, barrier, max-over-ranks, one line; "
                          "no device call (the CPU test of the launcher)")
@@ -810,7 +808,9 @@ def run_mixed(args, world, rank, dev):
     n = args.packets if args.packets != (1 << 20) else 3_400_000
     multi = (args.launch or "single") == "multi"
     engine = args.launch == "engine"
-    vonly = args.verify_only and not multi
+    # the verify step writes the status byte alone, what the reference's verify keeps (ip.cc:121-127:
+    # drop when get() != 0); --rx-out2 adds both checksums (2-3.6 % slower: profiles/r05_cfg3_terms.log)
+    vonly = not multi and not args.rx_out2
     lens = synth.zipf_lengths(n, seed=SEED + rank)
     lens_rx = synth.zipf_lengths(n, seed=SEED + 7717 + rank) if multi else lens
     R = max(1, args.rotate)  # distinct batches launched in turn (no cached-line replay)

@@ -566,15 +566,6 @@ __device__ __forceinline__ uint32_t header_dword(const u32x4 (&h)[4], uint32_t h
 // kOutPolicyShift..+2): 0 = plain global store; buffer stores with 1 = nt,
 // 2 = sc1, 3 = sc0 sc1, 4 = sc0.  t + lane is the element this lane writes.
 constexpr uint32_t kOutPolicyShift = 8;
-// f(integral_constant<int, I>) for I in [I0, N): indices the compiler sees as constants
-template <int I, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, N>(f);
-    }
-}
-
 template <typename T>
 __device__ __forceinline__ void tile_store(T* t, uint32_t lane, T v, uint32_t pol) {
     if (pol == 0) {
@@ -820,13 +811,7 @@ __device__ unsigned long long g_step_xcd[kStepRec][8][2];
 #endif
 
 constexpr int kGapUnits = 4;  // flat runs tolerate gaps of up to 4 units (64 B) between packets
-// flat_body: result slots a wave of the U = 16 launch forms defers its stores in
-#ifdef SCCSUM_AB_NODEFER
-constexpr bool kDeferResults = false;  // A/B only: results stored after each tile
-#else
-constexpr bool kDeferResults = true;
-#endif
-constexpr int kDeferSlots = 32;
+
 
 // The batches one flat-kernel launch works through: up to kMaxQueues
 // independent batches (rx / tx queues, the tx and rx halves of a step), each
@@ -1688,37 +1673,6 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
             if (status) tile_store(status + bse, lane, static_cast<uint8_t>(sv), pol_st);
         }
     };
-    // Deferred result stores (launches of the U = 16 forms): a wave keeps its
-    // tiles' results in registers — KD slots: the result word and the status
-    // byte of the lane's packet, the tile number in lane k of dtile — and
-    // stores them when the slots are full and when it leaves the tile loop, so
-    // most of a launch's result writes leave in its drain, when the read
-    // stream no longer fills HBM.  Stored after each tile, cfg 3's results
-    // (13.6 MB of out2, or 3.4 MB of status) cost its stream 12 / 7 us
-    // (profiles/r05_cfg3_terms.log).  An engine stores as it goes: its steps
-    // report while the grid runs.
-    constexpr bool kDefer = !Src::kEngine && U >= 16 && kDeferResults;
-    constexpr int KD = kDefer ? kDeferSlots : 4;
-    uint32_t dtile = 0;
-    uint32_t dword[KD];
-    uint32_t dst[KD / 4];
-    uint32_t nd = 0;
-    auto dflush = [&]() {
-        for (uint32_t k = 0; k < nd; ++k) {
-            uint32_t wd = 0, sv = 0;
-            static_for<0, KD>([&](auto kc) {
-                constexpr int kk = decltype(kc)::value;
-                if (static_cast<uint32_t>(kk) == k) {
-                    wd = dword[kk];
-                    sv = (dst[kk / 4] >> (8 * (kk % 4))) & 0xffu;
-                }
-            });
-            const uint32_t tk = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dtile), static_cast<int>(k)));
-            const Ref r = src.ref(tk);
-            put(r, r.base, lane < r.cnt, wd, sv);
-        }
-        nd = 0;
-    };
 #ifdef SCCSUM_AB_TIMELINE
     const unsigned long long tl_start = wall_clock64();
     unsigned long long tl_first = 0, tl_tiles = 0;
@@ -2060,25 +2014,7 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
             }
         }
 
-        if constexpr (kDefer) {
-            // slot nd keeps this tile's results (uniform nd: scalar branches;
-            // constant indices keep the slots in registers)
-            static_for<0, KD>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                if (static_cast<uint32_t>(k) == nd) dword[k] = word;
-            });
-            static_for<0, KD / 4>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                if (static_cast<uint32_t>(j) == nd / 4u) {
-                    const uint32_t sh = 8u * (nd % 4u);
-                    dst[j] = (dst[j] & ~(0xffu << sh)) | ((st & 0xffu) << sh);
-                }
-            });
-            dtile = lane == nd ? static_cast<uint32_t>(t) : dtile;
-            if (++nd == static_cast<uint32_t>(KD)) dflush();
-        } else {
-            put(cur.ref, base, mine, word, st);
-        }
+        put(cur.ref, base, mine, word, st);
         // (readfirstlane: the compiler otherwise loses the tile number's
         // uniformity across the issue branches and reads the next tile's queue
         // fields with vector loads, 8 more per tile)
@@ -2095,9 +2031,6 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
         }
         t = t1;
         t1 = t2;
-    }
-    if constexpr (kDefer) {
-        if (nd) dflush();
     }
 #ifdef SCCSUM_AB_TIMELINE
     if (lane == 0 && wglob < kTimelineWaves) {
