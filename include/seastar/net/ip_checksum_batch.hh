@@ -18,6 +18,8 @@
 //   toeplitz_hash(rss_key(), forward_hash)  net.cc:330-341    ipv4_rss(batch, key, ...) / ipv4_frames_rss(...)
 //   per packet as qp::poll_tx / DPDK rx hand them over         burst_queue (host packets, async completion)
 //       net.cc:81-105, dpdk.cc:2190-2204
+//   a shard's steady stream of bursts, polled like its queues  resident_engine (one grid, steps streamed in;
+//       reactor.cc:3543-3550                                   fills too: submit_fill)
 //
 // Results are network-order uint16 values, exactly what checksummer::get()
 // returns; a verify passes when the value is 0.  Errors throw
@@ -212,6 +214,64 @@ public:
         return did != 0;
     }
     void drain() { check(sccsum_burst_drain(_q), "sccsum_burst_drain"); }
+};
+
+// Resident engine (<sccsum.h> sccsum_engine_*): one grid kept on the GPU
+// while a shard streams steps into it, as the reactor keeps polling its
+// queues (reactor.cc:3543-3550); each step is up to 4 batches, computed
+// exactly as the one-launch calls compute them.  Frames engines may take
+// in-place fills (fill = true).  One engine runs per device at a time:
+// try_start() is false while another engine of the process runs there.
+//   resident_engine eng(gpu, SCCSUM_PIPE_IPV4, /*max_steps=*/4096, /*in flight=*/8, /*fill=*/true);
+//   eng.start(stream);
+//   sccsum_batch tx = {...}, rx = {...};
+//   uint64_t a = eng.submit_fill(&tx, 1, SCCSUM_FILL_IP | SCCSUM_FILL_L4);
+//   uint64_t b = eng.submit(&rx, 1);
+//   eng.wait(b); eng.wait(a); eng.stop();
+class resident_engine {
+    sccsum_engine* _e = nullptr;
+
+    static void check(int rc, const char* what) {
+        if (rc != SCCSUM_OK) {
+            throw std::runtime_error(std::string(what) + ": " + sccsum_strerror(rc));
+        }
+    }
+
+public:
+    resident_engine(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, bool fill = false) {
+        check(sccsum_engine_create(device, mode | (fill ? SCCSUM_ENGINE_FILL : 0), max_steps, max_in_flight, &_e),
+              "sccsum_engine_create");
+    }
+    resident_engine(const resident_engine&) = delete;
+    resident_engine& operator=(const resident_engine&) = delete;
+    ~resident_engine() { sccsum_engine_destroy(_e); }
+
+    // launch the grid on `stream` (the calling thread's current device, the engine's)
+    void start(void* stream) { check(sccsum_engine_start(_e, stream), "sccsum_engine_start"); }
+    // false: another engine of this process runs on the device (SCCSUM_EBUSY)
+    bool try_start(void* stream) {
+        const int rc = sccsum_engine_start(_e, stream);
+        if (rc == SCCSUM_EBUSY) return false;
+        check(rc, "sccsum_engine_start");
+        return true;
+    }
+    uint64_t submit(const sccsum_batch* batches, uint32_t nbatch, uint64_t timeout_ns = 1'000'000'000) {
+        uint64_t step = 0;
+        check(sccsum_engine_submit(_e, batches, nbatch, 0, timeout_ns, &step), "sccsum_engine_submit");
+        return step;
+    }
+    // in-place fill of every batch (d_out: the values, required); the step returned is done once
+    // the frames hold their checksums
+    uint64_t submit_fill(const sccsum_batch* batches, uint32_t nbatch, uint32_t mode,
+                         uint64_t timeout_ns = 1'000'000'000) {
+        uint64_t step = 0;
+        check(sccsum_engine_submit_fill(_e, batches, nbatch, mode, timeout_ns, &step), "sccsum_engine_submit_fill");
+        return step;
+    }
+    void wait(uint64_t step, uint64_t timeout_ns = 1'000'000'000) {
+        check(sccsum_engine_wait(_e, step, timeout_ns), "sccsum_engine_wait");
+    }
+    void stop() { check(sccsum_engine_stop(_e), "sccsum_engine_stop"); }
 };
 
 }  // namespace net

@@ -71,6 +71,34 @@ def test_batch_cpp_program_on_gpu(tmp_path):
     assert "OK" in r.stdout
 
 
+def _engine_prog(tmp_path) -> str:
+    exe = str(tmp_path / "engine_gpu")
+    cmd = ["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"),
+           os.path.join(REPO, "tests", "cpp", "engine_gpu.cc"), os.path.join(REPO, "seastar_amd", "csrc", "checksummer.cc"),
+           "-L", os.path.join(REPO, "seastar_amd", "lib"), "-lsccsum",
+           "-Wl,-rpath," + os.path.join(REPO, "seastar_amd", "lib"), "-o", exe]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def test_engine_cpp_program_builds(tmp_path):
+    """seastar::net::resident_engine over sccsum_engine_* compiles and links."""
+    _engine_prog(tmp_path)
+
+
+@pytest.mark.gpu
+def test_engine_cpp_program_on_gpu(tmp_path):
+    """Native host program: a shard's resident engine fills frames in place
+    (generate + store steps), verifies them in the same run and generates a
+    copy, all against the per-packet API; a second engine on the device is
+    refused while the first runs and runs after its stop."""
+    exe = _engine_prog(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout
+
+
 def test_burst_queue_header_compiles(tmp_path):
     """seastar::net::burst_queue over sccsum_burst_*, fed a packet's fragment
     array in the reference's own layout (packet.hh:43-46)."""
