@@ -1846,6 +1846,21 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
                 for (uint32_t g = 0; g < ext; g += C) {
                     const uint32_t left = ext - g;
                     const bool last = last_run && left <= C;  // the tile's last loads: then the claim
+#ifndef SCCSUM_AB_NOREMROW
+                    if (left > C && left <= C + static_cast<uint32_t>(kWave)) {
+                        // a full chunk and a remainder of at most one row (a 65 535 B
+                        // segment's extent is 4 097-4 104 units): the row is loaded with
+                        // the chunk, so it costs no round trip of its own
+                        u32x4 v[U];
+                        u32x4 t[1];
+                        load(r, g, v);
+                        load(r, g + C, t);
+                        if (last_run) issue();
+                        chunk(g, v);
+                        chunk(g + C, t);
+                        break;
+                    }
+#endif
                     if (!short_chunks || left > C / 2) {
                         u32x4 v[U];
                         load(r, g, v);
