@@ -517,3 +517,63 @@ def test_engine_reads_bytes_rewritten_during_the_run(dev):
         assert np.array_equal(batch.as_u16(o).reshape(-1, 2), want)
         assert np.array_equal(st.cpu().numpy(), want_st)
     eng.close()
+
+
+def test_engine_fill_limits_and_empty_batches(dev):
+    """A fill takes two of the run's steps, both or neither: with one step
+    left, submit_fill is SCCSUM_EBUSY and publishes nothing; a fill step may
+    hold empty batches beside real ones; a fill on an engine created without
+    SCCSUM_ENGINE_FILL, or without out2, or in a header-only mode, is refused
+    (SCCSUM_EINVAL); the step a fill returns is its store step, done once
+    the frames hold their values."""
+    import ctypes
+
+    from test_gpu_parity import _tx_frames
+
+    rng = np.random.default_rng(0xEA)
+    buf, off, length = _tx_frames(rng, 700)
+    m = native.FILL_IP | native.FILL_L4
+    want = oracle.batch_ipv4_fill(buf, off, length, m)
+    b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+    empty = batch.PacketBatch(data=torch.zeros(16, dtype=torch.uint8, device=dev),
+                              off=torch.zeros(0, dtype=torch.int64, device=dev),
+                              length=torch.zeros(0, dtype=torch.int32, device=dev), bytes_len=0, max_len=0)
+    out2 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+    st = torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    lib = native.load()
+    plain = batch.Engine(0, frames=True, max_steps=4, max_in_flight=2)
+    arr = (native.Batch * 1)()
+    arr[0] = native.Batch(b.data.data_ptr(), b.bytes_len, b.off.data_ptr(), b.length.data_ptr(), None,
+                          out2.data_ptr(), None, b.n)
+    step = ctypes.c_uint64()
+    stream = torch.cuda.Stream(device=dev)
+    plain.start(stream)
+    assert lib.sccsum_engine_submit_fill(plain._h, ctypes.cast(arr, ctypes.c_void_p), 1, m, 10**9,
+                                         ctypes.byref(step)) == native.SCCSUM_EINVAL  # not a fill engine
+    plain.stop()
+    stream.synchronize()
+    plain.close()
+    eng = batch.Engine(0, frames=True, fill=True, max_steps=3, max_in_flight=2)
+    eng.start(stream)
+    no_out = (native.Batch * 1)()
+    no_out[0] = native.Batch(b.data.data_ptr(), b.bytes_len, b.off.data_ptr(), b.length.data_ptr(), None, None,
+                             st.data_ptr(), b.n)
+    assert lib.sccsum_engine_submit_fill(eng._h, ctypes.cast(no_out, ctypes.c_void_p), 1, m, 10**9,
+                                         ctypes.byref(step)) == native.SCCSUM_EINVAL  # no out2
+    assert lib.sccsum_engine_submit_fill(eng._h, ctypes.cast(arr, ctypes.c_void_p), 1,
+                                         native.FILL_IP | native.FILL_L4_PSEUDO, 10**9,
+                                         ctypes.byref(step)) == native.SCCSUM_EINVAL  # header-only mode
+    s1 = eng.submit_fill([(empty, torch.empty(2, dtype=torch.int16, device=dev), None), (b, out2, st)], m)
+    assert s1 == 1  # the store step (the generate step is step 0)
+    with pytest.raises(native.SccsumError) as e:  # one step left: both or neither
+        eng.submit_fill([(b, out2, st)], m)
+    assert e.value.code == native.SCCSUM_EBUSY
+    eng.wait(s1)
+    eng.stop()
+    stream.synchronize()
+    got = b.data.cpu().numpy()[: b.bytes_len]
+    assert np.array_equal(got, want[0])
+    assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want[1])
+    assert np.array_equal(st.cpu().numpy(), want[2])
+    eng.close()
