@@ -1,0 +1,134 @@
+// Small steps through the resident engine against one launch per step, native
+// host side (no Python between steps): the reactor model of SURVEY §8(f)3,
+// where a shard hands its GPU bursts of 32 packets (DPDK rx, dpdk.cc:2190-2204)
+// or tx refills of up to 128 (qp::poll_tx, net.cc:81-105) as they come.
+// For each step size B, k steps over distinct slices of a batch of 1500 B
+// IPv4/UDP frames (verify-only: status bytes), timed on the host clock from
+// the first submit to the last step's completion:
+//   launch  sccsum_ipv4_frames per step on one stream, then one sync
+//   engine  one resident grid per run, sccsum_engine_submit per step
+//           (64 steps in flight), then a wait on the last step
+// Prints one JSON line per size.  Build (tools/gpu_session.sh bin: step):
+//   hipcc -O2 -std=c++17 -I include tools/dev/engine_steps.cc -L seastar_amd/lib -lsccsum \
+//         -Wl,-rpath,$PWD/seastar_amd/lib -o tools/dev/engine_steps
+#include <hip/hip_runtime.h>
+#include <sccsum.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#define HIP_OK(x)                                                                                \
+    do {                                                                                         \
+        hipError_t e_ = (x);                                                                     \
+        if (e_ != hipSuccess) {                                                                  \
+            std::printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);    \
+            return 2;                                                                            \
+        }                                                                                        \
+    } while (0)
+#define SC_OK(x)                                                                                 \
+    do {                                                                                         \
+        int r_ = (x);                                                                            \
+        if (r_ != SCCSUM_OK) {                                                                   \
+            std::printf("sccsum error %s at %s:%d\n", sccsum_strerror(r_), __FILE__, __LINE__);   \
+            return 3;                                                                            \
+        }                                                                                        \
+    } while (0)
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main() {
+    const uint64_t n_all = 1 << 18;  // 262 144 frames, 393 MB
+    const uint32_t L = 1500;
+    std::vector<uint8_t> host(n_all * L);
+    uint64_t x = 0x5EA57A2C;
+    for (auto& b : host) {
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        b = uint8_t(x >> 56);
+    }
+    for (uint64_t i = 0; i < n_all; ++i) {  // IPv4 / UDP headers, fields as sent
+        uint8_t* f = host.data() + i * L;
+        f[0] = 0x45; f[1] = 0; f[2] = L >> 8; f[3] = L & 0xff;
+        f[6] = f[7] = 0; f[8] = 64; f[9] = 17;
+    }
+    std::vector<uint64_t> off(n_all);
+    std::vector<uint32_t> len(n_all, L);
+    for (uint64_t i = 0; i < n_all; ++i) off[i] = i * L;
+    SC_OK(sccsum_init(0));
+    void* d_bytes;
+    uint64_t* d_off;
+    uint32_t* d_len;
+    uint8_t* d_st;
+    HIP_OK(hipMalloc(&d_bytes, host.size() + 16));
+    HIP_OK(hipMalloc(&d_off, n_all * 8));
+    HIP_OK(hipMalloc(&d_len, n_all * 4));
+    HIP_OK(hipMalloc(&d_st, n_all));
+    HIP_OK(hipMemcpy(d_bytes, host.data(), host.size(), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_off, off.data(), n_all * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_len, len.data(), n_all * 4, hipMemcpyHostToDevice));
+    hipStream_t s;
+    HIP_OK(hipStreamCreate(&s));
+    const uint32_t sizes[] = {32, 128, 1024, 16384};
+    for (uint32_t B : sizes) {
+        const uint64_t slices = n_all / B;
+        const uint64_t k = B <= 128 ? 20000 : (B <= 1024 ? 5000 : 400);
+        // a slice: B frames; its offsets are absolute in the one buffer (each step
+        // reads its own B frames: distinct slices, rotating)
+        auto slice = [&](uint64_t j) {
+            sccsum_batch b{};
+            const uint64_t q = j % slices;
+            b.d_bytes = d_bytes;
+            b.bytes_len = host.size();
+            b.d_off = d_off + q * B;
+            b.d_len = d_len + q * B;
+            b.d_status = d_st + q * B;
+            b.n = B;
+            return b;
+        };
+        // launches
+        for (uint64_t j = 0; j < 64; ++j) {
+            const sccsum_batch b = slice(j);
+            SC_OK(sccsum_ipv4_frames(b.d_bytes, b.bytes_len, b.d_off, b.d_len, nullptr, b.d_status, B, L, s));
+        }
+        HIP_OK(hipStreamSynchronize(s));
+        double t0 = now_s();
+        for (uint64_t j = 0; j < k; ++j) {
+            const sccsum_batch b = slice(j);
+            SC_OK(sccsum_ipv4_frames(b.d_bytes, b.bytes_len, b.d_off, b.d_len, nullptr, b.d_status, B, L, s));
+        }
+        HIP_OK(hipStreamSynchronize(s));
+        const double launch_s = now_s() - t0;
+        // engine
+        sccsum_engine* e = nullptr;
+        SC_OK(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, static_cast<uint32_t>(k + 64), 64, &e));
+        double engine_s = 0;
+        for (int run = 0; run < 2; ++run) {  // the first run warms up
+            const uint64_t kk = run ? k : 64;
+            SC_OK(sccsum_engine_start(e, s));
+            uint64_t step = 0;
+            t0 = now_s();
+            for (uint64_t j = 0; j < kk; ++j) {
+                const sccsum_batch b = slice(j);
+                SC_OK(sccsum_engine_submit(e, &b, 1, L, 10'000'000'000ull, &step));
+            }
+            SC_OK(sccsum_engine_wait(e, step, 10'000'000'000ull));
+            if (run) engine_s = now_s() - t0;
+            SC_OK(sccsum_engine_stop(e));
+            HIP_OK(hipStreamSynchronize(s));
+        }
+        SC_OK(sccsum_engine_destroy(e));
+        // (a timing probe: the checksum fields are random, so most frames fail their checks; the
+        // engine's results are checked against the oracle by tests/test_gpu_engine.py)
+        const double bytes = double(k) * B * L;
+        std::printf("{\"packets_per_step\": %u, \"steps\": %llu, \"launch_us_per_step\": %.2f, "
+                    "\"launch_GiBps\": %.1f, \"engine_us_per_step\": %.2f, \"engine_GiBps\": %.1f, "
+                    "\"engine_over_launch\": %.2f}\n",
+                    B, (unsigned long long)k, launch_s / k * 1e6, bytes / launch_s / (1u << 30), engine_s / k * 1e6,
+                    bytes / engine_s / (1u << 30), launch_s / engine_s);
+        std::fflush(stdout);
+    }
+    return 0;
+}
