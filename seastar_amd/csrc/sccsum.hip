@@ -1252,7 +1252,9 @@ struct EngineSrc {
                                                   __HIP_MEMORY_SCOPE_SYSTEM);
                 return false;
             }
-            __builtin_amdgcn_s_sleep(127);  // ~3.4 us
+            // ~3.4 us (s_sleep 32 polled the mirror more and ran 32-packet steps
+            // 13-29 % slower: profiles/r05_engine_small_steps.log)
+            __builtin_amdgcn_s_sleep(127);
         }
     }
     __device__ uint64_t first() {
