@@ -3525,7 +3525,11 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
                                ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u);
         int rc = sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, vals, d_status, n, max_len,
                                       stream, flags);
+#ifdef SCCSUM_AB_FILL_GEN_ONLY
+        if (false) {  // A/B only: the generate pass alone (the frames are not written)
+#else
         if (rc == SCCSUM_OK) {
+#endif
             const unsigned grid = static_cast<unsigned>((n + sccsum::kBlock - 1) / sccsum::kBlock);
             rc = static_cast<int>(sccsum::launch_kernel(sccsum::fill_store_kernel, dim3(grid), s,
                                                         static_cast<uint8_t*>(d_bytes), bytes_len, d_off, d_len,
