@@ -577,3 +577,50 @@ def test_engine_fill_limits_and_empty_batches(dev):
     assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want[1])
     assert np.array_equal(st.cpu().numpy(), want[2])
     eng.close()
+
+
+@pytest.mark.parametrize("in_flight", [2, 64])
+def test_engine_fill_stress_small_steps(dev, in_flight):
+    """Many small steps, fills and verifies interleaved, 2 or 64 in flight:
+    100 fill steps of 1-3 tiny batches (1-40 of the tx generator's odd frames,
+    so every store tile waits on a generate step of a few one-frame tiles)
+    and 100 verify steps between them, in one run.  Every filled batch equals
+    the oracle's fill, every verify the oracle (a race in the store step's
+    dependency would leave fields unwritten or written from stale values)."""
+    from test_gpu_parity import _tx_frames
+
+    rng = np.random.default_rng(0xEB + in_flight)
+    m = native.FILL_IP | native.FILL_L4 | native.FILL_ICMP_ECHO
+    fills, verifies = [], []
+    for k in range(100):
+        items = []
+        for q in range(int(rng.integers(1, 4))):
+            buf, off, length = _tx_frames(rng, int(rng.integers(1, 41)))
+            b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+            out2 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+            st = torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev)
+            items.append((b, out2, st, oracle.batch_ipv4_fill(buf, off, length, m)))
+        fills.append(items)
+        buf, off, length = _tx_frames(rng, int(rng.integers(1, 41)))
+        vb = batch.PacketBatch.from_host(buf, off, length, device=dev)
+        vout = torch.full((2 * vb.n,), -1, dtype=torch.int16, device=dev)
+        verifies.append((vb, vout, oracle.batch_ipv4(buf, off, length)[0]))
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, fill=True, max_steps=512, max_in_flight=in_flight)
+    stream = torch.cuda.Stream(device=dev)
+    eng.start(stream)
+    last = 0
+    for items, (vb, vout, _) in zip(fills, verifies):
+        last = max(last, eng.submit_fill([(b, o, s) for b, o, s, _ in items], m))
+        last = max(last, eng.submit([(vb, vout, None)]))
+    eng.wait(last)
+    eng.stop()
+    stream.synchronize()
+    for items in fills:
+        for b, out2, st, (want_buf, want_out2, want_st) in items:
+            assert np.array_equal(b.data.cpu().numpy()[: b.bytes_len], want_buf)
+            assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want_out2)
+            assert np.array_equal(st.cpu().numpy(), want_st)
+    for vb, vout, want in verifies:
+        assert np.array_equal(batch.as_u16(vout).reshape(-1, 2), want)
+    eng.close()
