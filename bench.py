@@ -97,6 +97,9 @@ def parse():
                     help="A/B: cache policy of the flat kernel's result stores (sccsum_set_out_policy)")
     ap.add_argument("--engine-in-flight", type=int, default=8,
                     help="--launch engine: steps published ahead of the grid (max_in_flight)")
+    ap.add_argument("--engine-sync", type=int, default=None,
+                    help="A/B: --launch engine steps re-synchronise the grid every k steps (the step waits for "
+                         "the one before it; sccsum_set_engine_sync_every)")
     ap.add_argument("--engine-wt", type=int, default=None,
                     help="A/B: engine result stores written through (1) or stored as a launch does (0) "
                          "(sccsum_set_engine_write_through)")
@@ -110,12 +113,13 @@ def parse():
                     help="udp1500 / mixed / fill: step k launches on stream k %% S (A/B: with 2, consecutive steps' "
                          "launches run concurrently)")
     ap.add_argument("--launch", default=None, choices=["multi", "single", "engine"],
-                    help="udp1500 / mixed: one sccsum_ipv4_frames_multi launch per step over the tx and rx batches "
-                         "(multi; udp1500's default) or one sccsum_ipv4_frames launch per batch (single; mixed: "
-                         "the rx batch only, mixed's default — its multi step measured 1-2 %% slower on three "
-                         "boxes, DESIGN.md §5.3); engine = one resident grid per timed run, the steps submitted "
-                         "into it as they go, at most --engine-in-flight in flight (sccsum_engine_*, DESIGN.md "
-                         "§5.11; fill: sccsum_engine_submit_fill)")
+                    help="udp1500 / mixed: engine (the default) = one resident grid per timed run, the steps "
+                         "submitted into it as they go, at most --engine-in-flight in flight, the grid "
+                         "re-synchronised every 10 steps (sccsum_engine_*, DESIGN.md §5.11; fill: "
+                         "sccsum_engine_submit_fill, not its default); multi = one sccsum_ipv4_frames_multi "
+                         "launch per step over the tx and rx batches (udp1500's launch form, and its default with "
+                         "--share-devices); single = one sccsum_ipv4_frames launch per batch (mixed: the rx batch "
+                         "only, mixed's launch form)")
     ap.add_argument("--rx-out2", action="store_true",
                     help="udp1500 / mixed: the verify (rx) half — mixed's single form: its one batch — also writes "
                          "both checksums per frame (default: status bits only, what the reference's verify keeps: "
@@ -432,6 +436,15 @@ class Launches:
 LAUNCHES = Launches()
 
 
+def default_launch(args, launches: str) -> str:
+    """cfg 2 and cfg 3 run through the resident engine by default (round 5):
+    with the grid re-synchronised every 10 big steps (sccsum.hip engine_put)
+    it beats one launch per step by 2.0-2.9 % on the same box
+    (profiles/r05_engine_sync.log).  Ranks that share a device (--share-devices)
+    use launches: one engine grid holds every CU of its device."""
+    return launches if args.share_devices else "engine"
+
+
 def make_streams(args, dev):
     """The step's launch streams: step k goes to streams[k % S].  Default 1 =
     the current stream, one launch at a time, so a launch's duration is the
@@ -632,7 +645,7 @@ def read_ceiling(data, nbytes, stream, reps=10):
 
 def run_udp1500(args, world, rank, dev):
     n = args.packets
-    args.launch = args.launch or "multi"
+    args.launch = args.launch or default_launch(args, "multi")
     # R distinct tx/rx batch pairs launched in turn: 2R x 1.5 GB per rank, so no
     # launch finds its batch's lines left in the 256 MB MALL by an earlier one
     # (a replay of one resident batch would measure cache reuse, not streaming)
@@ -806,7 +819,8 @@ def run_mixed(args, world, rank, dev):
     from seastar_amd import synth
 
     n = args.packets if args.packets != (1 << 20) else 3_400_000
-    multi = (args.launch or "single") == "multi"
+    args.launch = args.launch or default_launch(args, "single")
+    multi = args.launch == "multi"
     engine = args.launch == "engine"
     # the verify step writes the status byte alone, what the reference's verify keeps (ip.cc:121-127:
     # drop when get() != 0); --rx-out2 adds both checksums (2-3.6 % slower: profiles/r05_cfg3_terms.log)
@@ -1347,6 +1361,8 @@ def main():
             native.check(native.load().sccsum_set_blocks_per_cu(args.blocks_per_cu), "sccsum_set_blocks_per_cu")
         if args.out_policy is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_out_policy(args.out_policy), "sccsum_set_out_policy")
+        if args.engine_sync is not None:  # A/B only (sccsum_diag.h)
+            native.check(native.load().sccsum_set_engine_sync_every(args.engine_sync), "sccsum_set_engine_sync_every")
         if args.engine_wt is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_engine_write_through(args.engine_wt),
                          "sccsum_set_engine_write_through")

@@ -66,6 +66,12 @@ int sccsum_set_engine_write_through(int on);
  * a new step before its waiting waves give up and the run reports
  * SCCSUM_EIDLE (default 1000 ms; 1 .. 3 600 000).  Tests shorten it. */
 int sccsum_set_engine_idle_ms(int ms);
+/* Engine steps submitted later by this thread: every k-th step's tiles wait
+ * until the step before it is done (a barrier that lines up dequeue groups
+ * drifting apart over a long run).  -1 (default) = every
+ * 10th step of those with at least 2 tiles per wave of the grid; 0 = never;
+ * k = every k-th step.  SCCSUM_EINVAL outside -1 .. 65536. */
+int sccsum_set_engine_sync_every(int steps);
 
 /* Flat kernel forms without a chunk in flight (U 8 form 14, U 16): a run's
  * last chunk loads and scans only the rows its units reach, U / 8 .. U (1, the

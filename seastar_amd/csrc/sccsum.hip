@@ -1048,6 +1048,7 @@ constexpr uint32_t kStepSum = 0;        // checksums into out / status (sccsum_e
 constexpr uint32_t kStepFillGen = 1;    // fill, generate half: values into out2, status; frames untouched
 constexpr uint32_t kStepFillStore = 2;  // fill, store half: out2's values into the frames' fields
 constexpr uint32_t kStoreTilePackets = 256;  // store tiles: 4 frames per lane
+constexpr uint32_t kEngineSyncEvery = 10;    // big steps: every 10th waits for the one before it
 // Store tiles write each field through (sc0 sc1).  Stored plain (the L2
 // merging a frame's two fields) with one system-scope release per wave at the
 // step's flush instead, a fill step took 408 us against 328 (the releases'
@@ -2311,6 +2312,8 @@ struct Knobs {
     int run_align = kRunAlign;       // flat kernel: run extents start on 1 / 4 / 8-unit (16 / 64 / 128 B) boundaries
     int engine_wt = 1;               // engine: results written through (1) or stored as a launch stores them (0)
     int engine_idle_ms = 1000;       // engine: a run given no new step for this long gives up (SCCSUM_EIDLE)
+    int engine_sync_every = -1;      // engine: every k-th step waits for the step before it (0 = never,
+                                     // -1 = every kEngineSyncEvery steps of >= 2 tiles per wave)
 };
 thread_local Knobs t_knobs;
 
@@ -3113,6 +3116,16 @@ uint64_t engine_put(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbat
     for (uint32_t q = 0; q <= SCCSUM_ENGINE_MAX_BATCHES; ++q) d[sccsum::kEdTile0 + q] = tile0[q];
     d[sccsum::kEdKind] = kind;
     d[sccsum::kEdDep] = dep;
+    // Re-synchronise the grid every k steps: the step's tiles wait for the one
+    // before it, so dequeue groups that drifted apart line up again.  A grid
+    // of fixed groups drifts over a long run: cfg 2's
+    // 200-step run took 457-458 us per step unsynchronised, 448-449 with a
+    // barrier every 10 steps, 456 with one every step, and launches 461
+    // (profiles/r05_engine_sync.log).  By default only big steps (>= 2 tiles
+    // per wave) synchronise; a stream of small steps keeps its pipeline full.
+    int sync = sccsum::t_knobs.engine_sync_every;
+    if (sync < 0) sync = ntiles >= 2 * e->waves ? static_cast<int>(sccsum::kEngineSyncEvery) : 0;
+    if (dep == 0 && sync > 0 && s > 0 && s % static_cast<uint64_t>(sync) == 0) d[sccsum::kEdDep] = s;
     if (ntiles == 0) {  // nothing to sum: done at once (the descriptor still keeps the walk in order)
         __atomic_store_n(e->ctl_h + sccsum::kEcDone + 8u * s, s + 1, __ATOMIC_RELEASE);
     }
@@ -3591,6 +3604,12 @@ int sccsum_set_out_policy(int policy) {
 
 int sccsum_set_engine_write_through(int on) {
     sccsum::t_knobs.engine_wt = on ? 1 : 0;
+    return SCCSUM_OK;
+}
+
+int sccsum_set_engine_sync_every(int steps) {
+    if (steps < -1 || steps > 65536) return SCCSUM_EINVAL;
+    sccsum::t_knobs.engine_sync_every = steps;
     return SCCSUM_OK;
 }
 

@@ -105,6 +105,7 @@ _PROTOS = {
     "sccsum_engine_submit": (ctypes.c_int, [_vp, _vp, _u32, _u32, _u64, ctypes.POINTER(_u64)]),
     "sccsum_engine_submit_fill": (ctypes.c_int, [_vp, _vp, _u32, _u32, _u64, ctypes.POINTER(_u64)]),
     "sccsum_set_engine_idle_ms": (ctypes.c_int, [ctypes.c_int]),
+    "sccsum_set_engine_sync_every": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_engine_wait": (ctypes.c_int, [_vp, _u64, _u64]),
     "sccsum_engine_stop": (ctypes.c_int, [_vp]),
     "sccsum_engine_destroy": (ctypes.c_int, [_vp]),

@@ -127,6 +127,9 @@ static void checks() {
     EXPECT(sccsum_set_engine_write_through(0) == SCCSUM_OK && sccsum_set_engine_write_through(1) == SCCSUM_OK);
     EXPECT(sccsum_set_engine_idle_ms(0) == SCCSUM_EINVAL && sccsum_set_engine_idle_ms(3600001) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_engine_idle_ms(250) == SCCSUM_OK && sccsum_set_engine_idle_ms(1000) == SCCSUM_OK);
+    EXPECT(sccsum_set_engine_sync_every(-2) == SCCSUM_EINVAL && sccsum_set_engine_sync_every(65537) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_engine_sync_every(20) == SCCSUM_OK && sccsum_set_engine_sync_every(0) == SCCSUM_OK);
+    EXPECT(sccsum_set_engine_sync_every(-1) == SCCSUM_OK);
     // host pipeline
     sccsum_pipeline* p = nullptr;
     EXPECT(sccsum_pipeline_create(0, 1 << 20, 1024, 0, &p) == SCCSUM_EINVAL);
