@@ -1433,7 +1433,11 @@ __device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {
             __hip_atomic_store(reinterpret_cast<uint16_t*>(p), static_cast<uint16_t>(v), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         } else {
+#ifdef SCCSUM_AB_FILLSTORE_NT
+            __builtin_nontemporal_store(static_cast<uint16_t>(v), reinterpret_cast<uint16_t*>(p));
+#else
             *gst(reinterpret_cast<uint16_t*>(p)) = static_cast<uint16_t>(v);
+#endif
         }
     } else if constexpr (kWriteThrough) {
         __hip_atomic_store(p, static_cast<uint8_t>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2132,7 +2136,11 @@ __global__ __launch_bounds__(kBlock) void fill_store_kernel(uint8_t* __restrict_
     const uint64_t o = off[i];
     const uint32_t L = len[i];
     if (o > bytes_len || L > bytes_len - o || L < 20u) return;
+#ifdef SCCSUM_AB_FILLSTORE_LAUNCH_WT
+    fill_apply<false, true>(bytes + o, L, fill_load<false>(bytes + o, words + i), mode);
+#else
     fill_apply<false>(bytes + o, L, fill_load<false>(bytes + o, words + i), mode);
+#endif
 }
 
 // Header-only generate (no payload bytes read): the IPv4 header checksum
