@@ -624,3 +624,55 @@ def test_engine_fill_stress_small_steps(dev, in_flight):
     for vb, vout, want in verifies:
         assert np.array_equal(batch.as_u16(vout).reshape(-1, 2), want)
     eng.close()
+
+
+@pytest.mark.parametrize("sync_every", [1, 3, 0])
+def test_engine_barrier_period(dev, sync_every):
+    """The grid's barrier (a step that waits for the one before it,
+    sccsum_set_engine_sync_every; by default every 10 big steps): with a
+    barrier on every step, every third step, or none, 60 steps of mixed frame
+    batches and fills, 16 in flight, give the oracle's results.  Every step
+    waiting on the one before is the dependency path's worst case: each wave
+    parks on a step its neighbours have not finished."""
+    from test_gpu_parity import _tx_frames
+
+    lib = native.load()
+    rng = np.random.default_rng(0xEC + sync_every)
+    m = native.FILL_IP | native.FILL_L4
+    steps = []
+    for k in range(60):
+        if k % 4 == 3:
+            buf, off, length = _tx_frames(rng, int(rng.integers(1, 300)))
+            b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+            out2 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+            steps.append(("fill", b, out2, oracle.batch_ipv4_fill(buf, off, length, m)))
+        else:
+            b, want, want_st = _frames_step(rng, dev, int(rng.integers(0, 3)))
+            out = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+            st = torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev)
+            steps.append(("frames", b, (out, st), (want, want_st)))
+    torch.cuda.synchronize()
+    native.check(lib.sccsum_set_engine_sync_every(sync_every), "sync_every")
+    try:
+        eng = batch.Engine(0, frames=True, fill=True, max_steps=128, max_in_flight=16)
+        stream = torch.cuda.Stream(device=dev)
+        eng.start(stream)
+        last = 0
+        for kind, b, out, _ in steps:
+            if kind == "fill":
+                last = max(last, eng.submit_fill([(b, out, None)], m))
+            else:
+                last = max(last, eng.submit([(b, out[0], out[1])]))
+        eng.wait(last)
+        eng.stop()
+        stream.synchronize()
+    finally:
+        lib.sccsum_set_engine_sync_every(-1)
+    for kind, b, out, want in steps:
+        if kind == "fill":
+            assert np.array_equal(b.data.cpu().numpy()[: b.bytes_len], want[0])
+            assert np.array_equal(batch.as_u16(out).reshape(-1, 2), want[1])
+        else:
+            assert np.array_equal(batch.as_u16(out[0]).reshape(-1, 2), want[0])
+            assert np.array_equal(out[1].cpu().numpy(), want[1])
+    eng.close()
