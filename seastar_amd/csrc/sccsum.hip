@@ -3000,6 +3000,7 @@ struct sccsum_engine {
     bool running = false, launched = false, left_recorded = false;
     uint64_t waves = 0;          // the running grid's waves (tile sizing)
     uint64_t next_step = 0, next_first = 0;
+    uint64_t done_floor = 0;     // every step below it is known done (engine_room)
 };
 
 namespace {
@@ -3064,13 +3065,24 @@ int engine_check(const sccsum_engine* e, const sccsum_batch* batches, uint32_t n
     return SCCSUM_OK;
 }
 
-// Room to publish k more steps now: pacing by max_in_flight (waits for the
-// step max_in_flight before the last of them), max_steps, a live grid.
+// Room to publish k more steps now: pacing by max_in_flight, max_steps, a
+// live grid.  Every step up to max_in_flight before the last of them must be
+// done, not only that one: steps can finish out of order (a small step behind
+// a big one's last tile), and a step's completion counters and done word are
+// slot step % kEngineCountSlots, which the step kEngineCountSlots later takes
+// over (max_in_flight <= kEngineCountSlots).  The caller may also free an
+// older step's buffers once a later submit returns.
 int engine_room(sccsum_engine* e, uint32_t k, uint64_t timeout_ns) {
     if (__atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE)) return SCCSUM_EIDLE;
     const uint64_t last = e->next_step + k - 1;
     if (last >= e->max_steps) return SCCSUM_EBUSY;  // the run's descriptors are used up: stop, start again
-    if (last >= e->max_in_flight) return engine_wait_done(e, last - e->max_in_flight, timeout_ns);
+    if (last < e->max_in_flight) return SCCSUM_OK;
+    const uint64_t target = last - e->max_in_flight, t0 = now_ns();
+    for (; e->done_floor <= target; ++e->done_floor) {
+        const uint64_t spent = now_ns() - t0;
+        const int rc = engine_wait_done(e, e->done_floor, spent < timeout_ns ? timeout_ns - spent : 0);
+        if (rc != SCCSUM_OK) return rc;
+    }
     return SCCSUM_OK;
 }
 
@@ -3268,6 +3280,7 @@ int sccsum_engine_start(sccsum_engine* e, void* stream) {
     e->running = true;
     e->next_step = 0;
     e->next_first = 0;
+    e->done_floor = 0;
     return SCCSUM_OK;
 }
 

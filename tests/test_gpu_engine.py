@@ -676,3 +676,55 @@ def test_engine_barrier_period(dev, sync_every):
             assert np.array_equal(batch.as_u16(out[0]).reshape(-1, 2), want[0])
             assert np.array_equal(out[1].cpu().numpy(), want[1])
     eng.close()
+
+
+
+def test_engine_pacing_counts_every_older_step(dev):
+    """Steps finish out of order: tiny steps behind a big one (2 M frames,
+    ~0.5 ms) finish long before it.  Pacing must still hold every step up to
+    max_in_flight before the newest one done when a submit returns — the
+    header's "at most max_in_flight submitted and not yet done", which the
+    caller relies on to free an older step's buffers, and which keeps a
+    step's completion slot (step % 64) from being taken over while the step
+    still counts.  A fill publishes two steps at once; pacing that waited on
+    only the step max_in_flight before the newest skipped the one before
+    that, here the big step."""
+    from seastar_amd import devsynth
+    from test_gpu_parity import _tx_frames
+
+    lib = native.load()
+    rng = np.random.default_rng(0xED)
+    big = devsynth.udp_frames(2 << 20, 1500, seed=77, device=dev)
+    big_st = torch.empty(big.n, dtype=torch.uint8, device=dev)
+    buf, off, length = _tx_frames(rng, 40)
+    m = native.FILL_IP | native.FILL_L4
+    want = oracle.batch_ipv4_fill(buf, off, length, m)
+    fills = []
+    for k in range(12):
+        b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+        fills.append((b, torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)))
+    tiny = batch.PacketBatch.from_host(buf, off, length, device=dev)
+    tiny_st = torch.empty(tiny.n, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, fill=True, max_steps=64, max_in_flight=2)
+    stream = torch.cuda.Stream(device=dev)
+    late = []
+    for rep in range(3):
+        eng.start(stream)
+        eng.submit([(big, None, big_st)])  # step 0
+        eng.submit([(tiny, None, tiny_st)])  # step 1
+        floor = 0  # every step below it was seen done
+        for b, out2 in fills:
+            s = eng.submit_fill([(b, out2, None)], m)  # steps s - 1 (generate) and s (store)
+            while floor < s and lib.sccsum_engine_wait(eng._h, floor, 0) == native.SCCSUM_OK:
+                floor += 1
+            if floor < s + 1 - eng.max_in_flight:
+                late.append((rep, s, floor))
+        eng.wait(s)
+        eng.stop()
+        stream.synchronize()
+    assert not late, f"(run, store step submitted, first step not done): {late[:8]}"
+    for b, out2 in fills:
+        assert np.array_equal(b.data.cpu().numpy()[: b.bytes_len], want[0])
+        assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want[1])
+    eng.close()
