@@ -234,10 +234,11 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  *       publish one step; waits (spinning, up to timeout_ns) while
  *       max_in_flight steps are pending.  SCCSUM_EBUSY: the run already took
  *       max_steps steps (stop and start a new run) or the wait timed out.
- *       max_len is taken for symmetry with the _multi calls and not used:
- *       the engine always runs the flat kernel, so sparse layouts give exact
- *       results but belong on the launches, whose row kernel reads them
- *       faster.  Frames take no seeds.
+ *       max_len (0 = unknown) caps the mean packet length the step's tiles
+ *       are sized by (bytes_len / n otherwise, too big for a batch that is a
+ *       slice of a larger buffer).  The engine always runs the flat kernel, so
+ *       sparse layouts give exact results but belong on the launches, whose
+ *       row kernel reads them faster.  Frames take no seeds.
  *   sccsum_engine_submit_fill(e, batches, nbatch, mode, timeout_ns, &step)
  *       an in-place fill (sccsum_ipv4_fill's SCCSUM_FILL_L4 and/or
  *       SCCSUM_FILL_ICMP_ECHO, optionally | SCCSUM_FILL_IP) of every batch,

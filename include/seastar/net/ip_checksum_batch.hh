@@ -255,9 +255,11 @@ public:
         check(rc, "sccsum_engine_start");
         return true;
     }
-    uint64_t submit(const sccsum_batch* batches, uint32_t nbatch, uint64_t timeout_ns = 1'000'000'000) {
+    // max_len: the longest packet, if known (sizes the step's tiles; 0 = from bytes_len / n)
+    uint64_t submit(const sccsum_batch* batches, uint32_t nbatch, uint64_t timeout_ns = 1'000'000'000,
+                    uint32_t max_len = 0) {
         uint64_t step = 0;
-        check(sccsum_engine_submit(_e, batches, nbatch, 0, timeout_ns, &step), "sccsum_engine_submit");
+        check(sccsum_engine_submit(_e, batches, nbatch, max_len, timeout_ns, &step), "sccsum_engine_submit");
         return step;
     }
     // in-place fill of every batch (d_out: the values, required); the step returned is done once

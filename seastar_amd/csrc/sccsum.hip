@@ -1239,7 +1239,11 @@ struct EngineSrc {
                                                       __HIP_MEMORY_SCOPE_SYSTEM);
                     return false;
                 }
+#ifdef SCCSUM_AB_DEP_SLEEP
+                __builtin_amdgcn_s_sleep(SCCSUM_AB_DEP_SLEEP);
+#else
                 __builtin_amdgcn_s_sleep(32);  // ~0.9 us: a dependency ends with a step's last tiles
+#endif
                 continue;
             }
             if (stop) return false;  // stopped, and v lies past every published step
@@ -3089,26 +3093,36 @@ int engine_room(sccsum_engine* e, uint32_t k, uint64_t timeout_ns) {
 // Write one step's descriptor over checked batches (nbatch 0: an empty step,
 // done at once) and publish it; engine_room made the room.  kind = the
 // descriptor's kind word, dep = 0 or 1 + the step its tiles wait for.
-uint64_t engine_put(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint64_t kind, uint64_t dep) {
+// Packets per tile of a summing step, as a launch picks them (launch_flat):
+// about tile_bytes of packets, at most 64, and no fewer tiles than the grid
+// has waves.  The mean packet is the batches' bytes over their packets, capped
+// by max_len when the caller gives it: a batch that is a slice of a larger
+// buffer (bytes_len covers the whole buffer) would otherwise look sparse and
+// get tiles of a packet or two.
+uint64_t engine_tile(const sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len) {
     uint64_t n_total = 0, bytes_total = 0;
     for (uint32_t i = 0; i < nbatch; ++i) {
         n_total += batches[i].n;
         bytes_total += batches[i].n ? batches[i].bytes_len : 0;
     }
-    uint64_t B = sccsum::kStoreTilePackets;  // store tiles: four frames per lane
-    if ((kind & 0xffu) != sccsum::kStepFillStore) {
-        // tile size as a launch would pick it (launch_flat): ~tile_bytes of packets, at most 64
-        const sccsum::Knobs& K = sccsum::t_knobs;
-        uint64_t bmax = static_cast<uint64_t>(K.tile_packets);
-        if (K.tile_bytes && n_total) {
-            const uint64_t mean = bytes_total / n_total ? bytes_total / n_total : 1;
-            const uint64_t tb = static_cast<uint64_t>(K.tile_bytes);
-            const uint64_t bb = tb / mean ? tb / mean : 1;
-            bmax = bb < bmax ? bb : bmax;
-        }
-        B = e->waves ? (n_total + e->waves - 1) / e->waves : 1;
-        B = B < 1 ? 1 : (B > bmax ? bmax : B);
+    const sccsum::Knobs& K = sccsum::t_knobs;
+    uint64_t bmax = static_cast<uint64_t>(K.tile_packets);
+    if (K.tile_bytes && n_total) {
+        uint64_t mean = bytes_total / n_total ? bytes_total / n_total : 1;
+        if (max_len && mean > max_len) mean = max_len;
+        const uint64_t tb = static_cast<uint64_t>(K.tile_bytes);
+        const uint64_t bb = tb / mean ? tb / mean : 1;
+        bmax = bb < bmax ? bb : bmax;
     }
+    uint64_t B = e->waves ? (n_total + e->waves - 1) / e->waves : 1;
+    return B < 1 ? 1 : (B > bmax ? bmax : B);
+}
+
+// B: packets per tile of a summing step (engine_tile); a store step's tiles
+// always hold kStoreTilePackets frames.
+uint64_t engine_put(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint64_t kind, uint64_t dep,
+                    uint64_t B) {
+    if ((kind & 0xffu) == sccsum::kStepFillStore) B = sccsum::kStoreTilePackets;  // four frames per lane
     const uint64_t s = e->next_step;
     uint64_t* const d = e->ring_h + s * sccsum::kEngineSlotWords;
     uint64_t tile0[SCCSUM_ENGINE_MAX_BATCHES + 1] = {};
@@ -3286,11 +3300,10 @@ int sccsum_engine_start(sccsum_engine* e, void* stream) {
 
 int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
                          uint64_t timeout_ns, uint64_t* step) {
-    (void)max_len;
     if (!e || !e->running || !step) return SCCSUM_EINVAL;
     if (const int rc = engine_check(e, batches, nbatch, false); rc != SCCSUM_OK) return rc;
     if (const int rc = engine_room(e, 1, timeout_ns); rc != SCCSUM_OK) return rc;
-    *step = engine_put(e, batches, nbatch, sccsum::kStepSum, 0);
+    *step = engine_put(e, batches, nbatch, sccsum::kStepSum, 0, engine_tile(e, batches, nbatch, max_len));
     return SCCSUM_OK;
 }
 
@@ -3315,14 +3328,15 @@ int sccsum_engine_submit_fill(sccsum_engine* e, const sccsum_batch* batches, uin
     const uint64_t kflags = ((mode & SCCSUM_FILL_L4) ? sccsum::kFlagFillL4 : 0u) |
                             ((mode & SCCSUM_FILL_ICMP_ECHO) ? sccsum::kFlagFillIcmp : 0u) |
                             ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u);
-    const uint64_t gen = engine_put(e, batches, nbatch, sccsum::kStepFillGen | (kflags << 8) | (uint64_t(mode) << 16), 0);
+    const uint64_t gen = engine_put(e, batches, nbatch, sccsum::kStepFillGen | (kflags << 8) | (uint64_t(mode) << 16),
+                                    0, engine_tile(e, batches, nbatch, 0));
     // the store half: no status (the generate half reported it)
     sccsum_batch st[SCCSUM_ENGINE_MAX_BATCHES];
     for (uint32_t i = 0; i < nbatch; ++i) {
         st[i] = batches[i];
         st[i].d_status = nullptr;
     }
-    *step = engine_put(e, st, nbatch, sccsum::kStepFillStore | (uint64_t(mode) << 16), gen + 1);
+    *step = engine_put(e, st, nbatch, sccsum::kStepFillStore | (uint64_t(mode) << 16), gen + 1, 0);
     return SCCSUM_OK;
 }
 

@@ -728,3 +728,48 @@ def test_engine_pacing_counts_every_older_step(dev):
         assert np.array_equal(b.data.cpu().numpy()[: b.bytes_len], want[0])
         assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want[1])
     eng.close()
+
+
+def test_engine_slices_of_one_buffer_with_max_len(dev):
+    """Steps that are slices of one large buffer (a shard's rx ring: each
+    step's off/len/out arrays point into the whole ring's, bytes_len covers
+    the ring): with max_len the engine sizes the tiles by max_len (32 frames
+    of 1500 B), not by bytes_len / n (a slice of 1/64 of the ring looked like
+    96 KB packets: tiles of a frame or two).  Every slice exact against the
+    oracle, at max_len 1500 and 0 (unknown)."""
+    import ctypes
+
+    lib = native.load()
+    n_all, L = 1 << 16, 1500
+    buf, off, lens, _ = synth.udp_ipv4_frames(n_all, L, seed=31)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
+    b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+    out = torch.full((2 * n_all,), -1, dtype=torch.int16, device=dev)
+    st = torch.full((n_all,), 0xEE, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, max_steps=256, max_in_flight=8)
+    stream = torch.cuda.Stream(device=dev)
+    sizes = [1024, 4096, 16384, 1, 33]
+    for max_len in (L, 0):
+        eng.start(stream)
+        lo, k, last = 0, 0, 0
+        while lo < n_all:
+            m = min(sizes[k % len(sizes)], n_all - lo)
+            arr = (native.Batch * 1)()
+            arr[0] = native.Batch(b.data.data_ptr(), b.bytes_len, b.off.data_ptr() + 8 * lo,
+                                  b.length.data_ptr() + 4 * lo, None, out.data_ptr() + 4 * lo,
+                                  st.data_ptr() + lo, m)
+            step = ctypes.c_uint64()
+            native.check(lib.sccsum_engine_submit(eng._h, ctypes.cast(arr, ctypes.c_void_p), 1, max_len, 10**10,
+                                                  ctypes.byref(step)), "submit")
+            last = step.value
+            lo, k = lo + m, k + 1
+        eng.wait(last)
+        eng.stop()
+        stream.synchronize()
+        assert np.array_equal(batch.as_u16(out).reshape(-1, 2), want)
+        assert np.array_equal(st.cpu().numpy(), want_st)
+        out.fill_(-1)
+        st.fill_(0xEE)
+        torch.cuda.synchronize()
+    eng.close()
