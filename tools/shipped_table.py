@@ -62,7 +62,10 @@ def main():
     print("|---|---|---|---|---|---|---|" + ("" if len(dirs) == 1 else "---|"))
     names = sorted(first, key=lambda n: ORDER.index(n) if n in ORDER else 99)
     for n in names:
-        cfg = n.replace("headline", "udp1500")
+        # the headline's profile: the driver's form profiled as prof:udp1500+--steps+200+--warmup+5
+        # where the session has it, else the 10-step udp1500 profile
+        cfg = n if n != "headline" else ("udp1500_steps_200_warmup_5" if "udp1500_steps_200_warmup_5" in pm
+                                         else "udp1500")
         line = row(n, first[n], pm.get(cfg))
         if len(dirs) > 1:
             others = [lines(x).get(n, {}).get("roofline", {}) or {} for x in dirs[1:]]
