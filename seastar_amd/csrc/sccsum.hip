@@ -1424,8 +1424,8 @@ struct EngineSrc {
 // (sc0 sc1), so the host may copy the frames out once the step reports.
 template <bool kCoherent>
 __device__ __forceinline__ uint32_t fill_ld32(const uint32_t* q) {
-    if constexpr (kCoherent) {
-        return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (kCoherent) {  // (a global-space pointer: global_load, not flat_load, which also counts lgkm)
+        return __hip_atomic_load(gld(q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
         return *gld(q);
     }
@@ -1434,7 +1434,7 @@ template <bool kWriteThrough>
 __device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {
     if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0u) {
         if constexpr (kWriteThrough) {
-            __hip_atomic_store(reinterpret_cast<uint16_t*>(p), static_cast<uint16_t>(v), __ATOMIC_RELAXED,
+            __hip_atomic_store(gst(reinterpret_cast<uint16_t*>(p)), static_cast<uint16_t>(v), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         } else {
 #ifdef SCCSUM_AB_FILLSTORE_NT
@@ -1444,8 +1444,8 @@ __device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {
 #endif
         }
     } else if constexpr (kWriteThrough) {
-        __hip_atomic_store(p, static_cast<uint8_t>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(p + 1, static_cast<uint8_t>(v >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(gst(p), static_cast<uint8_t>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(gst(p + 1), static_cast<uint8_t>(v >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     } else {
         gst(p)[0] = static_cast<uint8_t>(v);
         gst(p)[1] = static_cast<uint8_t>(v >> 8);
