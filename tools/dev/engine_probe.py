@@ -62,6 +62,10 @@ def main():
     if fn is not None:
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    tl_fn = getattr(lib, "sccsum_ab_timeline", None)  # per-wave start / first data / end / tiles
+    if tl_fn is not None:
+        tl_fn.restype = ctypes.c_int
+        tl_fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     st_fn = getattr(lib, "sccsum_ab_step_times", None)  # per-step group / XCD retire times
     if st_fn is not None:
         st_fn.restype = ctypes.c_int
@@ -94,7 +98,9 @@ def main():
             if st_fn is not None:  # clear the last run's records
                 native.check(st_fn(steps_rec.ctypes.data, steps_rec.nbytes), "sccsum_ab_step_times")
             e0.record(s)
+            t_start = time.perf_counter()
             eng.start(s)
+            start_us = (time.perf_counter() - t_start) * 1e6
             blocked, ret = [], []
             for k in range(K):
                 t0 = time.perf_counter()
@@ -115,6 +121,7 @@ def main():
         d = {"frames_per_batch": n, "steps": K, "in_flight": in_flight,
              "run_us": round(e0.elapsed_time(e1) * 1e3, 1),
              "us_per_step": round(e0.elapsed_time(e1) * 1e3 / K, 1),
+             "host_start_call_us": round(start_us, 1),
              "host_blocked_us_mean": round(float(np.mean(blocked)) * 1e6, 1),
              "host_blocked_us_max": round(float(np.max(blocked)) * 1e6, 1),
              "step_us_by_tenth_of_run": q,
@@ -136,6 +143,26 @@ def main():
                 "host_polls_total": int(w[:, 7].sum())})
         if st_fn is not None:
             d.update(step_spread(steps_rec, min(K, 1024)))
+        if tl_fn is not None and st_fn is not None:  # where a run's fixed cost goes
+            tl = np.zeros((16384, 4), dtype=np.uint64)
+            native.check(tl_fn(tl.ctypes.data, tl.nbytes), "sccsum_ab_timeline")
+            w = tl[tl[:, 0] > 0].astype(np.float64)
+            grp = steps_rec[:1024 * 64].reshape(1024, 64)[:K].astype(np.float64)
+            xcd = steps_rec[1024 * 64:].reshape(1024, 8, 2)[:K]
+            k_start = w[:, 0].min()
+            first_retire0 = (~xcd[0, :, 1]).astype(np.float64).min()
+            last_done = grp[K - 1].max()
+            fd = w[w[:, 1] > 0, 1]
+            d["run_phases_us"] = {
+                "waves_started_over": round((w[:, 0].max() - k_start) * TICK_US, 1),
+                "kernel_start_to_first_data_median": round((np.median(fd) - k_start) * TICK_US, 1),
+                "kernel_start_to_first_data_min": round((fd.min() - k_start) * TICK_US, 1),
+                "kernel_start_to_step0_first_retire": round((first_retire0 - k_start) * TICK_US, 1),
+                "step0_done": round((grp[0].max() - k_start) * TICK_US, 1),
+                "last_step_done": round((last_done - k_start) * TICK_US, 1),
+                "last_step_done_to_last_wave_end": round((w[:, 2].max() - last_done) * TICK_US, 1),
+                "kernel_span": round((w[:, 2].max() - k_start) * TICK_US, 1),
+                "events_minus_kernel_span": round(e0.elapsed_time(e1) * 1e3 - (w[:, 2].max() - k_start) * TICK_US, 1)}
         print(json.dumps(d), flush=True)
         eng.close()
         del txs, rxs
