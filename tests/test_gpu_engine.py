@@ -773,3 +773,44 @@ def test_engine_slices_of_one_buffer_with_max_len(dev):
         st.fill_(0xEE)
         torch.cuda.synchronize()
     eng.close()
+
+
+def test_engine_run_of_max_steps(dev):
+    """One run of the most steps a run takes (65 536): every step a batch of
+    1-3 frames (a tiny step: most waves claim past the published tiles and
+    wait), results into a rotating set of outputs; the 65 537th submit is
+    SCCSUM_EBUSY; the last outputs of every slot equal the oracle.  Covers the
+    step-indexed words at their limit (done words, descriptor ring, the 64
+    completion slots wrapping 1 024 times)."""
+    import ctypes
+
+    lib = native.load()
+    buf, off, lens, _ = synth.udp_ipv4_frames(3, 600, seed=41)
+    want, _ = oracle.batch_ipv4(buf, off, lens)
+    b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+    slots = 64
+    outs = torch.full((slots, 6), -1, dtype=torch.int16, device=dev)
+    torch.cuda.synchronize()
+    max_steps = 65536
+    eng = batch.Engine(0, frames=True, max_steps=max_steps, max_in_flight=32)
+    stream = torch.cuda.Stream(device=dev)
+    eng.start(stream)
+    arr = (native.Batch * 1)()
+    step = ctypes.c_uint64()
+    for k in range(max_steps):
+        n = 1 + k % 3
+        arr[0] = native.Batch(b.data.data_ptr(), b.bytes_len, b.off.data_ptr(), b.length.data_ptr(), None,
+                              outs[k % slots].data_ptr(), None, n)
+        rc = lib.sccsum_engine_submit(eng._h, ctypes.cast(arr, ctypes.c_void_p), 1, 600, 10**10, ctypes.byref(step))
+        assert rc == native.SCCSUM_OK, (k, rc)
+    assert step.value == max_steps - 1
+    assert lib.sccsum_engine_submit(eng._h, ctypes.cast(arr, ctypes.c_void_p), 1, 600, 10**9,
+                                    ctypes.byref(step)) == native.SCCSUM_EBUSY
+    eng.wait(max_steps - 1)
+    eng.stop()
+    stream.synchronize()
+    got = batch.as_u16(outs).reshape(slots, 3, 2)
+    for s in range(slots):
+        n = 1 + (max_steps - slots + s) % 3  # the slot's last step's frame count
+        assert np.array_equal(got[s, :n], want[:n]), s
+    eng.close()
