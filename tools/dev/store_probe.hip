@@ -17,11 +17,14 @@
 //   rdH16/64  the read pass with the units over each frame's first 16 / 64 bytes loaded default-policy
 //             (the rest nt), so the heads may still be cached when a store pass follows; rdD: every unit
 //             default-policy
-// usage: store_probe [reps] [set: 1 = the side-buffer set only, 2 = the fill-floor set]
+//   rdbar+... register stash + grid barrier + whole-line drain (set 3, round 5; see k_rdbar)
+// usage: store_probe [reps] [set: 1 = the side-buffer set only, 2 = the fill-floor set,
+//                           3 = the register-stash / grid-barrier set (round 5)]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #define CK(x)                                                                              \
@@ -346,6 +349,139 @@ __global__ __launch_bounds__(256) void k_rdhead(const uint8_t* buf, uint64_t n, 
     if (acc == 0x12345u) sink[0] = acc;
 }
 
+// Round 5: register stash + grid barrier + whole-line drain.  Every wave streams
+// its TPW tiles of 64 frames (nt), keeps each frame's aligned 64-B head line
+// (holding frame+10) in registers, then all waves meet at a grid barrier
+// (one counter, system-scope polls, 400 us limit) and only then write the
+// head lines back WHOLE: full-line writes need no read-modify-write in HBM and
+// none of them lands inside the read stream.
+// MODE 0 = barrier only (no stores), 1 = barrier then 2-byte field stores,
+// 2 = barrier then whole lines (stash reloaded default-policy after each tile),
+// 3 = barrier then whole lines from register values (no reload: pure write
+// cost), 4 = no barrier, whole reloaded lines after the wave's own stream,
+// 5 = as 2 but the stash is cut out of the streamed registers' lanes through
+// LDS instead of reloaded (the product's form: no extra read).
+constexpr int kTpw = 4;
+#ifndef POLL_SLEEP
+#define POLL_SLEEP 127
+#endif
+__device__ __forceinline__ uint64_t probe_clock() { return static_cast<uint64_t>(wall_clock64()); }
+__device__ uint64_t g_trace[4096 * 3];  // per wave: start, arrival, leave (100 MHz), last launch
+template <int MODE>
+__global__ __launch_bounds__(256) void k_rdbar(uint8_t* buf, uint64_t n, uint64_t* bar, uint64_t target,
+                                               uint64_t* sink) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t t_start = probe_clock();
+    const uint64_t wave = (uint64_t(blockIdx.x) * 256 + threadIdx.x) >> 6;
+    const uint64_t nw = uint64_t(gridDim.x) * 4;
+    const uint64_t tiles = n / 64;
+    __shared__ u32x4 lds[4][64 * 4];
+    u32x4* my = lds[threadIdx.x >> 6];
+    uint32_t acc = 0;
+    u32x4 stash[kTpw][4];
+#pragma unroll
+    for (int j = 0; j < kTpw; ++j) {
+        const uint64_t t = wave + uint64_t(j) * nw;
+        if (t >= tiles) break;
+        const uint64_t tb = reinterpret_cast<uint64_t>(buf) + t * 64 * kFrame;
+        const u32x4* base = reinterpret_cast<const u32x4*>(tb);
+        constexpr uint32_t units = 64 * kFrame / 16;  // 6000
+        for (uint32_t u = lane; u < units; u += 64 * 8) {
+            u32x4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t uu = u + 64 * k;
+                v[k] = uu < units ? __builtin_nontemporal_load(base + uu) : u32x4{0, 0, 0, 0};
+            }
+            if (MODE == 5) {
+                // units inside some frame's head line go to that frame's LDS slot
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t uu = u + 64 * k;
+                    if (uu < units) {
+                        const uint64_t a = tb + uint64_t(uu) * 16;
+                        const uint64_t rel = a - tb;
+                        const uint32_t fr = uint32_t(rel / kFrame);
+                        const uint64_t hl = (tb + uint64_t(fr) * kFrame + 10) & ~63ull;
+                        if (a >= hl && a < hl + 64) my[fr * 4 + uint32_t((a - hl) >> 4)] = v[k];
+                        if (fr + 1 < 64) {  // a unit may also sit in the next frame's head line
+                            const uint64_t hn = (tb + uint64_t(fr + 1) * kFrame + 10) & ~63ull;
+                            if (a >= hn && a < hn + 64) my[(fr + 1) * 4 + uint32_t((a - hn) >> 4)] = v[k];
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
+        }
+        const uint64_t f = tb + uint64_t(lane) * kFrame;
+        const u32x4* L = reinterpret_cast<const u32x4*>((f + 10) & ~63ull);
+        if (MODE == 2 || MODE == 4) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) stash[j][k] = L[k];
+        } else if (MODE == 5) {
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int k = 0; k < 4; ++k) stash[j][k] = my[lane * 4 + k];
+            __builtin_amdgcn_wave_barrier();
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) stash[j][k] = u32x4{acc, acc + k, acc, acc};
+        }
+        stash[j][0].z ^= acc | 1u;
+    }
+    if (MODE != 4) {
+        // block barrier in hardware, then one poller per block (every ~3.4 us)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            // the block that completes the count publishes the generation to 64 flag lines
+            // (4 352 B apart: different channels); each block polls its own line
+            const uint64_t got = __hip_atomic_fetch_add(bar, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint64_t gen = target / (uint64_t(gridDim.x) * 4);
+            uint64_t* flags = bar + 8;
+            if (got + 4 == target) {
+                for (int i = 0; i < 64; ++i)
+                    __hip_atomic_store(flags + i * 544, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            const uint64_t t0 = probe_clock();
+            uint64_t seen = 0;
+            uint64_t* mine = flags + (blockIdx.x & 63) * 544;
+            while ((seen = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) < gen) {
+                if (probe_clock() - t0 > 40000) {  // 400 us: the grid was not co-resident
+                    __hip_atomic_fetch_add(sink + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (blockIdx.x == 0) { sink[2] = got; sink[3] = seen; sink[4] = target; }
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(POLL_SLEEP);
+            }
+            const uint64_t wv = blockIdx.x;
+            if (wv < 4096) {
+                g_trace[wv * 3] = t_start;
+                g_trace[wv * 3 + 1] = t0;
+                g_trace[wv * 3 + 2] = probe_clock();
+            }
+        }
+        __syncthreads();
+    }
+    if (MODE != 0) {
+#pragma unroll
+        for (int j = 0; j < kTpw; ++j) {
+            const uint64_t t = wave + uint64_t(j) * nw;
+            if (t >= tiles) break;
+            uint8_t* f = buf + (t * 64 + lane) * kFrame;
+            if (MODE == 1) {
+                *reinterpret_cast<uint16_t*>(f + 10) = uint16_t(stash[j][0].z);
+                *reinterpret_cast<uint16_t*>(f + 26) = uint16_t(stash[j][0].z);
+            } else {
+                u32x4* L = reinterpret_cast<u32x4*>((reinterpret_cast<uint64_t>(f) + 10) & ~63ull);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) L[k] = stash[j][k];
+            }
+        }
+    }
+    if (acc == 0x12345u) sink[0] = acc;
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? std::atoi(argv[1]) : 3;
     constexpr int R = 4;
@@ -382,6 +518,67 @@ int main(int argc, char** argv) {
     };
     u32x4* side;
     CK(hipMalloc(&side, kFrames * 64));
+    if (argc > 2 && std::atoi(argv[2]) == 3) {  // register stash + grid barrier + whole-line drain (round 5)
+        uint64_t* bar;
+        CK(hipMalloc(&bar, 64 + 64 * 4352));
+        CK(hipMemset(bar, 0, 64 + 64 * 4352));
+        CK(hipMemset(sink, 0, 64));
+        const unsigned blocks = unsigned(kFrames / 64 / kTpw / 4);  // 4 waves per block, kTpw tiles per wave
+        const uint64_t nwaves = uint64_t(blocks) * 4;
+        uint64_t gen = 0;
+        auto bar_launch = [&](auto kern, uint8_t* b) {
+            ++gen;
+            kern<<<blocks, 256>>>(b, kFrames, bar, gen * nwaves, sink);
+        };
+        std::printf("blocks %u (%.1f per CU), waves %llu\n", blocks, double(blocks) / cus,
+                    (unsigned long long)nwaves);
+        run("rd only", [&](uint8_t* b) { k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+        run("rdbar only", [&](uint8_t* b) { bar_launch(k_rdbar<0>, b); });
+        run("rdbar+st2", [&](uint8_t* b) { bar_launch(k_rdbar<1>, b); });
+        run("rdbar+lineR", [&](uint8_t* b) { bar_launch(k_rdbar<2>, b); });
+        run("rdbar+lineV", [&](uint8_t* b) { bar_launch(k_rdbar<3>, b); });
+        run("rd+lineR", [&](uint8_t* b) { k_rdbar<4><<<blocks, 256>>>(b, kFrames, bar, 0, sink); });
+        run("rdbar+lineL", [&](uint8_t* b) { bar_launch(k_rdbar<5>, b); });
+        run("rd;st2", [&](uint8_t* b) {
+            k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st2<<<g_frames, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rd;st64rw", [&](uint8_t* b) {
+            k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink);
+            k_st64rw<<<g_frames * 4, 256>>>(b, kFrames, 0x1234);
+        });
+        run("rdbar+lineR", [&](uint8_t* b) { bar_launch(k_rdbar<2>, b); });
+        run("rdbar+lineL", [&](uint8_t* b) { bar_launch(k_rdbar<5>, b); });
+        run("rd only", [&](uint8_t* b) { k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink); });
+        {
+            int nb0 = 0, nb5 = 0;
+            CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb0, k_rdbar<0>, 256, 0));
+            CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb5, k_rdbar<5>, 256, 0));
+            std::printf("occupancy blocks/CU: mode0 %d mode5 %d\n", nb0, nb5);
+            std::vector<uint64_t> tr(4096 * 3);
+            CK(hipMemset(sink, 0, 64));
+            bar_launch(k_rdbar<0>, bufs[0]);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpyFromSymbol(tr.data(), HIP_SYMBOL(g_trace), tr.size() * 8));
+            uint64_t s0 = ~0ull, s1 = 0, a0 = ~0ull, a1 = 0, l0 = ~0ull, l1 = 0;
+            for (uint64_t w = 0; w < blocks; ++w) {
+                s0 = std::min(s0, tr[w * 3]); s1 = std::max(s1, tr[w * 3]);
+                a0 = std::min(a0, tr[w * 3 + 1]); a1 = std::max(a1, tr[w * 3 + 1]);
+                l0 = std::min(l0, tr[w * 3 + 2]); l1 = std::max(l1, tr[w * 3 + 2]);
+            }
+            std::printf("mode0 one launch (us from first start): start %.1f..%.1f arrive %.1f..%.1f leave %.1f..%.1f\n",
+                        0.0, (s1 - s0) / 100.0, (a0 - s0) / 100.0, (a1 - s0) / 100.0, (l0 - s0) / 100.0, (l1 - s0) / 100.0);
+            for (uint64_t w = 0; w < blocks; w += 128)
+                std::printf("  block %4llu start %.1f arrive %.1f leave %.1f\n", (unsigned long long)w,
+                            (tr[w * 3] - s0) / 100.0, (tr[w * 3 + 1] - s0) / 100.0, (tr[w * 3 + 2] - s0) / 100.0);
+        }
+        uint64_t h[5];
+        CK(hipMemcpy(h, sink, 40, hipMemcpyDeviceToHost));
+        std::printf("block 0: fetch_add got %llu, last seen %llu, target %llu\n", (unsigned long long)h[2],
+                    (unsigned long long)h[3], (unsigned long long)h[4]);
+        std::printf("barrier time-outs (waves): %llu\n", (unsigned long long)h[1]);
+        return 0;
+    }
     if (argc > 2 && std::atoi(argv[2]) == 2) {  // the fill's floor: does a cached frame head make the store pass cheap?
         const unsigned g4 = g_frames * 4;
         run("rd only", [&](uint8_t* b) { k_rdst<3, false><<<cus * 4, 256>>>(b, kFrames, sink); });
