@@ -346,8 +346,9 @@ int sccsum_ipv4_frames_rss(const void* d_bytes, uint64_t bytes_len, const uint64
  * headers are value-initialised, packet.hh:586-589; ip.cc:270), so the
  * fields' current contents do not matter.  The L4 field is UDP +6 / TCP +16
  * (ICMP +2 with SCCSUM_FILL_ICMP_ECHO) after 4*ihl; other protocols' L4 is
- * left alone, as is any frame that is malformed (as in sccsum_ipv4_frames) or
- * too short to hold the field.  An IP fragment gets the IP header checksum
+ * left alone, as is any frame that is malformed (as in sccsum_ipv4_frames),
+ * too short to hold the field, or whose ihl is below 5 (its L4 header would
+ * overlap the 20-byte IP header; ipv4::send always writes ihl 5, ip.cc:249).  An IP fragment gets the IP header checksum
  * only (ipv4::send checksums each fragment's header, ip.cc:256-278, after the
  * L4 writer summed the whole datagram, ip.cc:283-294): its L4 bytes — the
  * first fragment's L4 header, a later fragment's payload — are never written.

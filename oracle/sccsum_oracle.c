@@ -362,8 +362,10 @@ void oracle_batch_ipv4_fill(uint8_t* bytes, const uint64_t* off, const uint32_t*
             }
             /* L4 writers never touch a fragment: the reference sums the whole
              * datagram before ipv4::send cuts it (udp.cc:184-195 / tcp.hh:1656-1694
-             * run first, ip.cc:283-294 fragments after) */
-            const int atomic = !f.frag && !(st & 4);
+             * run first, ip.cc:283-294 fragments after).  Nor a frame whose ihl is
+             * below 5: its L4 header would overlap the 20-byte IP header, which
+             * no reference writer builds (ipv4::send writes ihl 5, ip.cc:249) */
+            const int atomic = !f.frag && !(st & 4) && f.ihl >= 5;
             uint32_t fo = proto == 17 ? 6 : (proto == 6 ? 16 : 0);
             if ((mode & 6) && fo && atomic && f.l4_len >= fo + 2) {
                 uint8_t* field = p + f.l4_off + fo;

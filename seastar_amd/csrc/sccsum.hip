@@ -1491,9 +1491,9 @@ __device__ __forceinline__ void fill_apply(uint8_t* p, uint32_t L, const FillHea
     const uint32_t proto = hbyte(9);
     const uint32_t l4_off = 4u * ihl;
     const uint32_t l4_end = ip_len < L ? ip_len : L;
-    // as frame_decode: malformed, or an IP fragment -> no L4 write
+    // as frame_decode: malformed, an IP fragment, or ihl < 5 -> no L4 write
     const bool atomic = !(L < ip_len || l4_off > l4_end || (fragw & 0x1fffu) * 8u + l4_end > 65535u ||
-                          (fragw & 0x3fffu) != 0u);
+                          (fragw & 0x3fffu) != 0u || ihl < 5u);
     const uint32_t l4_len = l4_off > l4_end ? 0u : l4_end - l4_off;
     if (mode & SCCSUM_FILL_IP) store_field<kWriteThrough>(p + 10, w);
     if (!atomic) return;
@@ -1953,8 +1953,10 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
                 if (mine) rss.hash[base + lane] = (range_bad || short_frame) ? 0u : hv;  // one queue with RSS
             }
             if (fill_tile) {
-                // L4 writers never touch an IP fragment or a malformed frame
-                const bool atomic = (st & (SCCSUM_ST_MALFORMED | SCCSUM_ST_IPFRAG)) == 0u;
+                // L4 writers never touch an IP fragment, a malformed frame, or a
+                // frame whose ihl is below 5 (its L4 header would overlap the
+                // 20-byte IP header: no reference writer builds one, ip.cc:249)
+                const bool atomic = (st & (SCCSUM_ST_MALFORMED | SCCSUM_ST_IPFRAG)) == 0u && ihl >= 5u;
                 uint32_t fo = 0;
                 if (fill_l4 && (D.proto == 17u || D.proto == 6u)) fo = D.proto == 17u ? 6u : 16u;
                 if (icmp_lane && atomic && l4_len >= 8u) {  // get_header<icmp_hdr>(0): 8 bytes (ip.hh:143-156)
@@ -2185,7 +2187,8 @@ __global__ __launch_bounds__(kBlock) void fill_header_kernel(uint8_t* __restrict
         }
         if (mode & SCCSUM_FILL_L4_PSEUDO) {
             const uint32_t fo = proto == 17u ? 6u : (proto == 6u ? 16u : 0u);
-            if (fo != 0u && l4_len >= fo + 2u && (st & (SCCSUM_ST_MALFORMED | SCCSUM_ST_IPFRAG)) == 0u) {
+            if (fo != 0u && l4_len >= fo + 2u && (st & (SCCSUM_ST_MALFORMED | SCCSUM_ST_IPFRAG)) == 0u &&
+                D.ihl >= 5u) {
                 const uint32_t plen = ((mode & SCCSUM_FILL_TSO) && proto == 6u) ? 0u : l4_len;
                 const uint32_t ps = fold16(static_cast<uint64_t>(h[6]) + h[7] + h[8] + h[9] + (proto << 8) +
                                            swap16(plen & 0xffffu));
