@@ -512,3 +512,104 @@ def test_fuzz_desc(dev, case):
         want = oracle.batch_spans(buf, off, L, seeds)
         assert np.array_equal(batch.as_u16(out), want), f"case {case}"
         assert np.array_equal(st[:n].cpu().numpy(), (want == 0).astype(np.uint8)), f"case {case}"
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_fuzz_burst(dev, case):
+    """The burst queue with random batch limits, depth and delay, spans or
+    frames, copied or zero-copy fragments, every fused form: results in
+    submit order, each the oracle's."""
+    from seastar_amd import pipeline
+    from seastar_amd.burst import BurstQueue
+    from test_gpu_burst import _split
+
+    rng = np.random.default_rng(9000 + case)
+    lib = native.load()
+    frames = case % 2 == 0
+    n = int(rng.choice([1, 200, 1500]))
+    L = np.minimum(_lengths(rng, n, huge=False), 30000).astype(np.uint32)
+    off, total = synth.pack(L, seed=int(rng.integers(1, 2**31)), max_gap=5)
+    host = rng.integers(0, 256, size=max(int(total), 1), dtype=np.uint8)
+    if frames:
+        _ipv4_headers(rng, host, off, L)
+    pinned = pipeline.pinned_empty(host.size)
+    pinned[:] = host
+    seeds = None if frames else rng.integers(0, 65536, n).astype(np.uint32)
+    fused = int(rng.integers(0, 3))
+    native.check(lib.sccsum_set_burst_fused(fused), "burst_fused")
+    q = BurstQueue(native.PIPE_IPV4 if frames else native.PIPE_SPANS,
+                   batch_bytes=int(rng.choice([64 << 10, 256 << 10, 4 << 20])) + int(L.max(initial=0)),
+                   batch_packets=int(rng.choice([1, 7, 32, 128, 1024])),
+                   max_delay_ns=int(rng.choice([0, 50_000, 10**12])), depth=int(rng.choice([1, 2, 4, 8])))
+    mapped_frac = float(rng.choice([0.0, 0.5, 1.0]))
+    try:
+        tickets = []
+        for i in range(n):
+            mapped = bool(rng.random() < mapped_frac)
+            src = pinned if mapped else host
+            pkt = src[int(off[i]):int(off[i]) + int(L[i])]
+            while (t := q.submit(_split(rng, pkt), 0 if seeds is None else int(seeds[i]), mapped=mapped)) is None:
+                q.poll()
+            tickets.append(t)
+            if rng.random() < 0.1:
+                q.poll()
+        q.drain()
+    finally:
+        lib.sccsum_set_burst_fused(2)
+    msg = f"case {case}: n {n}, fused {fused}, mapped {mapped_frac}"
+    assert tickets == list(range(n)), msg
+    if frames:
+        w2, wst = oracle.batch_ipv4(host, off, L)
+        got = np.stack([q.results[t] for t in tickets]) if n else np.zeros((0, 2), np.uint16)
+        st = np.array([q.status[t] for t in tickets], np.uint8)
+        assert np.array_equal(got, w2) and np.array_equal(st, wst), msg
+    else:
+        want = oracle.batch_spans(host, off, L, seeds)
+        got = np.array([int(q.results[t]) for t in tickets], np.uint16)
+        assert np.array_equal(got, want), msg
+    q.close()
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_fuzz_host_pipeline(dev, case):
+    """Host batches through the pipeline with random chunk limits and depth,
+    every gather form, spans or frames, packed or slot-shaped layouts."""
+    from seastar_amd import pipeline
+
+    rng = np.random.default_rng(9500 + case)
+    lib = native.load()
+    frames = case % 2 == 0
+    gather = case % 4
+    n = int(rng.choice([1, 300, 2500]))
+    if rng.random() < 0.5:  # mbuf-slot-shaped: one pitch, odd start, packets up to the pitch
+        pitch = int(rng.choice([640, 2304]))
+        L = rng.integers(0, pitch + 1, n).astype(np.uint32)
+        off = np.arange(n, dtype=np.uint64) * pitch + int(rng.integers(0, 300))
+        total = int(off[-1]) + pitch + 64
+    else:
+        L = np.minimum(_lengths(rng, n, huge=False), 20000).astype(np.uint32)
+        off, total = synth.pack(L, seed=int(rng.integers(1, 2**31)), max_gap=9)
+        total = int(total) + 16
+    host = rng.integers(0, 256, size=total, dtype=np.uint8)
+    if frames:
+        _ipv4_headers(rng, host, off, L)
+    buf = pipeline.pinned_empty(total)
+    buf[:] = host
+    knobs = _knobs(rng, lib)
+    ml = int(L.max(initial=0))
+    pl = pipeline.HostPipeline(0, chunk_bytes=int(rng.choice([2 * ml + 4096, 1 << 20, 64 << 20])),
+                               chunk_packets=int(rng.choice([1, 64, 300, 1 << 16])), depth=int(rng.choice([1, 2, 3, 5])))
+    try:
+        msg = f"case {case}: n {n}, gather {gather}, knobs {knobs}"
+        if frames:
+            got, st = pl.run(native.PIPE_IPV4, buf, off, L, status=True, gather=gather, max_len=ml)
+            w2, wst = oracle.batch_ipv4(host, off, L)
+            assert np.array_equal(got, w2) and np.array_equal(st, wst), msg
+        else:
+            seeds = rng.integers(0, 65536, n).astype(np.uint32)
+            got, st = pl.run(native.PIPE_SPANS, buf, off, L, seeds=seeds, status=True, gather=gather, max_len=ml)
+            want = oracle.batch_spans(host, off, L, seeds)
+            assert np.array_equal(got, want), msg
+            assert np.array_equal(st, (want == 0).astype(np.uint8)), msg
+    finally:
+        pl.close()
