@@ -257,10 +257,17 @@ def test_fuzz_multi(dev, case):
         buf = rng.integers(0, 256, size=max(total, 1), dtype=np.uint8)
         if frames:
             _ipv4_headers(rng, buf, off, L)
-            want = oracle.batch_ipv4(buf, off, L)
+        bad = _range_bad(rng, off, L, total)
+        ok = ~bad
+        if frames:
+            w2, wst = oracle.batch_ipv4(buf, off[ok], L[ok])
+            want = (np.zeros((n, 2), np.uint16), np.full(n, native.ST_RANGE, np.uint8))
+            want[0][ok], want[1][ok] = w2, wst
         else:
             seeds = rng.integers(0, 65536, size=n).astype(np.uint32)
-            want = (oracle.batch_spans(buf, off, L, seeds), seeds)
+            w = np.zeros(n, np.uint16)
+            w[ok] = oracle.batch_spans(buf, off[ok], L[ok], seeds[ok])
+            want = (w, seeds, bad)
         b = batch.PacketBatch.from_host(buf[:total], off, L, device=dev)
         st = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
         out = torch.empty(max((2 if frames else 1) * n, 2), dtype=torch.int16, device=dev)
@@ -285,7 +292,8 @@ def test_fuzz_multi(dev, case):
         else:
             got = batch.as_u16(it[1][:n])
             assert np.array_equal(got, want[0]), msg
-            assert np.array_equal(st, (want[0] == 0).astype(np.uint8)), msg
+            wst = np.where(want[2], native.ST_RANGE, (want[0] == 0).astype(np.uint8))
+            assert np.array_equal(st, wst), msg
 
 
 FILL_MODES = [
@@ -613,3 +621,48 @@ def test_fuzz_host_pipeline(dev, case):
             assert np.array_equal(st, (want == 0).astype(np.uint8)), msg
     finally:
         pl.close()
+
+
+@pytest.mark.parametrize("case", range(3))
+def test_fuzz_engine_spans(dev, case):
+    """A spans engine (SCCSUM_PIPE_SPANS): random steps of 1..4 seeded span
+    batches, out-of-range entries included, every result the oracle's."""
+    rng = np.random.default_rng(9900 + case)
+    lib = native.load()
+    knobs = _knobs(rng, lib, fill=True)
+    plan = []
+    for _ in range(int(rng.integers(5, 30))):
+        items, wants = [], []
+        for _ in range(int(rng.integers(1, native.ENGINE_MAX_BATCHES + 1))):
+            n = int(rng.choice([0, 1, 64, 65, 500, 3000]))
+            L = _lengths(rng, n, huge=case == 0)
+            off, total, kind = _layout(rng, L)
+            if kind == "shuffled":
+                off, L = _shuffle_pairs(rng, off, L)
+            buf = rng.integers(0, 256, size=max(total, 1), dtype=np.uint8)
+            bad = _range_bad(rng, off, L, total)
+            seeds = rng.integers(0, 65536, size=n).astype(np.uint32)
+            w = np.zeros(n, np.uint16)
+            w[~bad] = oracle.batch_spans(buf, off[~bad], L[~bad], seeds[~bad])
+            b = batch.PacketBatch.from_host(buf[:total], off, L, device=dev)
+            out = torch.empty(max(n, 1), dtype=torch.int16, device=dev)
+            st = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+            items.append((b, out, st, torch.from_numpy(seeds.view(np.int32)).to(dev)))
+            wants.append((w, np.where(bad, native.ST_RANGE, (w == 0).astype(np.uint8))))
+        plan.append((items, wants))
+    eng = batch.Engine(0, frames=False, max_steps=64, max_in_flight=int(rng.choice([2, 8, 64])))
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    eng.start(stream)
+    try:
+        steps = [eng.submit(items) for items, _ in plan]
+    finally:
+        eng.stop()
+        stream.synchronize()
+        eng.close()
+    for step, (items, wants) in zip(steps, plan):
+        for j, (it, (w, wst)) in enumerate(zip(items, wants)):
+            n = it[0].n
+            msg = f"case {case} step {step} batch {j}: n {n}, knobs {knobs}"
+            assert np.array_equal(batch.as_u16(it[1][:n]), w), msg
+            assert np.array_equal(it[2][:n].cpu().numpy(), wst), msg
