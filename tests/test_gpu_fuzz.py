@@ -376,7 +376,8 @@ def test_fuzz_engine_steps(dev, case):
             buf = rng.integers(0, 256, size=max(total, 1), dtype=np.uint8)
             _ipv4_headers(rng, buf, off, L)
             b = batch.PacketBatch.from_host(buf[:total], off, L, device=dev)
-            out2 = torch.empty(max(2 * n, 2), dtype=torch.int16, device=dev)
+            # a third of the batches verify only (status, no out2: what cfg 3 and the rx half submit)
+            out2 = torch.empty(max(2 * n, 2), dtype=torch.int16, device=dev) if rng.random() < 0.67 else None
             st = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
             items.append((b, out2, st))
             wants.append(oracle.batch_ipv4(buf, off, L))
@@ -402,8 +403,9 @@ def test_fuzz_engine_steps(dev, case):
         if what == "sum":
             for j, (it, (w2, wst)) in enumerate(zip(*data)):
                 n = it[0].n
-                got = batch.as_u16(it[1][: 2 * n]).reshape(n, 2)
-                assert np.array_equal(got, w2), f"{msg} batch {j}"
+                if it[1] is not None:
+                    got = batch.as_u16(it[1][: 2 * n]).reshape(n, 2)
+                    assert np.array_equal(got, w2), f"{msg} batch {j}"
                 assert np.array_equal(it[2][:n].cpu().numpy(), wst), f"{msg} batch {j}"
         else:
             b, out2, st, buf, off, L, total, mode = data
