@@ -668,3 +668,41 @@ def test_fuzz_engine_spans(dev, case):
             msg = f"case {case} step {step} batch {j}: n {n}, knobs {knobs}"
             assert np.array_equal(batch.as_u16(it[1][:n]), w), msg
             assert np.array_equal(it[2][:n].cpu().numpy(), wst), msg
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_fuzz_large_batches(dev, case):
+    """100 k-300 k packets under random knobs: long claim chains per wave,
+    the tail split over many tiles, grids capped at 1-3 blocks per CU."""
+    rng = np.random.default_rng(9700 + case)
+    lib = native.load()
+    frames = case % 2 == 1
+    n = int(rng.integers(100_000, 300_001))
+    L = np.minimum(_lengths(rng, n, huge=False), 4000).astype(np.uint32)
+    off, total, kind = _layout(rng, L)
+    if kind == "shuffled":
+        off, L = _shuffle_pairs(rng, off, L)
+    buf = rng.integers(0, 256, size=max(total, 1), dtype=np.uint8)
+    if frames:
+        _ipv4_headers(rng, buf, off, L)
+    bad = _range_bad(rng, off, L, total, frac=0.001)
+    ok = ~bad
+    knobs = _knobs(rng, lib)
+    b = batch.PacketBatch.from_host(buf[:total], off, L, device=dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    msg = _case_msg(case, kind, knobs, n)
+    if frames:
+        got = batch.as_u16(batch.ipv4_frames(b, status=st)).reshape(n, 2)
+        torch.cuda.synchronize()
+        w2, wst = oracle.batch_ipv4(buf, off[ok], L[ok], nthreads=8)
+        gst = st.cpu().numpy()
+        assert np.array_equal(got[ok], w2) and np.array_equal(gst[ok], wst), msg
+    else:
+        seeds = rng.integers(0, 65536, size=n).astype(np.uint32)
+        got = batch.as_u16(batch.spans(b, seeds=torch.from_numpy(seeds.view(np.int32)).to(dev), status=st))
+        torch.cuda.synchronize()
+        want = oracle.batch_spans(buf, off[ok], L[ok], seeds[ok], nthreads=8)
+        gst = st.cpu().numpy()
+        assert np.array_equal(got[ok], want), msg
+        assert np.array_equal(gst[ok], (want == 0).astype(np.uint8)), msg
+    assert np.all(gst[bad] == native.ST_RANGE), msg
