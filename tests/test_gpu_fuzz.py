@@ -706,3 +706,83 @@ def test_fuzz_large_batches(dev, case):
         assert np.array_equal(got[ok], want), msg
         assert np.array_equal(gst[ok], (want == 0).astype(np.uint8)), msg
     assert np.all(gst[bad] == native.ST_RANGE), msg
+
+
+def test_fuzz_shard_threads(dev):
+    """Seastar's model from Python: six shard threads on one GPU, each with its
+    own sccsum_init, stream, random knobs (thread-local) and random launches
+    (spans, frames, multi, fills, fragment lists) in flight together; every
+    result checked against the oracle once the thread's stream is done."""
+    import threading
+
+    errors = []
+
+    def shard(t):
+        try:
+            rng = np.random.default_rng(9800 + t)
+            lib = native.load()
+            native.check(lib.sccsum_init(0), "sccsum_init")
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            knobs = _knobs(rng, lib)
+            checks = []
+            with torch.cuda.stream(s):
+                for it in range(12):
+                    op = str(rng.choice(["spans", "frames", "multi", "fill", "frags"]))
+                    n = int(rng.choice([1, 64, 400, 1500]))
+                    L = _lengths(rng, n, huge=False, lo=20 if op == "fill" else 0)
+                    off, total, kind = _layout(rng, L, disjoint=op == "fill")
+                    if kind == "shuffled":
+                        off, L = _shuffle_pairs(rng, off, L)
+                    buf = rng.integers(0, 256, size=max(total, 1), dtype=np.uint8)
+                    if op in ("frames", "multi", "fill"):
+                        _ipv4_headers(rng, buf, off, L)
+                    b = batch.PacketBatch.from_host(buf[:total], off, L, device=dev)
+                    if op == "spans":
+                        out = batch.spans(b, stream=s)
+                        checks.append((op, out, oracle.batch_spans(buf, off, L)))
+                    elif op == "frames":
+                        st = torch.empty(n, dtype=torch.uint8, device=dev)
+                        out = batch.ipv4_frames(b, status=st, stream=s)
+                        checks.append((op, (out, st), oracle.batch_ipv4(buf, off, L)))
+                    elif op == "multi":
+                        st = torch.empty(n, dtype=torch.uint8, device=dev)
+                        outs = batch.ipv4_frames_multi([(b, None, st), (b, None, None)], stream=s)
+                        checks.append((op, (outs, st), oracle.batch_ipv4(buf, off, L)))
+                    elif op == "fill":
+                        mode = native.FILL_IP | native.FILL_L4
+                        out2 = torch.empty(2 * n, dtype=torch.int16, device=dev)
+                        batch.ipv4_fill(b, mode, out2=out2, stream=s)
+                        checks.append((op, (b, total), oracle.batch_ipv4_fill(buf, off, L, mode)[0][:total]))
+                    else:
+                        first = np.arange(n + 1, dtype=np.uint32)  # one fragment per packet
+                        got = batch.fragments(b.data, total, b.off, b.length,
+                                              torch.from_numpy(first.view(np.int32)).to(dev), stream=s)
+                        checks.append((op, got, oracle.batch_spans(buf, off, L)))
+            s.synchronize()
+            for k, (op, got, want) in enumerate(checks):
+                msg = f"thread {t} launch {k} ({op}), knobs {knobs}"
+                if op in ("spans", "frags"):
+                    assert np.array_equal(batch.as_u16(got), want), msg
+                elif op == "frames":
+                    n = got[1].numel()
+                    assert np.array_equal(batch.as_u16(got[0]).reshape(n, 2), want[0]), msg
+                    assert np.array_equal(got[1].cpu().numpy(), want[1]), msg
+                elif op == "multi":
+                    outs, st = got
+                    for o in outs:
+                        assert np.array_equal(batch.as_u16(o).reshape(-1, 2), want[0]), msg
+                    assert np.array_equal(st.cpu().numpy(), want[1]), msg
+                else:
+                    b, total = got
+                    assert np.array_equal(b.data[:total].cpu().numpy(), want), msg
+        except Exception as e:  # noqa: BLE001 - reported by the main thread
+            errors.append(f"thread {t}: {e!r}")
+
+    threads = [threading.Thread(target=shard, args=(t,)) for t in range(6)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in threads), "a shard thread hung"
+    assert not errors, errors
