@@ -103,6 +103,8 @@ def parse():
     ap.add_argument("--engine-wt", type=int, default=None,
                     help="A/B: engine result stores written through (1) or stored as a launch does (0) "
                          "(sccsum_set_engine_write_through)")
+    ap.add_argument("--fill-single-max", type=int, default=None,
+                    help="A/B: in-place fills of at most this many frames run in one pass (sccsum_set_fill_single_max)")
     ap.add_argument("--run-align", type=int, default=None, help="A/B: run-start alignment in units (sccsum_set_run_align)")
     ap.add_argument("--sync", default="auto", choices=["auto", "spin", "yield"],
                     help="how the host thread waits on the device (hipSetDeviceFlags schedule)")
@@ -1366,6 +1368,8 @@ def main():
         if args.engine_wt is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_engine_write_through(args.engine_wt),
                          "sccsum_set_engine_write_through")
+        if args.fill_single_max is not None:  # A/B only (sccsum_diag.h)
+            native.check(native.load().sccsum_set_fill_single_max(args.fill_single_max), "sccsum_set_fill_single_max")
         if args.run_align is not None:  # A/B only (sccsum_diag.h)
             native.check(native.load().sccsum_set_run_align(args.run_align), "sccsum_set_run_align")
         {"udp1500": run_udp1500, "tcp64k": run_tcp64k, "mixed": run_mixed, "e2e": run_e2e, "fill": run_fill,

@@ -239,18 +239,19 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  *       slice of a larger buffer).  The engine always runs the flat kernel, so
  *       sparse layouts give exact results but belong on the launches, whose
  *       row kernel reads them faster.  Frames take no seeds.
- *   sccsum_engine_submit_fill(e, batches, nbatch, mode, timeout_ns, &step)
+ *   sccsum_engine_submit_fill(e, batches, nbatch, max_len, mode, timeout_ns, &step)
  *       an in-place fill (sccsum_ipv4_fill's SCCSUM_FILL_L4 and/or
- *       SCCSUM_FILL_ICMP_ECHO, optionally | SCCSUM_FILL_IP) of every batch,
- *       as two steps: a generate step (the flat kernel's fill values into each
- *       batch's d_out, required here, and the status bits into d_status) and a
- *       store step whose tiles wait for the generate step and write the values
- *       into the frames' fields (d_bytes is written).  *step = the store step:
- *       once it is done the frames are wire-ready in device memory and d_out
- *       holds the values stored.  Both steps or neither are published (a
- *       fill takes 2 of the run's max_steps).  The store step reads the values
- *       from d_out: no other step may write a fill's d_out (nor its frames)
- *       before the fill is done.
+ *       SCCSUM_FILL_ICMP_ECHO, optionally | SCCSUM_FILL_IP) of every batch
+ *       (d_bytes is written; each batch's d_out, required here, gets the
+ *       values stored and d_status the status bits).  A fill of at most
+ *       262 144 frames (sccsum_set_fill_single_max) is ONE step whose tiles
+ *       store the fields themselves; a larger one is two: a generate step into
+ *       d_out and a store step whose tiles wait for it and write the values
+ *       into the frames' fields (both or neither are published: such a fill
+ *       takes 2 of the run's max_steps).  *step = the fill's last step: once
+ *       it is done the frames are wire-ready in device memory and d_out holds
+ *       the values stored.  No other step may write a fill's d_out (nor its
+ *       frames) before the fill is done.  max_len as for submit.
  *   sccsum_engine_wait(e, step, timeout_ns)   0 once the step is done
  *   sccsum_engine_stop(e)               no more steps: the grid leaves once the
  *       published steps are done (synchronise `stream` to wait for it)
@@ -274,8 +275,8 @@ int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_
 int sccsum_engine_start(sccsum_engine* e, void* stream);
 int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
                          uint64_t timeout_ns, uint64_t* step);
-int sccsum_engine_submit_fill(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t mode,
-                              uint64_t timeout_ns, uint64_t* step);
+int sccsum_engine_submit_fill(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
+                              uint32_t mode, uint64_t timeout_ns, uint64_t* step);
 int sccsum_engine_wait(sccsum_engine* e, uint64_t step, uint64_t timeout_ns);
 int sccsum_engine_stop(sccsum_engine* e);
 int sccsum_engine_destroy(sccsum_engine* e);

@@ -73,6 +73,12 @@ int sccsum_set_engine_idle_ms(int ms);
  * k = every k-th step.  SCCSUM_EINVAL outside -1 .. 65536. */
 int sccsum_set_engine_sync_every(int steps);
 
+/* In-place fills (SCCSUM_FILL_L4 / SCCSUM_FILL_ICMP_ECHO, launches and engine
+ * fill steps) of at most `frames` frames run in one pass: the generate tiles
+ * store the fields themselves (default 262 144; 0 = always two passes).
+ * SCCSUM_EINVAL below 0. */
+int sccsum_set_fill_single_max(int frames);
+
 /* Flat kernel forms without a chunk in flight (U 8 form 14, U 16): a run's
  * last chunk loads and scans only the rows its units reach, U / 8 .. U (1, the
  * default), or always U rows (0).  SCCSUM_EINVAL otherwise. */

@@ -265,9 +265,10 @@ public:
     // in-place fill of every batch (d_out: the values, required); the step returned is done once
     // the frames hold their checksums
     uint64_t submit_fill(const sccsum_batch* batches, uint32_t nbatch, uint32_t mode,
-                         uint64_t timeout_ns = 1'000'000'000) {
+                         uint64_t timeout_ns = 1'000'000'000, uint32_t max_len = 0) {
         uint64_t step = 0;
-        check(sccsum_engine_submit_fill(_e, batches, nbatch, mode, timeout_ns, &step), "sccsum_engine_submit_fill");
+        check(sccsum_engine_submit_fill(_e, batches, nbatch, max_len, mode, timeout_ns, &step),
+              "sccsum_engine_submit_fill");
         return step;
     }
     void wait(uint64_t step, uint64_t timeout_ns = 1'000'000'000) {

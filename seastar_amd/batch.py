@@ -501,7 +501,7 @@ class Engine:
         arr, nb, ml, items, fill_mode = prep
         step = ctypes.c_uint64()
         if fill_mode:
-            native.check(self._lib.sccsum_engine_submit_fill(self._h, ctypes.cast(arr, ctypes.c_void_p), nb,
+            native.check(self._lib.sccsum_engine_submit_fill(self._h, ctypes.cast(arr, ctypes.c_void_p), nb, ml,
                                                               fill_mode, int(timeout_s * 1e9), ctypes.byref(step)),
                          "sccsum_engine_submit_fill")
         else:

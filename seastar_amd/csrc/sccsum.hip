@@ -54,6 +54,7 @@ constexpr uint32_t kFlagFillL4 = 2;  // frames: generate the TCP/UDP checksum an
 constexpr uint32_t kFlagFillIp = 4;  // frames (with kFlagFillL4): also generate + store the IPv4 header checksum
 constexpr uint32_t kFlagFillIcmp = 8;  // frames: turn ICMP echo requests into replies in place (ip.cc:464-474)
 constexpr uint32_t kFillFlags = kFlagFillL4 | kFlagFillIcmp;  // the in-place (FILL) instantiation
+constexpr uint32_t kFlagFillNow = 64;  // frames (FILL): each tile stores its frames' fields itself (one pass)
 constexpr uint32_t kFlagFullChunks = 16;  // flat kernel: a run's last chunk loads all U rows (diagnostic A/B)
 constexpr uint32_t kFlagEngineWT = 32;    // engine: results written through (sc0 sc1), else stored by the launch
                                           // rule and released (agent scope) before a step's count
@@ -2043,6 +2044,22 @@ __device__ __forceinline__ void flat_body(Src& src, const uint32_t flags, const 
         }
 
         put(cur.ref, base, mine, word, st);
+        // A single-pass fill (kFlagFillNow: small fills, sccsum_ipv4_fill and
+        // sccsum_engine_submit_fill) stores the fields from the tile, after
+        // every read of it: the status says which (ST_OK the IP field,
+        // ST_L4_OK the L4 or ICMP one; RANGE / MALFORMED frames none).  A
+        // store inside the read stream costs more than the store pass at 1 M
+        // frames (§5.6); a small fill is bound by latency instead, and one
+        // pass saves the store kernel's launch or the store step's wait.
+        // (The engine writes them through, as its store tiles do.)
+        if (FILL && fill_tile && (ff & kFlagFillNow) && mine) {
+            uint8_t* const f0 = reinterpret_cast<uint8_t*>(a0);
+            if (st & SCCSUM_ST_OK) store_field<Src::kEngine>(f0 + head + 10, word);
+            if (st & SCCSUM_ST_L4_OK) {
+                if (icmp_lane) store_field<Src::kEngine>(f0 + fpos - 2, 0u);  // echo reply: type 0, code 0
+                store_field<Src::kEngine>(f0 + fpos, word >> 16);
+            }
+        }
         // (readfirstlane: the compiler otherwise loses the tile number's
         // uniformity across the issue branches and reads the next tile's queue
         // fields with vector loads, 8 more per tile)
@@ -2310,6 +2327,13 @@ constexpr int kOutPolicy = 1;
 // spans 168.8 -> 166.7 us, 1500 B frames and 64 KiB spans -0.4-0.5 %; 64 B
 // (4 units) lands in between.
 constexpr int kRunAlign = 8;
+// In-place fills (FILL_L4 / FILL_ICMP_ECHO) of at most this many frames store
+// their fields from the generate tiles (kFlagFillNow) instead of a second pass.
+// One pass wins up to 262 144 frames (launch 88.3 against 92.1 us, engine 79.4
+// against 98.2) and loses at 1 M (launch 355 against 330 us, engine 342
+// against 332), where the stores inside the read stream cost more than the
+// store pass (profiles/r05_fill_one_pass.log)
+constexpr uint32_t kFillSingleMax = 262144;
 
 // Diagnostic knobs (include/sccsum_diag.h): per host thread, so one shard's
 // A/B settings never leak into another thread's launches.
@@ -2327,6 +2351,7 @@ struct Knobs {
     int run_align = kRunAlign;       // flat kernel: run extents start on 1 / 4 / 8-unit (16 / 64 / 128 B) boundaries
     int engine_wt = 1;               // engine: results written through (1) or stored as a launch stores them (0)
     int engine_idle_ms = 1000;       // engine: a run given no new step for this long gives up (SCCSUM_EIDLE)
+    uint32_t fill_single_max = kFillSingleMax;  // in-place fills of at most this many frames run in one pass
     int engine_sync_every = -1;      // engine: every k-th step waits for the step before it (0 = never,
                                      // -1 = every kEngineSyncEvery steps of >= 2 tiles per wave)
 };
@@ -2631,9 +2656,23 @@ bool batch_ok(const void* d_bytes, const uint64_t* d_off, const uint32_t* d_len,
 // 2304 B mbuf slots (data at +256), per 1 M frames: flat 537 us (920 without
 // short chunks), one wave per packet 359-368 us, one row per packet 253-259 us
 // (profiles/r02_ab_slots.log, r02_ab_rows.log).
+// The bytes a launch's packets can span: bytes_len, capped by n * max_len when
+// the caller gives max_len.  A batch that is a slice of a larger buffer (a
+// shard's rx ring handed over a burst at a time; offsets into the whole ring)
+// has a bytes_len far above its packets' bytes, and sizing tiles or picking
+// the form from it gave such a launch tiles of one or two packets: a
+// 16 384-frame fill on a slice of a 393 MB ring took 26.0 us a launch with
+// 2-frame tiles, 16.9 with 8-frame ones (profiles/r05_engine_small_steps_final.log).
+uint64_t packet_bytes(uint64_t n_total, uint64_t bytes_total, uint32_t max_len) {
+    if (max_len == 0) return bytes_total;
+    const uint64_t cap = n_total * static_cast<uint64_t>(max_len);
+    return cap < bytes_total ? cap : bytes_total;
+}
+
 int pick_variant(uint64_t n_total, uint64_t bytes_total, uint32_t flags, uint32_t max_len) {
     int variant = t_knobs.variant;
-    const int dflt = (n_total >= (512u << 10) && bytes_total >= (256ull << 20)) ? 16 : 15;
+    const uint64_t pb = packet_bytes(n_total, bytes_total, max_len);
+    const int dflt = (n_total >= (512u << 10) && pb >= (256ull << 20)) ? 16 : 15;
     const bool fill = (flags & kFillFlags) != 0;
     const bool sparse = max_len != 0 && n_total != 0 && bytes_total / n_total >= uint64_t(max_len) + 64u;
     if (variant == 0 && sparse && !fill) return 2;
@@ -2674,7 +2713,8 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
         Q.out[0] = d_out;
         Q.status[0] = d_status;
         Q.n[0] = n;
-        return static_cast<int>(launch_flat_variant<IPV4>(variant, s, dev, Q, n, bytes_len, flags, rss));
+        return static_cast<int>(
+            launch_flat_variant<IPV4>(variant, s, dev, Q, n, packet_bytes(n, bytes_len, max_len), flags, rss));
     }
 }
 
@@ -2726,7 +2766,8 @@ int launch_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
         Q.status[q] = x.d_status;
         Q.n[q] = x.n;
     }
-    return static_cast<int>(launch_flat_variant<IPV4>(variant, s, dev, Q, n_total, bytes_total, 0, kNoRss));
+    return static_cast<int>(launch_flat_variant<IPV4>(variant, s, dev, Q, n_total,
+                                                      packet_bytes(n_total, bytes_total, max_len), 0, kNoRss));
 }
 
 // ---- gather: fragments from device-readable memory (HBM, or pinned host
@@ -3326,20 +3367,32 @@ int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t
 // behind the next fill's generate step instead (no drain wait), the store
 // tiles of the groups that finished first ran inside the other groups' read
 // stream, and a fill took 354-356 us against 328 (profiles/r05_engine_fill.log).
-int sccsum_engine_submit_fill(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t mode,
-                              uint64_t timeout_ns, uint64_t* step) {
+int sccsum_engine_submit_fill(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
+                              uint32_t mode, uint64_t timeout_ns, uint64_t* step) {
     constexpr uint32_t kEngineModes = SCCSUM_FILL_IP | SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO;
     if (!e || !e->running || !step || !e->fill || (mode & ~kEngineModes) ||
         !(mode & (SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO))) {
         return SCCSUM_EINVAL;
     }
     if (const int rc = engine_check(e, batches, nbatch, true); rc != SCCSUM_OK) return rc;
-    if (const int rc = engine_room(e, 2, timeout_ns); rc != SCCSUM_OK) return rc;
+    uint64_t n_total = 0;
+    for (uint32_t i = 0; i < nbatch; ++i) n_total += batches[i].n;
+    // a small fill is one step whose tiles store their own fields (no store
+    // step, no wait on the generate step: a store step's waves hold the next
+    // fill's tiles while they wait, which chained small fills one after another)
+    const bool single = n_total <= sccsum::t_knobs.fill_single_max;
+    if (const int rc = engine_room(e, single ? 1 : 2, timeout_ns); rc != SCCSUM_OK) return rc;
     const uint64_t kflags = ((mode & SCCSUM_FILL_L4) ? sccsum::kFlagFillL4 : 0u) |
                             ((mode & SCCSUM_FILL_ICMP_ECHO) ? sccsum::kFlagFillIcmp : 0u) |
-                            ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u);
+                            ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u) |
+                            (single ? sccsum::kFlagFillNow : 0u);
+    if (single) {
+        *step = engine_put(e, batches, nbatch, sccsum::kStepFillGen | (kflags << 8) | (uint64_t(mode) << 16), 0,
+                           engine_tile(e, batches, nbatch, max_len));
+        return SCCSUM_OK;
+    }
     const uint64_t gen = engine_put(e, batches, nbatch, sccsum::kStepFillGen | (kflags << 8) | (uint64_t(mode) << 16),
-                                    0, engine_tile(e, batches, nbatch, 0));
+                                    0, engine_tile(e, batches, nbatch, max_len));
     // the store half: no status (the generate half reported it)
     sccsum_batch st[SCCSUM_ENGINE_MAX_BATCHES];
     for (uint32_t i = 0; i < nbatch; ++i) {
@@ -3563,6 +3616,15 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
     const hipStream_t s = static_cast<hipStream_t>(stream);
     int dev = 0;
     if (const int rc = sccsum::launch_device(s, &dev); rc != SCCSUM_OK) return rc;
+    if (two_pass && n <= sccsum::t_knobs.fill_single_max) {
+        // a small fill in one pass: the generate tiles store the fields
+        // themselves (kFlagFillNow; d_out2 stays optional, nothing to hand over)
+        const uint32_t flags = ((mode & SCCSUM_FILL_L4) ? sccsum::kFlagFillL4 : 0u) |
+                               ((mode & SCCSUM_FILL_ICMP_ECHO) ? sccsum::kFlagFillIcmp : 0u) |
+                               ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u) | sccsum::kFlagFillNow;
+        return sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len, stream,
+                                    flags);
+    }
     if (two_pass) {
         // pass 1 generates into d_out2, pass 2 stores the fields.  Without a
         // caller's d_out2 the values go through a stream-ordered allocation
@@ -3616,6 +3678,12 @@ int sccsum_set_blocks_per_cu(int blocks) {
 int sccsum_set_group_units(int units) {
     if (units != 0 && units != 1 && units != 2 && units != 4 && units != 8) return SCCSUM_EINVAL;
     sccsum::t_knobs.group_units = units;
+    return SCCSUM_OK;
+}
+
+int sccsum_set_fill_single_max(int frames) {
+    if (frames < 0) return SCCSUM_EINVAL;
+    sccsum::t_knobs.fill_single_max = static_cast<uint32_t>(frames);
     return SCCSUM_OK;
 }
 

@@ -103,9 +103,10 @@ _PROTOS = {
     "sccsum_engine_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _u32, _u32, ctypes.POINTER(_vp)]),
     "sccsum_engine_start": (ctypes.c_int, [_vp, _vp]),
     "sccsum_engine_submit": (ctypes.c_int, [_vp, _vp, _u32, _u32, _u64, ctypes.POINTER(_u64)]),
-    "sccsum_engine_submit_fill": (ctypes.c_int, [_vp, _vp, _u32, _u32, _u64, ctypes.POINTER(_u64)]),
+    "sccsum_engine_submit_fill": (ctypes.c_int, [_vp, _vp, _u32, _u32, _u32, _u64, ctypes.POINTER(_u64)]),
     "sccsum_set_engine_idle_ms": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_set_engine_sync_every": (ctypes.c_int, [ctypes.c_int]),
+    "sccsum_set_fill_single_max": (ctypes.c_int, [ctypes.c_int]),
     "sccsum_engine_wait": (ctypes.c_int, [_vp, _u64, _u64]),
     "sccsum_engine_stop": (ctypes.c_int, [_vp]),
     "sccsum_engine_destroy": (ctypes.c_int, [_vp]),
@@ -129,6 +130,7 @@ class Batch(ctypes.Structure):
 
 
 MAX_BATCHES = 16
+FILL_SINGLE_MAX = 262144  # in-place fills of at most this many frames run in one pass (sccsum_diag.h)
 ENGINE_MAX_BATCHES = 4
 
 

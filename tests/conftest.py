@@ -23,3 +23,16 @@ def dev():
     native.check(native.load().sccsum_init(0), "sccsum_init")
     torch.cuda.set_device(0)
     return torch.device("cuda:0")
+
+
+@pytest.fixture(params=[1, 2], ids=["one_pass", "two_pass"])
+def fill_passes(request, dev):
+    """In-place fills in one pass (the generate tiles store the fields: the
+    default up to 262 144 frames) and in two (generate, then a store pass or
+    an engine store step): sccsum_set_fill_single_max, thread-local."""
+    from seastar_amd import native
+
+    lib = native.load()
+    native.check(lib.sccsum_set_fill_single_max(1 << 30 if request.param == 1 else 0), "sccsum_set_fill_single_max")
+    yield request.param
+    native.check(lib.sccsum_set_fill_single_max(native.FILL_SINGLE_MAX), "sccsum_set_fill_single_max")

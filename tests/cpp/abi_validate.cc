@@ -119,7 +119,7 @@ static void checks() {
     EXPECT(sccsum_engine_start(nullptr, nullptr) == SCCSUM_EINVAL);
     uint64_t step = 0;
     EXPECT(sccsum_engine_submit(nullptr, nullptr, 1, 0, 0, &step) == SCCSUM_EINVAL);
-    EXPECT(sccsum_engine_submit_fill(nullptr, nullptr, 1, SCCSUM_FILL_IP | SCCSUM_FILL_L4, 0, &step) ==
+    EXPECT(sccsum_engine_submit_fill(nullptr, nullptr, 1, 0, SCCSUM_FILL_IP | SCCSUM_FILL_L4, 0, &step) ==
            SCCSUM_EINVAL);
     EXPECT(sccsum_engine_wait(nullptr, 0, 0) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_stop(nullptr) == SCCSUM_EINVAL);

@@ -247,7 +247,7 @@ ENGINE_FILL_MODES = {
 
 
 @pytest.mark.parametrize("mode", list(ENGINE_FILL_MODES))
-def test_engine_fill_steps_match_oracle(dev, mode):
+def test_engine_fill_steps_match_oracle(dev, mode, fill_passes):
     """Fill steps (generate, then the store step that waits for it) of the tx
     generator's odd frames — UDP / TCP / ICMP, options, padding, truncation,
     runts, IP fragments, garbage checksum fields, odd offsets — among verify
@@ -525,15 +525,25 @@ def test_engine_fill_limits_and_empty_batches(dev):
     hold empty batches beside real ones; a fill on an engine created without
     SCCSUM_ENGINE_FILL, or without out2, or in a header-only mode, is refused
     (SCCSUM_EINVAL); the step a fill returns is its store step, done once
-    the frames hold their values."""
-    import ctypes
-
+    the frames hold their values.  (The two-step form: fills are forced past
+    the one-pass limit here.)"""
     from test_gpu_parity import _tx_frames
 
     rng = np.random.default_rng(0xEA)
     buf, off, length = _tx_frames(rng, 700)
     m = native.FILL_IP | native.FILL_L4
     want = oracle.batch_ipv4_fill(buf, off, length, m)
+    lib0 = native.load()
+    native.check(lib0.sccsum_set_fill_single_max(0), "two passes")  # this test is about the two-step form
+    try:
+        _fill_limits_two_steps(dev, rng, buf, off, length, m, want)
+    finally:
+        native.check(lib0.sccsum_set_fill_single_max(native.FILL_SINGLE_MAX), "default")
+
+
+def _fill_limits_two_steps(dev, rng, buf, off, length, m, want):
+    import ctypes
+
     b = batch.PacketBatch.from_host(buf, off, length, device=dev)
     empty = batch.PacketBatch(data=torch.zeros(16, dtype=torch.uint8, device=dev),
                               off=torch.zeros(0, dtype=torch.int64, device=dev),
@@ -549,7 +559,7 @@ def test_engine_fill_limits_and_empty_batches(dev):
     step = ctypes.c_uint64()
     stream = torch.cuda.Stream(device=dev)
     plain.start(stream)
-    assert lib.sccsum_engine_submit_fill(plain._h, ctypes.cast(arr, ctypes.c_void_p), 1, m, 10**9,
+    assert lib.sccsum_engine_submit_fill(plain._h, ctypes.cast(arr, ctypes.c_void_p), 1, 0, m, 10**9,
                                          ctypes.byref(step)) == native.SCCSUM_EINVAL  # not a fill engine
     plain.stop()
     stream.synchronize()
@@ -559,9 +569,9 @@ def test_engine_fill_limits_and_empty_batches(dev):
     no_out = (native.Batch * 1)()
     no_out[0] = native.Batch(b.data.data_ptr(), b.bytes_len, b.off.data_ptr(), b.length.data_ptr(), None, None,
                              st.data_ptr(), b.n)
-    assert lib.sccsum_engine_submit_fill(eng._h, ctypes.cast(no_out, ctypes.c_void_p), 1, m, 10**9,
+    assert lib.sccsum_engine_submit_fill(eng._h, ctypes.cast(no_out, ctypes.c_void_p), 1, 0, m, 10**9,
                                          ctypes.byref(step)) == native.SCCSUM_EINVAL  # no out2
-    assert lib.sccsum_engine_submit_fill(eng._h, ctypes.cast(arr, ctypes.c_void_p), 1,
+    assert lib.sccsum_engine_submit_fill(eng._h, ctypes.cast(arr, ctypes.c_void_p), 1, 0,
                                          native.FILL_IP | native.FILL_L4_PSEUDO, 10**9,
                                          ctypes.byref(step)) == native.SCCSUM_EINVAL  # header-only mode
     s1 = eng.submit_fill([(empty, torch.empty(2, dtype=torch.int16, device=dev), None), (b, out2, st)], m)
@@ -580,7 +590,7 @@ def test_engine_fill_limits_and_empty_batches(dev):
 
 
 @pytest.mark.parametrize("in_flight", [2, 64])
-def test_engine_fill_stress_small_steps(dev, in_flight):
+def test_engine_fill_stress_small_steps(dev, in_flight, fill_passes):
     """Many small steps, fills and verifies interleaved, 2 or 64 in flight:
     100 fill steps of 1-3 tiny batches (1-40 of the tx generator's odd frames,
     so every store tile waits on a generate step of a few one-frame tiles)
@@ -813,4 +823,39 @@ def test_engine_run_of_max_steps(dev):
     for s in range(slots):
         n = 1 + (max_steps - slots + s) % 3  # the slot's last step's frame count
         assert np.array_equal(got[s, :n], want[:n]), s
+    eng.close()
+
+
+def test_engine_fill_single_pass_takes_one_step(dev):
+    """A fill of at most sccsum_set_fill_single_max frames (262 144 by default)
+    is ONE engine step whose tiles store the fields themselves: it returns
+    that step, takes one of the run's steps (with one step left it still
+    fits), and leaves the frames exactly as the oracle's writers do."""
+    from test_gpu_parity import _tx_frames
+
+    rng = np.random.default_rng(0xEC)
+    buf, off, length = _tx_frames(rng, 700)
+    m = native.FILL_IP | native.FILL_L4 | native.FILL_ICMP_ECHO
+    want = oracle.batch_ipv4_fill(buf, off, length, m)
+    b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+    out2 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+    st = torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev)
+    vb, vwant, _ = _frames_step(rng, dev, 1)
+    vout = torch.full((2 * vb.n,), -1, dtype=torch.int16, device=dev)
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, fill=True, max_steps=2, max_in_flight=2)
+    stream = torch.cuda.Stream(device=dev)
+    eng.start(stream)
+    try:
+        assert eng.submit([(vb, vout, None)]) == 0
+        s1 = eng.submit_fill([(b, out2, st)], m)
+        assert s1 == 1  # one step: the run's last
+        eng.wait(s1)
+    finally:
+        eng.stop()
+        stream.synchronize()
+    assert np.array_equal(b.data.cpu().numpy()[: b.bytes_len], want[0])
+    assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want[1])
+    assert np.array_equal(st.cpu().numpy(), want[2])
+    assert np.array_equal(batch.as_u16(vout).reshape(-1, 2), vwant)
     eng.close()

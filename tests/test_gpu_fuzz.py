@@ -9,7 +9,8 @@ Each case draws
   with the frame, fragments, TCP / UDP / ICMP / other protocols, fields right
   or wrong;
 - random diagnostic knobs: kernel family and form, tile packets, tile bytes,
-  run alignment, short chunks, tail split, dynamic tiles, grid cap.
+  run alignment, short chunks, tail split, dynamic tiles, grid cap, and
+  fills in one pass or two.
 
 Then it compares every output bit with the oracle (oracle/sccsum_oracle.c).
 The knobs never change results (include/sccsum_diag.h), so one oracle answer
@@ -41,6 +42,7 @@ def _knobs(rng, lib, fill=False):
         "tail": (int(rng.choice([1, 2, 4, 8])), int(rng.integers(0, 65))),
         "dynamic": int(rng.integers(0, 2)),
         "blocks_per_cu": int(rng.choice([8, 1, 2, 3])),
+        "fill_single_max": int(rng.choice([native.FILL_SINGLE_MAX, 0])),  # fills in one pass, or generate + store
     }
     native.check(lib.sccsum_set_kernel_variant(k["variant"]), "variant")
     native.check(lib.sccsum_set_tile_packets(k["tile_packets"]), "tile_packets")
@@ -50,6 +52,7 @@ def _knobs(rng, lib, fill=False):
     native.check(lib.sccsum_set_tail_split(*k["tail"]), "tail_split")
     native.check(lib.sccsum_set_dynamic_tiles(k["dynamic"]), "dynamic")
     native.check(lib.sccsum_set_blocks_per_cu(k["blocks_per_cu"]), "blocks_per_cu")
+    native.check(lib.sccsum_set_fill_single_max(k["fill_single_max"]), "fill_single_max")
     return k
 
 
@@ -65,6 +68,7 @@ def _default_knobs(dev):
     lib.sccsum_set_tail_split(1, 4)
     lib.sccsum_set_dynamic_tiles(1)
     lib.sccsum_set_blocks_per_cu(8)
+    lib.sccsum_set_fill_single_max(native.FILL_SINGLE_MAX)
 
 
 def _lengths(rng, n, huge=True, lo=0):

@@ -470,7 +470,7 @@ FILL_MODES = {
 
 
 @pytest.mark.parametrize("mode", list(FILL_MODES))
-def test_ipv4_fill_in_place(dev, mode):
+def test_ipv4_fill_in_place(dev, mode, fill_passes):
     """Tx generate + in-place store == the reference writers, byte for byte."""
     m = FILL_MODES[mode]
     rng = np.random.default_rng(0xF111 + m)
@@ -555,7 +555,7 @@ def _packed_tx_frames(rng, n, gaps=(0,)):
 
 
 @pytest.mark.parametrize("gaps", [(0,), (0, 0, 0, 1, 3, 16)], ids=["contiguous", "mostly_contiguous"])
-def test_ipv4_fill_whole_unit_stores(dev, gaps):
+def test_ipv4_fill_whole_unit_stores(dev, gaps, fill_passes):
     """In-place fill rewrites the 16-byte units holding the fields whole where
     no other frame writes their bytes: byte-exact against the oracle on packed
     frames whose neighbours share those units (short frames, lengths at the
@@ -792,7 +792,7 @@ def test_many_launches_in_flight_streams_and_graphs(dev, kernel_variant):
 
 
 @pytest.mark.parametrize("path", ["c_abi", "wrapper"])
-def test_fill_without_out2_in_a_graph(dev, kernel_variant, path):
+def test_fill_without_out2_in_a_graph(dev, kernel_variant, path, fill_passes):
     """sccsum_ipv4_fill with no d_out2, captured in a HIP graph.  Through the
     C-ABI with d_out2 = NULL the library's scratch is a stream-ordered
     allocation (a graph memory node); the Python wrapper passes a scratch from

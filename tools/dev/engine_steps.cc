@@ -8,13 +8,19 @@
 //   launch  sccsum_ipv4_frames per step on one stream, then one sync
 //   engine  one resident grid per run, sccsum_engine_submit per step
 //           (64 steps in flight), then a wait on the last step
+// With the argument `fill`, every step is an in-place fill of its slice
+// (SCCSUM_FILL_IP | SCCSUM_FILL_L4: the tx half, ip.cc:266-278, udp.cc:184-195):
+//   launch  sccsum_ipv4_fill per step (a generate and a store kernel)
+//   engine  a fill engine, sccsum_engine_submit_fill per step (two engine steps)
 // Prints one JSON line per size.  Build (tools/gpu_session.sh bin: step):
 //   hipcc -O2 -std=c++17 -I include tools/dev/engine_steps.cc -L seastar_amd/lib -lsccsum \
 //         -Wl,-rpath,$PWD/seastar_amd/lib -o tools/dev/engine_steps
 #include <hip/hip_runtime.h>
 #include <sccsum.h>
+#include <sccsum_diag.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -40,7 +46,9 @@ static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const bool fill = argc > 1 && std::strcmp(argv[1], "fill") == 0;
+    const uint32_t mode = SCCSUM_FILL_IP | SCCSUM_FILL_L4;
     const uint64_t n_all = 1 << 18;  // 262 144 frames, 393 MB
     const uint32_t L = 1500;
     std::vector<uint8_t> host(n_all * L);
@@ -58,11 +66,14 @@ int main() {
     std::vector<uint32_t> len(n_all, L);
     for (uint64_t i = 0; i < n_all; ++i) off[i] = i * L;
     SC_OK(sccsum_init(0));
+    if (const char* tb = std::getenv("ENGINE_STEPS_TILE_BYTES")) SC_OK(sccsum_set_tile_bytes(std::atoi(tb)));  // A/B
     void* d_bytes;
     uint64_t* d_off;
     uint32_t* d_len;
     uint8_t* d_st;
+    uint16_t* d_out2;
     HIP_OK(hipMalloc(&d_bytes, host.size() + 16));
+    HIP_OK(hipMalloc(&d_out2, n_all * 4));
     HIP_OK(hipMalloc(&d_off, n_all * 8));
     HIP_OK(hipMalloc(&d_len, n_all * 4));
     HIP_OK(hipMalloc(&d_st, n_all));
@@ -71,10 +82,12 @@ int main() {
     HIP_OK(hipMemcpy(d_len, len.data(), n_all * 4, hipMemcpyHostToDevice));
     hipStream_t s;
     HIP_OK(hipStreamCreate(&s));
-    const uint32_t sizes[] = {32, 128, 1024, 16384};
+    if (const char* fs = std::getenv("ENGINE_STEPS_FILL_SINGLE_MAX")) SC_OK(sccsum_set_fill_single_max(std::atoi(fs)));
+    const uint32_t sizes[] = {32, 128, 1024, 16384, 65536, 262144};
     for (uint32_t B : sizes) {
+        if (!fill && B > 16384) continue;
         const uint64_t slices = n_all / B;
-        const uint64_t k = B <= 128 ? 20000 : (B <= 1024 ? 5000 : 400);
+        const uint64_t k = B <= 128 ? 20000 : (B <= 1024 ? 5000 : (B <= 16384 ? 400 : 100));
         // a slice: B frames; its offsets are absolute in the one buffer (each step
         // reads its own B frames: distinct slices, rotating)
         auto slice = [&](uint64_t j) {
@@ -85,25 +98,26 @@ int main() {
             b.d_off = d_off + q * B;
             b.d_len = d_len + q * B;
             b.d_status = d_st + q * B;
+            b.d_out = fill ? d_out2 + 2 * q * B : nullptr;
             b.n = B;
             return b;
         };
+        auto launch = [&](const sccsum_batch& b) {
+            return fill ? sccsum_ipv4_fill(const_cast<void*>(b.d_bytes), b.bytes_len, b.d_off, b.d_len, static_cast<uint16_t*>(b.d_out),
+                                           b.d_status, B, L, mode, s)
+                        : sccsum_ipv4_frames(b.d_bytes, b.bytes_len, b.d_off, b.d_len, nullptr, b.d_status, B, L, s);
+        };
         // launches
-        for (uint64_t j = 0; j < 64; ++j) {
-            const sccsum_batch b = slice(j);
-            SC_OK(sccsum_ipv4_frames(b.d_bytes, b.bytes_len, b.d_off, b.d_len, nullptr, b.d_status, B, L, s));
-        }
+        for (uint64_t j = 0; j < 64; ++j) SC_OK(launch(slice(j)));
         HIP_OK(hipStreamSynchronize(s));
         double t0 = now_s();
-        for (uint64_t j = 0; j < k; ++j) {
-            const sccsum_batch b = slice(j);
-            SC_OK(sccsum_ipv4_frames(b.d_bytes, b.bytes_len, b.d_off, b.d_len, nullptr, b.d_status, B, L, s));
-        }
+        for (uint64_t j = 0; j < k; ++j) SC_OK(launch(slice(j)));
         HIP_OK(hipStreamSynchronize(s));
         const double launch_s = now_s() - t0;
         // engine
         sccsum_engine* e = nullptr;
-        SC_OK(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, static_cast<uint32_t>(k + 64), 64, &e));
+        SC_OK(sccsum_engine_create(0, SCCSUM_PIPE_IPV4 | (fill ? SCCSUM_ENGINE_FILL : 0),
+                                   static_cast<uint32_t>(2 * (k + 64)), 64, &e));
         double engine_s = 0;
         for (int run = 0; run < 2; ++run) {  // the first run warms up
             const uint64_t kk = run ? k : 64;
@@ -112,7 +126,11 @@ int main() {
             t0 = now_s();
             for (uint64_t j = 0; j < kk; ++j) {
                 const sccsum_batch b = slice(j);
-                SC_OK(sccsum_engine_submit(e, &b, 1, L, 10'000'000'000ull, &step));
+                if (fill) {
+                    SC_OK(sccsum_engine_submit_fill(e, &b, 1, L, mode, 10'000'000'000ull, &step));
+                } else {
+                    SC_OK(sccsum_engine_submit(e, &b, 1, L, 10'000'000'000ull, &step));
+                }
             }
             SC_OK(sccsum_engine_wait(e, step, 10'000'000'000ull));
             if (run) engine_s = now_s() - t0;
@@ -123,10 +141,10 @@ int main() {
         // (a timing probe: the checksum fields are random, so most frames fail their checks; the
         // engine's results are checked against the oracle by tests/test_gpu_engine.py)
         const double bytes = double(k) * B * L;
-        std::printf("{\"packets_per_step\": %u, \"steps\": %llu, \"launch_us_per_step\": %.2f, "
+        std::printf("{\"form\": \"%s\", \"packets_per_step\": %u, \"steps\": %llu, \"launch_us_per_step\": %.2f, "
                     "\"launch_GiBps\": %.1f, \"engine_us_per_step\": %.2f, \"engine_GiBps\": %.1f, "
                     "\"engine_over_launch\": %.2f}\n",
-                    B, (unsigned long long)k, launch_s / k * 1e6, bytes / launch_s / (1u << 30), engine_s / k * 1e6,
+                    fill ? "fill" : "verify", B, (unsigned long long)k, launch_s / k * 1e6, bytes / launch_s / (1u << 30), engine_s / k * 1e6,
                     bytes / engine_s / (1u << 30), launch_s / engine_s);
         std::fflush(stdout);
     }
