@@ -83,6 +83,8 @@ int main(int argc, char** argv) {
     hipStream_t s;
     HIP_OK(hipStreamCreate(&s));
     if (const char* fs = std::getenv("ENGINE_STEPS_FILL_SINGLE_MAX")) SC_OK(sccsum_set_fill_single_max(std::atoi(fs)));
+    if (const char* dy = std::getenv("ENGINE_STEPS_DYNAMIC")) SC_OK(sccsum_set_dynamic_tiles(std::atoi(dy)));  // A/B
+    if (const char* va = std::getenv("ENGINE_STEPS_VARIANT")) SC_OK(sccsum_set_kernel_variant(std::atoi(va)));  // A/B
     const uint32_t sizes[] = {32, 128, 1024, 16384, 65536, 262144};
     for (uint32_t B : sizes) {
         if (!fill && B > 16384) continue;
