@@ -2581,7 +2581,15 @@ hipError_t launch_rows(uint32_t max_len, hipStream_t s, int dev, const uint8_t* 
         const int occ = kernel_occupancy(reinterpret_cast<const void*>(kern));
         const uint64_t bpc = static_cast<uint64_t>(occ < t_knobs.blocks_per_cu ? occ : t_knobs.blocks_per_cu);
         const uint64_t cap = static_cast<uint64_t>(cu_count(dev)) * bpc;
-        uint64_t blocks = ((n + 63u) / 64u + kWavesPerBlock - 1) / kWavesPerBlock;  // a wave takes 64-packet tiles
+#ifdef SCCSUM_AB_ROWS_TILE64
+        uint64_t blocks = ((n + 63u) / 64u + kWavesPerBlock - 1) / kWavesPerBlock;  // A/B: 64-packet tiles
+#else
+        // waves for every four packets (one row step each) up to what the chip
+        // holds: a launch too small to fill the chip splits its packets evenly
+        // into short tiles (the kernel's last-round rule) instead of giving
+        // each of n / 64 waves 16 row steps one after another
+        uint64_t blocks = ((n + 3u) / 4u + kWavesPerBlock - 1) / kWavesPerBlock;
+#endif
         blocks = blocks < cap ? blocks : cap;
         blocks = (blocks + 7u) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
         return launch_kernel(kern, dim3(static_cast<unsigned>(blocks)), s, b, bytes_len, d_off, d_len, d_seed, d_out,
