@@ -2334,6 +2334,8 @@ constexpr int kRunAlign = 8;
 // against 332), where the stores inside the read stream cost more than the
 // store pass (profiles/r05_fill_one_pass.log)
 constexpr uint32_t kFillSingleMax = 262144;
+// Single-batch launches of at most this many packets run the row kernel (launch)
+constexpr uint64_t kSmallRowsMax = 65536;
 
 // Diagnostic knobs (include/sccsum_diag.h): per host thread, so one shard's
 // A/B settings never leak into another thread's launches.
@@ -2701,7 +2703,17 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
     const hipStream_t s = static_cast<hipStream_t>(stream);
     int dev = 0;
     if (const int rc = launch_device(s, &dev); rc != SCCSUM_OK) return rc;
-    const int variant = pick_variant(n, bytes_len, flags, max_len);
+    int variant = pick_variant(n, bytes_len, flags, max_len);
+    // a small single-batch launch runs the row kernel whatever the layout:
+    // four packets per wave in one row step reach the results sooner than the
+    // flat kernel's plan, scan and pick-up (dense 1500 B batches, eager: 32
+    // packets 4.2 against 6.4 us, 1 024 4.5 against 6.9, 16 384 8.4 against
+    // 11.3, 65 536 22.5 against 23.8; level at 262 144, 10 % slower at 1 M;
+    // profiles/r05_ab_rows_small.log).  In-place fills and fused RSS stay on
+    // the flat kernel, and multi launches too (the row kernel takes one batch).
+    if (t_knobs.variant == 0 && variant != 2 && n <= kSmallRowsMax && !(flags & kFillFlags) && rss.hash == nullptr) {
+        variant = 2;
+    }
     const uint8_t* b = static_cast<const uint8_t*>(d_bytes);
     if (variant == 1 || variant == 2) {
         hipError_t e = variant == 1
