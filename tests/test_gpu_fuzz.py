@@ -19,6 +19,8 @@ they must come back 0 with SCCSUM_ST_RANGE, and the oracle, which has no
 range checks, is asked only about the others.  Seeds are fixed, so a failure
 names its case and reproduces.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -29,6 +31,9 @@ from seastar_amd import batch, native, synth
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [0, 1, 2, 14, 15, 16]
+# SCCSUM_FUZZ_SCALE=k runs k times as many seeded cases per test (a deeper one-off run; the
+# default suite runs 1x)
+SCALE = max(1, int(os.environ.get("SCCSUM_FUZZ_SCALE", "1")))
 
 
 def _knobs(rng, lib, fill=False):
@@ -184,7 +189,7 @@ def _case_msg(case, kind, knobs, n):
     return f"case {case}: layout {kind}, n {n}, knobs {knobs}"
 
 
-@pytest.mark.parametrize("case", range(16))
+@pytest.mark.parametrize("case", range(16 * SCALE))
 def test_fuzz_spans(dev, case):
     rng = np.random.default_rng(1000 + case)
     lib = native.load()
@@ -213,7 +218,7 @@ def test_fuzz_spans(dev, case):
     assert np.all(got[bad] == 0) and np.all(gst[bad] == native.ST_RANGE), msg
 
 
-@pytest.mark.parametrize("case", range(16))
+@pytest.mark.parametrize("case", range(16 * SCALE))
 def test_fuzz_frames(dev, case):
     rng = np.random.default_rng(2000 + case)
     lib = native.load()
@@ -244,7 +249,7 @@ def test_fuzz_frames(dev, case):
     assert np.all(got[bad] == 0) and np.all(gst[bad] == native.ST_RANGE), msg
 
 
-@pytest.mark.parametrize("case", range(8))
+@pytest.mark.parametrize("case", range(8 * SCALE))
 def test_fuzz_multi(dev, case):
     """1..16 batches in one launch, spans or frames, each its own layout."""
     rng = np.random.default_rng(3000 + case)
@@ -312,7 +317,7 @@ FILL_MODES = [
 ]
 
 
-@pytest.mark.parametrize("case", range(16))
+@pytest.mark.parametrize("case", range(16 * SCALE))
 def test_fuzz_fill(dev, case):
     """In-place generate over disjoint frames (any order): the whole buffer,
     the values and the status must be the oracle's."""
@@ -345,7 +350,7 @@ def test_fuzz_fill(dev, case):
     assert np.all(gst[bad] == native.ST_RANGE), msg
 
 
-@pytest.mark.parametrize("case", range(4))
+@pytest.mark.parametrize("case", range(4 * SCALE))
 def test_fuzz_engine_steps(dev, case):
     """One engine run: random steps of 1..4 frame batches, and (fill engine)
     in-place fills between them, every step's results the oracle's."""
@@ -419,7 +424,7 @@ def test_fuzz_engine_steps(dev, case):
             assert np.array_equal(st.cpu().numpy(), wst), msg
 
 
-@pytest.mark.parametrize("case", range(8))
+@pytest.mark.parametrize("case", range(8 * SCALE))
 def test_fuzz_fragments(dev, case):
     """Packets as random fragment lists (odd lengths carry the byte order
     across fragments, empty fragments, fragments anywhere in the buffer)."""
@@ -448,7 +453,7 @@ def test_fuzz_fragments(dev, case):
     assert np.array_equal(st.cpu().numpy(), (want == 0).astype(np.uint8)), msg
 
 
-@pytest.mark.parametrize("case", range(8))
+@pytest.mark.parametrize("case", range(8 * SCALE))
 def test_fuzz_rss(dev, case):
     """Toeplitz RSS alone and fused into the frames pass, random keys of 4-52
     bytes, both hash modes, on the random frames above; the fused pass must
@@ -485,7 +490,7 @@ def test_fuzz_rss(dev, case):
     assert np.all(fst.cpu().numpy()[bad] == native.ST_RANGE), msg
 
 
-@pytest.mark.parametrize("case", range(6))
+@pytest.mark.parametrize("case", range(6 * SCALE))
 def test_fuzz_desc(dev, case):
     """Frames and spans as fragment descriptors in device memory or the
     stage buffer, cut at random points (inside headers too), fragments in a
@@ -528,7 +533,7 @@ def test_fuzz_desc(dev, case):
         assert np.array_equal(st[:n].cpu().numpy(), (want == 0).astype(np.uint8)), f"case {case}"
 
 
-@pytest.mark.parametrize("case", range(6))
+@pytest.mark.parametrize("case", range(6 * SCALE))
 def test_fuzz_burst(dev, case):
     """The burst queue with random batch limits, depth and delay, spans or
     frames, copied or zero-copy fragments, every fused form: results in
@@ -584,7 +589,7 @@ def test_fuzz_burst(dev, case):
     q.close()
 
 
-@pytest.mark.parametrize("case", range(8))
+@pytest.mark.parametrize("case", range(8 * SCALE))
 def test_fuzz_host_pipeline(dev, case):
     """Host batches through the pipeline with random chunk limits and depth,
     every gather form, spans or frames, packed or slot-shaped layouts."""
@@ -629,7 +634,7 @@ def test_fuzz_host_pipeline(dev, case):
         pl.close()
 
 
-@pytest.mark.parametrize("case", range(3))
+@pytest.mark.parametrize("case", range(3 * SCALE))
 def test_fuzz_engine_spans(dev, case):
     """A spans engine (SCCSUM_PIPE_SPANS): random steps of 1..4 seeded span
     batches, out-of-range entries included, every result the oracle's."""
@@ -674,7 +679,7 @@ def test_fuzz_engine_spans(dev, case):
             assert np.array_equal(it[2][:n].cpu().numpy(), wst), msg
 
 
-@pytest.mark.parametrize("case", range(4))
+@pytest.mark.parametrize("case", range(4 * SCALE))
 def test_fuzz_large_batches(dev, case):
     """100 k-300 k packets under random knobs: long claim chains per wave,
     the tail split over many tiles, grids capped at 1-3 blocks per CU."""
