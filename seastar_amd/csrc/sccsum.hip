@@ -610,12 +610,36 @@ __device__ __forceinline__ void tile_store(T* t, uint32_t lane, T v, uint32_t po
 // path cannot take (IP options, a trimmed IP length, over 128 KiB) are redone
 // exactly, one wave each (the flat kernel's phase D); results leave as one
 // coalesced store per tile.
-template <int V, bool IPV4>
+// Several batches in one row-kernel launch (MQ: small sccsum_*_multi
+// launches, whose batches would otherwise wait on the flat kernel's longer
+// plan): packet p of the launch is packet p - first[q] of batch q.
+constexpr uint32_t kRowQueues = 16;
+struct RowQueues {
+    uint32_t nq;
+    uint64_t first[kRowQueues + 1];
+    const uint8_t* bytes[kRowQueues];
+    uint64_t bytes_len[kRowQueues];
+    const uint64_t* off[kRowQueues];
+    const uint32_t* len[kRowQueues];
+    const uint32_t* seed[kRowQueues];
+    uint16_t* out[kRowQueues];
+    uint8_t* status[kRowQueues];
+};
+// a[q] for a lane-varying q with constant indices only (no private-memory copy of the argument)
+template <class T>
+__device__ __forceinline__ T row_pick(const T (&a)[kRowQueues], uint32_t q) {
+    T r = a[0];
+#pragma unroll
+    for (uint32_t i = 1; i < kRowQueues; ++i) r = q == i ? a[i] : r;
+    return r;
+}
+
+template <int V, bool IPV4, bool MQ = false>
 __global__ __launch_bounds__(kBlock) void csum_row_kernel(
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
     const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
-    uint8_t* __restrict__ status, uint64_t n, uint32_t flags) {
+    uint8_t* __restrict__ status, uint64_t n, uint32_t flags, const RowQueues rq) {
     constexpr uint32_t kRow = 16;
     const bool raw = !IPV4 && (flags & kFlagRaw);
     const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -645,14 +669,34 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
         // ---- A: lane k plans packet k of the tile (coalesced metadata loads)
         const uint64_t p = t0 + lane;
         const bool mine = lane < cnt;
-        const uint64_t o = mine ? off[p] : 0;
-        const uint32_t L = mine ? len[p] : 0u;
-        const uint32_t sd = (!IPV4 && seed && mine) ? seed[p] : 0u;
-        const bool range_bad = mine && (o > bytes_len || L > bytes_len - o);
+        // the packet's batch: the kernel's one, or (MQ) the one p falls in
+        const uint8_t* qbytes = bytes;
+        uint64_t qbytes_len = bytes_len, lp = p;
+        const uint64_t* qoff = off;
+        const uint32_t *qlen = len, *qseed = seed;
+        uint16_t* qout = out;
+        uint8_t* qstatus = status;
+        if constexpr (MQ) {
+            uint32_t q = 0;
+#pragma unroll
+            for (uint32_t i = 1; i < kRowQueues; ++i) q += (i < rq.nq && p >= rq.first[i]) ? 1u : 0u;
+            lp = p - row_pick(*reinterpret_cast<const uint64_t(*)[kRowQueues]>(rq.first), q);
+            qbytes = row_pick(rq.bytes, q);
+            qbytes_len = row_pick(rq.bytes_len, q);
+            qoff = row_pick(rq.off, q);
+            qlen = row_pick(rq.len, q);
+            qseed = row_pick(rq.seed, q);
+            qout = row_pick(rq.out, q);
+            qstatus = row_pick(rq.status, q);
+        }
+        const uint64_t o = mine ? qoff[lp] : 0;
+        const uint32_t L = mine ? qlen[lp] : 0u;
+        const uint32_t sd = (!IPV4 && qseed && mine) ? qseed[lp] : 0u;
+        const bool range_bad = mine && (o > qbytes_len || L > qbytes_len - o);
         const bool short_frame = IPV4 && mine && !range_bad && L < 20;
         const bool huge = mine && !range_bad && L > kExactMax;
         const bool fast = mine && !range_bad && !short_frame && !huge;
-        const uint64_t ptr = reinterpret_cast<uint64_t>(bytes) + (range_bad ? 0 : o);
+        const uint64_t ptr = reinterpret_cast<uint64_t>(qbytes) + (range_bad ? 0 : o);
         const uint32_t head = static_cast<uint32_t>(ptr & 15u);
         const uint64_t a0 = ptr - head;
         const uint32_t nunits = (fast && L) ? (head + L + 15u) >> 4 : 0u;
@@ -784,11 +828,11 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
         }
         if (mine) {
             if (IPV4) {
-                if (out) reinterpret_cast<uint32_t*>(out)[p] = word;
+                if (qout) reinterpret_cast<uint32_t*>(qout)[lp] = word;
             } else {
-                out[p] = static_cast<uint16_t>(word);
+                qout[lp] = static_cast<uint16_t>(word);
             }
-            if (status) status[p] = static_cast<uint8_t>(st);
+            if (qstatus) qstatus[lp] = static_cast<uint8_t>(st);
         }
     }
 }
@@ -2336,6 +2380,7 @@ constexpr int kRunAlign = 8;
 constexpr uint32_t kFillSingleMax = 262144;
 // Single-batch launches of at most this many packets run the row kernel (launch)
 constexpr uint64_t kSmallRowsMax = 65536;
+static_assert(kRowQueues >= kMaxQueues, "a multi launch's batches fit the row kernel's table");
 
 // Diagnostic knobs (include/sccsum_diag.h): per host thread, so one shard's
 // A/B settings never leak into another thread's launches.
@@ -2572,10 +2617,10 @@ hipError_t launch_simple(int uc, hipStream_t s, int dev, const uint8_t* b, uint6
     }
 }
 
-template <bool IPV4>
+template <bool IPV4, bool MQ = false>
 hipError_t launch_rows(uint32_t max_len, hipStream_t s, int dev, const uint8_t* b, uint64_t bytes_len,
                        const uint64_t* d_off, const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out,
-                       uint8_t* d_status, uint64_t n, uint32_t flags) {
+                       uint8_t* d_status, uint64_t n, uint32_t flags, const RowQueues& rq = RowQueues{}) {
     const uint64_t units = max_len ? (static_cast<uint64_t>(max_len) + 30u) / 16u : 128u;  // worst-case head of 15
     // the grid is what the chip holds at once (a grid-stride kernel: blocks
     // that only start when others end would make the tail)
@@ -2595,12 +2640,12 @@ hipError_t launch_rows(uint32_t max_len, hipStream_t s, int dev, const uint8_t* 
         blocks = blocks < cap ? blocks : cap;
         blocks = (blocks + 7u) & ~uint64_t(7);  // multiple of 8 for the XCD mapping
         return launch_kernel(kern, dim3(static_cast<unsigned>(blocks)), s, b, bytes_len, d_off, d_len, d_seed, d_out,
-                             d_status, n, flags);
+                             d_status, n, flags, rq);
     };
-    if (units <= 32) return go(csum_row_kernel<2, IPV4>);
-    if (units <= 64) return go(csum_row_kernel<4, IPV4>);
-    if (units <= 96) return go(csum_row_kernel<6, IPV4>);  // 1500 B frames: 95 units
-    return go(csum_row_kernel<8, IPV4>);
+    if (units <= 32) return go(csum_row_kernel<2, IPV4, MQ>);
+    if (units <= 64) return go(csum_row_kernel<4, IPV4, MQ>);
+    if (units <= 96) return go(csum_row_kernel<6, IPV4, MQ>);  // 1500 B frames: 95 units
+    return go(csum_row_kernel<8, IPV4, MQ>);
 }
 
 // Flat-kernel forms: 14 / 15 = U 8 (15: the next chunk in flight), 16 = U 16.
@@ -2761,6 +2806,27 @@ int launch_multi(const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
     int dev = 0;
     if (const int rc = launch_device(s, &dev); rc != SCCSUM_OK) return rc;
     const int variant = pick_variant(n_total, bytes_total, 0, max_len);
+    // a small multi launch runs the row kernel over all its batches at once
+    // (as a small single-batch launch does, launch(): 16 x 32 frames 6.3 ->
+    // profiles/r05_ab_rows_small.log)
+    if (t_knobs.variant == 0 && n_total <= kSmallRowsMax) {
+        RowQueues rq{};
+        for (uint32_t i = 0; i < nbatch; ++i) {
+            const sccsum_batch& x = batches[i];
+            if (!x.n) continue;
+            const uint32_t q = rq.nq++;
+            rq.first[q + 1] = rq.first[q] + x.n;
+            rq.bytes[q] = static_cast<const uint8_t*>(x.d_bytes);
+            rq.bytes_len[q] = x.bytes_len;
+            rq.off[q] = x.d_off;
+            rq.len[q] = x.d_len;
+            rq.seed[q] = x.d_seed;
+            rq.out[q] = static_cast<uint16_t*>(x.d_out);
+            rq.status[q] = x.d_status;
+        }
+        return static_cast<int>(launch_rows<IPV4, true>(max_len, s, dev, nullptr, 0, nullptr, nullptr, nullptr,
+                                                        nullptr, nullptr, n_total, 0, rq));
+    }
     if (variant == 1 || variant == 2) {  // the per-packet kernels take one batch per launch
         for (uint32_t i = 0; i < nbatch; ++i) {
             const sccsum_batch& x = batches[i];

@@ -252,14 +252,24 @@ def test_fuzz_frames(dev, case):
 @pytest.mark.parametrize("case", range(8 * SCALE))
 def test_fuzz_multi(dev, case):
     """1..16 batches in one launch, spans or frames, each its own layout."""
-    rng = np.random.default_rng(3000 + case)
+    _fuzz_multi(dev, case, np.random.default_rng(3000 + case), default_form=False)
+
+
+@pytest.mark.parametrize("case", range(8 * SCALE))
+def test_fuzz_multi_small_default_form(dev, case):
+    """Small multi launches (at most 65 536 packets) with the default kernel
+    choice: the multi-batch row kernel (one launch over every batch)."""
+    _fuzz_multi(dev, case, np.random.default_rng(3500 + case), default_form=True)
+
+
+def _fuzz_multi(dev, case, rng, default_form):
     lib = native.load()
     frames = case % 2 == 0
     nb = int(rng.integers(1, native.MAX_BATCHES + 1))
     items, wants = [], []
     for _ in range(nb):
-        n = int(rng.choice([0, 1, 40, 300, 1200]))
-        L = _lengths(rng, n, huge=False)
+        n = int(rng.choice([0, 1, 40, 300, 1200] if not default_form else [0, 1, 7, 64, 65, 300, 4000]))
+        L = _lengths(rng, n, huge=not default_form and case % 4 == 0)
         off, total, kind = _layout(rng, L)
         if kind == "shuffled":
             off, L = _shuffle_pairs(rng, off, L)
@@ -286,6 +296,9 @@ def test_fuzz_multi(dev, case):
             items.append((b, out, st, torch.from_numpy(want[1].view(np.int32)).to(dev)))
         wants.append(want)
     knobs = _knobs(rng, lib)
+    if default_form:
+        native.check(lib.sccsum_set_kernel_variant(0), "variant")
+        knobs["variant"] = 0
     if frames:
         batch.ipv4_frames_multi(items)
     else:
