@@ -244,7 +244,7 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  *       SCCSUM_FILL_ICMP_ECHO, optionally | SCCSUM_FILL_IP) of every batch
  *       (d_bytes is written; each batch's d_out, required here, gets the
  *       values stored and d_status the status bits).  A fill of at most
- *       262 144 frames (sccsum_set_fill_single_max) is ONE step whose tiles
+ *       524 288 frames (sccsum_set_fill_single_max) is ONE step whose tiles
  *       store the fields themselves; a larger one is two: a generate step into
  *       d_out and a store step whose tiles wait for it and write the values
  *       into the frames' fields (both or neither are published: such a fill

@@ -75,7 +75,7 @@ int sccsum_set_engine_sync_every(int steps);
 
 /* In-place fills (SCCSUM_FILL_L4 / SCCSUM_FILL_ICMP_ECHO, launches and engine
  * fill steps) of at most `frames` frames run in one pass: the generate tiles
- * store the fields themselves (default 262 144; 0 = always two passes).
+ * store the fields themselves (default 524 288; 0 = always two passes).
  * SCCSUM_EINVAL below 0. */
 int sccsum_set_fill_single_max(int frames);
 

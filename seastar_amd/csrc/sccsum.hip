@@ -2373,11 +2373,11 @@ constexpr int kOutPolicy = 1;
 constexpr int kRunAlign = 8;
 // In-place fills (FILL_L4 / FILL_ICMP_ECHO) of at most this many frames store
 // their fields from the generate tiles (kFlagFillNow) instead of a second pass.
-// One pass wins up to 262 144 frames (launch 88.3 against 92.1 us, engine 79.4
-// against 98.2) and loses at 1 M (launch 355 against 330 us, engine 342
-// against 332), where the stores inside the read stream cost more than the
-// store pass (profiles/r05_fill_one_pass.log)
-constexpr uint32_t kFillSingleMax = 262144;
+// One pass wins up to 512 Ki frames on rotated batches (launch 171.7 against
+// 181.3 us, engine 158.5 against 191.0) and loses at 1 Mi (launch 355 against
+// 330 us, engine 341.7 against 330), where the stores inside the read stream
+// cost more than the store pass (profiles/r05_fill_one_pass.log)
+constexpr uint32_t kFillSingleMax = 524288;
 // Single-batch launches of at most this many packets run the row kernel (launch)
 constexpr uint64_t kSmallRowsMax = 65536;
 static_assert(kRowQueues >= kMaxQueues, "a multi launch's batches fit the row kernel's table");
@@ -3481,6 +3481,8 @@ int sccsum_engine_submit_fill(sccsum_engine* e, const sccsum_batch* batches, uin
                            engine_tile(e, batches, nbatch, max_len));
         return SCCSUM_OK;
     }
+    // (cutting a 1 Mi-frame fill into two one-pass steps of 512 Ki did not help:
+    // 343.6 us a fill against 330 in two passes; profiles/r05_fill_one_pass.log)
     const uint64_t gen = engine_put(e, batches, nbatch, sccsum::kStepFillGen | (kflags << 8) | (uint64_t(mode) << 16),
                                     0, engine_tile(e, batches, nbatch, max_len));
     // the store half: no status (the generate half reported it)

@@ -130,7 +130,7 @@ class Batch(ctypes.Structure):
 
 
 MAX_BATCHES = 16
-FILL_SINGLE_MAX = 262144  # in-place fills of at most this many frames run in one pass (sccsum_diag.h)
+FILL_SINGLE_MAX = 524288  # in-place fills of at most this many frames run in one pass (sccsum_diag.h)
 ENGINE_MAX_BATCHES = 4
 
 

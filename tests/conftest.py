@@ -28,7 +28,7 @@ def dev():
 @pytest.fixture(params=[1, 2], ids=["one_pass", "two_pass"])
 def fill_passes(request, dev):
     """In-place fills in one pass (the generate tiles store the fields: the
-    default up to 262 144 frames) and in two (generate, then a store pass or
+    default up to 524 288 frames) and in two (generate, then a store pass or
     an engine store step): sccsum_set_fill_single_max, thread-local."""
     from seastar_amd import native
 

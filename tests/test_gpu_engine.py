@@ -176,7 +176,7 @@ def test_engine_grid_left_idle_leaves_on_its_own(dev):
 
 
 def test_engine_large_steps_property(dev):
-    """Bench-sized steps (2 x 262 144 x 1500 B frames, tx + verify-only rx) for
+    """Bench-sized steps (2 x 524 288 x 1500 B frames, tx + verify-only rx) for
     16 steps over 4 rotated batch pairs: every rx frame verifies except the
     corrupted ones, and every tx output equals a multi launch's."""
     from seastar_amd import devsynth
@@ -827,7 +827,7 @@ def test_engine_run_of_max_steps(dev):
 
 
 def test_engine_fill_single_pass_takes_one_step(dev):
-    """A fill of at most sccsum_set_fill_single_max frames (262 144 by default)
+    """A fill of at most sccsum_set_fill_single_max frames (524 288 by default)
     is ONE engine step whose tiles store the fields themselves: it returns
     that step, takes one of the run's steps (with one step left it still
     fits), and leaves the frames exactly as the oracle's writers do."""
@@ -859,3 +859,4 @@ def test_engine_fill_single_pass_takes_one_step(dev):
     assert np.array_equal(st.cpu().numpy(), want[2])
     assert np.array_equal(batch.as_u16(vout).reshape(-1, 2), vwant)
     eng.close()
+
