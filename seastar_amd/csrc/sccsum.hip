@@ -610,6 +610,30 @@ __device__ __forceinline__ void tile_store(T* t, uint32_t lane, T v, uint32_t po
 // path cannot take (IP options, a trimmed IP length, over 128 KiB) are redone
 // exactly, one wave each (the flat kernel's phase D); results leave as one
 // coalesced store per tile.
+// One checksum field of an in-place fill (2 bytes, little-endian as the
+// kernels hold it; byte stores at odd addresses).  kWriteThrough: sc0 sc1.
+template <bool kWriteThrough>
+__device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {
+    if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0u) {
+        if constexpr (kWriteThrough) {
+            __hip_atomic_store(gst(reinterpret_cast<uint16_t*>(p)), static_cast<uint16_t>(v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+#ifdef SCCSUM_AB_FILLSTORE_NT
+            __builtin_nontemporal_store(static_cast<uint16_t>(v), reinterpret_cast<uint16_t*>(p));
+#else
+            *gst(reinterpret_cast<uint16_t*>(p)) = static_cast<uint16_t>(v);
+#endif
+        }
+    } else if constexpr (kWriteThrough) {
+        __hip_atomic_store(gst(p), static_cast<uint8_t>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(gst(p + 1), static_cast<uint8_t>(v >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        gst(p)[0] = static_cast<uint8_t>(v);
+        gst(p)[1] = static_cast<uint8_t>(v >> 8);
+    }
+}
+
 // Several batches in one row-kernel launch (MQ: small sccsum_*_multi
 // launches, whose batches would otherwise wait on the flat kernel's longer
 // plan): packet p of the launch is packet p - first[q] of batch q.
@@ -634,20 +658,23 @@ __device__ __forceinline__ T row_pick(const T (&a)[kRowQueues], uint32_t q) {
     return r;
 }
 
-template <int V, bool IPV4, bool MQ = false>
+template <int V, bool IPV4, bool MQ = false, bool FILL = false>
 __global__ __launch_bounds__(kBlock) void csum_row_kernel(
     const uint8_t* __restrict__ bytes, uint64_t bytes_len,
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
     const uint32_t* __restrict__ seed, uint16_t* __restrict__ out,
     uint8_t* __restrict__ status, uint64_t n, uint32_t flags, const RowQueues rq) {
+    static_assert(!FILL || IPV4, "in-place fill is a frames mode");
     constexpr uint32_t kRow = 16;
     const bool raw = !IPV4 && (flags & kFlagRaw);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t r = lane & (kRow - 1), j = lane / kRow;  // lane r of row j
-    // per packet of the tile: units 0, 1, 2 and its last unit, for its finish
-    __shared__ u32x4 picks_all[kWavesPerBlock][kWave][4];
-    u32x4(*picks)[4] = picks_all[wv];
+    // per packet of the tile: units 0, 1, 2 (3 too for a fill: the TCP field
+    // may lie in it) and its last unit, for its finish
+    constexpr int kPick = FILL ? 5 : 4;
+    __shared__ u32x4 picks_all[kWavesPerBlock][kWave][kPick];
+    u32x4(*picks)[kPick] = picks_all[wv];
     const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
     const uint64_t wglob = static_cast<uint64_t>(xcd_block_id()) * kWavesPerBlock + wv;
     // 64-packet tiles dealt round robin for as many whole rounds of the grid
@@ -719,12 +746,12 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
                 }
 #pragma unroll
                 for (int u = 0; u < V; ++u) sum = sad4(v[u], sum);
-                if (g == 0 && r < 3) picks[k][r] = v[0];  // units 0..2 (zero past the packet)
+                if (g == 0 && r < static_cast<uint32_t>(kPick - 1)) picks[k][r] = v[0];  // units 0..2 (3) (zero past the packet)
                 // the lane holding the last unit (its unit u has lim - 1 == 16 u): select, then one store
                 u32x4 lastv = v[0];
 #pragma unroll
                 for (int u = 1; u < V; ++u) lastv = lim - 1 == 16 * u ? v[u] : lastv;
-                if (lim >= 1 && lim <= 16 * V && ((lim - 1) & 15) == 0) picks[k][3] = lastv;
+                if (lim >= 1 && lim <= 16 * V && ((lim - 1) & 15) == 0) picks[k][kPick - 1] = lastv;
             }
             // row sums (exact: < 2^32 up to kExactMax bytes), one per row, to the packets' lanes
             const uint32_t rsum = row_sum(sum);
@@ -737,10 +764,13 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
         __builtin_amdgcn_wave_barrier();  // the rows' LDS picks precede the lanes' reads
 
         // ---- C: lane k finishes packet k
-        u32x4 hs[4] = {picks[lane][0], picks[lane][1], picks[lane][2], u32x4{0, 0, 0, 0}};
-        const u32x4 hl = picks[lane][3];
+        u32x4 hs[4] = {picks[lane][0], picks[lane][1], picks[lane][2], FILL ? picks[lane][3] : u32x4{0, 0, 0, 0}};
+        const u32x4 hl = picks[lane][kPick - 1];
         __builtin_amdgcn_wave_barrier();  // this tile's reads precede the next tile's writes
-        const int rs0 = static_cast<int>(head) + (IPV4 ? 20 : 0);
+        // a fill's ICMP echo request: the reply's sum skips type, code and checksum (as flat_body)
+        const bool icmp_lane = FILL && (flags & kFlagFillIcmp) && mine && !range_bad && !short_frame &&
+                               ((header_dword(hs, head, 2) >> 8) & 0xffu) == 1u;
+        const int rs0 = static_cast<int>(head) + (IPV4 ? 20 + (icmp_lane ? 4 : 0) : 0);
         const int re0 = static_cast<int>(head + L);
         const int lastu16 = 16 * (static_cast<int>(nunits) - 1);
         uint32_t excl = unit_part(hs[0], 0, rs0);
@@ -749,9 +779,44 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
         const uint32_t kept = nunits ? res - excl : 0u;
         uint32_t S = fold16(kept);
         if (head & 1u) S = swap16(S);
-        uint32_t word = 0, st = 0, ipc = 0, pseudo = 0;
+        uint32_t word = 0, st = 0, ipc = 0, pseudo = 0, fpos = 0, srs = 0, sre = 0;
         bool slow = huge;  // (not streamed: phase D decodes its header from the frame)
-        if (IPV4) {
+        if (FILL) {
+            // in-place generate, one pass (the launch keeps huge frames off this
+            // kernel): flat_body's fill finish (phase C), then the stores below
+            const uint32_t h0 = header_dword(hs, head, 0), h1 = header_dword(hs, head, 1);
+            const uint32_t h2 = header_dword(hs, head, 2), h3 = header_dword(hs, head, 3);
+            const uint32_t h4 = header_dword(hs, head, 4);
+            const FrameDecode D = frame_decode(h0, h1, h2, h3, h4, L);
+            ipc = ~fold16(static_cast<uint64_t>(h0) + h1 + (h2 & 0xffffu) + h3 + h4) & 0xffffu;
+            st = D.st;
+            pseudo = D.pseudo;
+            const bool need = fast && (D.ihl != 5u || D.ip_len != L);
+            const bool atomic = (st & (SCCSUM_ST_MALFORMED | SCCSUM_ST_IPFRAG)) == 0u && D.ihl >= 5u;
+            uint32_t fo = 0;
+            if ((flags & kFlagFillL4) && (D.proto == 17u || D.proto == 6u)) fo = D.proto == 17u ? 6u : 16u;
+            if (icmp_lane && atomic && D.l4_len >= 8u) {
+                const uint32_t type = D.ihl == 5u ? header_dword(hs, head, 5) & 0xffu
+                                                  : reinterpret_cast<const uint8_t*>(a0)[head + D.l4_off];
+                fo = type == 8u ? 2u : 0u;
+            }
+            const bool has_field = fo != 0u && atomic && D.l4_len >= fo + 2u;
+            fpos = has_field ? head + D.l4_off + fo : 0u;
+            srs = head + D.l4_off + (icmp_lane ? 4u : 0u);
+            sre = head + D.l4_off + D.l4_len;
+            uint32_t rr;
+            if (icmp_lane) {
+                rr = ~S & 0xffffu;
+            } else {
+                uint32_t fv = 0;
+                if (has_field && !need) fv = fo == 6u ? header_dword(hs, head, 6) >> 16 : header_dword(hs, head, 9) & 0xffffu;
+                rr = ~fold16(static_cast<uint64_t>(S) + pseudo + (~fv & 0xffffu)) & 0xffffu;
+            }
+            const bool fill_ip = (flags & kFlagFillIp) != 0u;
+            word = (fill_ip ? ipc : 0u) | (has_field ? rr << 16 : 0u);
+            st |= (fill_ip ? SCCSUM_ST_OK : 0u) | (has_field ? SCCSUM_ST_L4_OK : 0u);
+            slow = need && has_field;
+        } else if (IPV4) {
             const uint32_t h0 = header_dword(hs, head, 0), h1 = header_dword(hs, head, 1);
             const uint32_t h2 = header_dword(hs, head, 2), h3 = header_dword(hs, head, 3);
             const uint32_t h4 = header_dword(hs, head, 4);
@@ -790,7 +855,10 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
             const uint32_t jL = __builtin_amdgcn_readlane(L, jl);
             uint64_t rs = jhead, re = static_cast<uint64_t>(jhead) + jL;
             uint32_t jipc = 0, jpseudo = 0, jst = 0;
-            if (IPV4) {
+            if (FILL) {  // the lane's own decisions from phase C (options or a trimmed IP length)
+                rs = static_cast<uint32_t>(__builtin_amdgcn_readlane(srs, jl));
+                re = static_cast<uint32_t>(__builtin_amdgcn_readlane(sre, jl));
+            } else if (IPV4) {
                 // the header from the frame itself (wave-uniform; over 128 KiB it was not picked
                 // up).  Dword 5 only when the header is not dword-aligned: for an aligned 20-byte
                 // frame it would lie past the frame, possibly past roundup(bytes_len, 16)
@@ -815,7 +883,15 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
             uint32_t SJ = exact_range_sum(ja0, rs, re, lane);
             if (jhead & 1u) SJ = swap16(SJ);
             if (lane == jl) {
-                if (IPV4) {
+                if (FILL) {
+                    uint32_t rr = ~SJ & 0xffffu;  // ICMP echo: the message after type, code, checksum
+                    if (!icmp_lane) {
+                        const uint8_t* fp = reinterpret_cast<const uint8_t*>(a0) + fpos;
+                        const uint32_t fv = static_cast<uint32_t>(fp[0]) | (static_cast<uint32_t>(fp[1]) << 8);
+                        rr = ~fold16(static_cast<uint64_t>(SJ) + pseudo + (~fv & 0xffffu)) & 0xffffu;
+                    }
+                    word = (word & 0xffffu) | (rr << 16);
+                } else if (IPV4) {
                     const uint32_t rr = ~fold16(static_cast<uint64_t>(SJ) + jpseudo) & 0xffffu;
                     word = frame_word(jipc, rr, jst);
                     st = frame_status(jipc, rr, jst);
@@ -824,6 +900,14 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
                     word = rr;
                     st = (!raw && rr == 0) ? SCCSUM_ST_OK : 0u;
                 }
+            }
+        }
+        if (FILL && mine) {  // the fields, after every read of the tile (st: which were generated)
+            uint8_t* const f0 = reinterpret_cast<uint8_t*>(a0);
+            if (st & SCCSUM_ST_OK) store_field<false>(f0 + head + 10, word);
+            if (st & SCCSUM_ST_L4_OK) {
+                if (icmp_lane) store_field<false>(f0 + fpos - 2, 0u);  // echo reply: type 0, code 0
+                store_field<false>(f0 + fpos, word >> 16);
             }
         }
         if (mine) {
@@ -1473,27 +1557,6 @@ __device__ __forceinline__ uint32_t fill_ld32(const uint32_t* q) {
         return __hip_atomic_load(gld(q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
         return *gld(q);
-    }
-}
-template <bool kWriteThrough>
-__device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {
-    if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0u) {
-        if constexpr (kWriteThrough) {
-            __hip_atomic_store(gst(reinterpret_cast<uint16_t*>(p)), static_cast<uint16_t>(v), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        } else {
-#ifdef SCCSUM_AB_FILLSTORE_NT
-            __builtin_nontemporal_store(static_cast<uint16_t>(v), reinterpret_cast<uint16_t*>(p));
-#else
-            *gst(reinterpret_cast<uint16_t*>(p)) = static_cast<uint16_t>(v);
-#endif
-        }
-    } else if constexpr (kWriteThrough) {
-        __hip_atomic_store(gst(p), static_cast<uint8_t>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(gst(p + 1), static_cast<uint8_t>(v >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {
-        gst(p)[0] = static_cast<uint8_t>(v);
-        gst(p)[1] = static_cast<uint8_t>(v >> 8);
     }
 }
 // What the store half reads of one frame: its value word and header bytes
@@ -2617,7 +2680,7 @@ hipError_t launch_simple(int uc, hipStream_t s, int dev, const uint8_t* b, uint6
     }
 }
 
-template <bool IPV4, bool MQ = false>
+template <bool IPV4, bool MQ = false, bool FILL = false>
 hipError_t launch_rows(uint32_t max_len, hipStream_t s, int dev, const uint8_t* b, uint64_t bytes_len,
                        const uint64_t* d_off, const uint32_t* d_len, const uint32_t* d_seed, uint16_t* d_out,
                        uint8_t* d_status, uint64_t n, uint32_t flags, const RowQueues& rq = RowQueues{}) {
@@ -2642,10 +2705,10 @@ hipError_t launch_rows(uint32_t max_len, hipStream_t s, int dev, const uint8_t* 
         return launch_kernel(kern, dim3(static_cast<unsigned>(blocks)), s, b, bytes_len, d_off, d_len, d_seed, d_out,
                              d_status, n, flags, rq);
     };
-    if (units <= 32) return go(csum_row_kernel<2, IPV4, MQ>);
-    if (units <= 64) return go(csum_row_kernel<4, IPV4, MQ>);
-    if (units <= 96) return go(csum_row_kernel<6, IPV4, MQ>);  // 1500 B frames: 95 units
-    return go(csum_row_kernel<8, IPV4, MQ>);
+    if (units <= 32) return go(csum_row_kernel<2, IPV4, MQ, FILL>);
+    if (units <= 64) return go(csum_row_kernel<4, IPV4, MQ, FILL>);
+    if (units <= 96) return go(csum_row_kernel<6, IPV4, MQ, FILL>);  // 1500 B frames: 95 units
+    return go(csum_row_kernel<8, IPV4, MQ, FILL>);
 }
 
 // Flat-kernel forms: 14 / 15 = U 8 (15: the next chunk in flight), 16 = U 16.
@@ -3714,6 +3777,14 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
         const uint32_t flags = ((mode & SCCSUM_FILL_L4) ? sccsum::kFlagFillL4 : 0u) |
                                ((mode & SCCSUM_FILL_ICMP_ECHO) ? sccsum::kFlagFillIcmp : 0u) |
                                ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u) | sccsum::kFlagFillNow;
+        // a small one (and no frame over the exact fast path's 128 KiB: the row
+        // kernel's fill finish reads each header from its picks) on the row kernel,
+        // as small verifies run (launch())
+        if (sccsum::t_knobs.variant == 0 && n <= sccsum::kSmallRowsMax && max_len != 0 && max_len <= sccsum::kExactMax) {
+            return static_cast<int>(sccsum::launch_rows<true, false, true>(
+                max_len, s, dev, static_cast<const uint8_t*>(d_bytes), bytes_len, d_off, d_len, nullptr, d_out2,
+                d_status, n, flags));
+        }
         return sccsum::launch<true>(d_bytes, bytes_len, d_off, d_len, nullptr, d_out2, d_status, n, max_len, stream,
                                     flags);
     }
