@@ -3201,6 +3201,7 @@ struct sccsum_engine {
     bool running = false, launched = false, left_recorded = false;
     uint64_t waves = 0;          // the running grid's waves (tile sizing)
     uint64_t next_step = 0, next_first = 0;
+    uint64_t last_tiled = ~0ull;  // the latest published step with tiles (a barrier's target), ~0 = none yet
     uint64_t done_floor = 0;     // every step below it is known done (engine_room)
     void* blk = nullptr;         // the device block: claims | mirror | sdone | counts | gdone (EngineBlock)
     bool dirty = true;           // the counts / gdone words may be nonzero (a run that gave up, or none yet)
@@ -3375,7 +3376,14 @@ uint64_t engine_put(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbat
     // per wave) synchronise; a stream of small steps keeps its pipeline full.
     int sync = sccsum::t_knobs.engine_sync_every;
     if (sync < 0) sync = ntiles >= 2 * e->waves ? static_cast<int>(sccsum::kEngineSyncEvery) : 0;
-    if (dep == 0 && sync > 0 && s > 0 && s % static_cast<uint64_t>(sync) == 0) d[sccsum::kEdDep] = s;
+    // The barrier waits for the latest step with tiles: a step without tiles
+    // is done in host memory only (below), and its device done word never
+    // rises, so waiting on it would hold the grid until the dependency limit
+    // (fuzz case 35 at 16x: a barrier step behind an empty step).
+    if (dep == 0 && sync > 0 && s > 0 && s % static_cast<uint64_t>(sync) == 0 && e->last_tiled != ~0ull) {
+        d[sccsum::kEdDep] = e->last_tiled + 1;
+    }
+    if (ntiles) e->last_tiled = s;
     if (ntiles == 0) {  // nothing to sum: done at once (the descriptor still keeps the walk in order)
         __atomic_store_n(e->ctl_h + sccsum::kEcDone + 8u * s, s + 1, __ATOMIC_RELEASE);
     }
@@ -3497,6 +3505,7 @@ int sccsum_engine_start(sccsum_engine* e, void* stream) {
     e->running = true;
     e->next_step = 0;
     e->next_first = 0;
+    e->last_tiled = ~0ull;
     e->done_floor = 0;
     e->dirty = false;  // (until this run is found to have given up)
     return SCCSUM_OK;

@@ -688,6 +688,46 @@ def test_engine_barrier_period(dev, sync_every):
     eng.close()
 
 
+def test_engine_barrier_behind_empty_steps(dev):
+    """A barrier step right behind a step without tiles (all its batches
+    empty) waits for the latest step that has tiles.  An empty step is done
+    in host memory only, so a barrier on it held the grid until the
+    dependency limit and the grid left with the barrier step's tiles unsummed
+    (the 16x fuzz run's case 35).  Barriers on every second step, with every
+    third step empty; each step is waited for, so a grid that gave up fails
+    here as SCCSUM_EIDLE."""
+    lib = native.load()
+    rng = np.random.default_rng(0xEB)
+    empty = batch.PacketBatch.from_host(np.zeros(1, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
+                                        device=dev)
+    empty_st = torch.zeros(1, dtype=torch.uint8, device=dev)
+    steps = []
+    for k in range(30):
+        if k % 3 == 1:
+            steps.append(None)
+            continue
+        b, want, want_st = _frames_step(rng, dev, int(rng.integers(0, 3)))
+        st = torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev)
+        steps.append((b, st, want_st))
+    torch.cuda.synchronize()
+    native.check(lib.sccsum_set_engine_sync_every(2), "sync_every")
+    eng = batch.Engine(0, frames=True, max_steps=64, max_in_flight=8)
+    try:
+        stream = torch.cuda.Stream(device=dev)
+        eng.start(stream)
+        ids = [eng.submit([(empty, None, empty_st)] if x is None else [(x[0], None, x[1])]) for x in steps]
+        for s in ids:
+            eng.wait(s, timeout_s=5.0)
+        eng.stop()
+        stream.synchronize()
+    finally:
+        lib.sccsum_set_engine_sync_every(-1)
+        eng.close()
+    for k, x in enumerate(steps):
+        if x is not None:
+            assert np.array_equal(x[1].cpu().numpy(), x[2]), f"step {k}"
+
+
 
 def test_engine_pacing_counts_every_older_step(dev):
     """Steps finish out of order: tiny steps behind a big one (2 M frames,
