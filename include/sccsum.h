@@ -254,8 +254,12 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  *       frames) before the fill is done.  max_len as for submit.
  *   sccsum_engine_wait(e, step, timeout_ns)   0 once the step is done
  *   sccsum_engine_stop(e)               no more steps: the grid leaves once the
- *       published steps are done (synchronise `stream` to wait for it)
- *   sccsum_engine_destroy(e)            stops and synchronises a running engine
+ *       published steps are done (synchronise `stream` to wait for it).  Its
+ *       SCCSUM_EIDLE only covers a give-up seen before the call: after the
+ *       stream sync, sccsum_engine_wait(e, step, 0) still answers for every
+ *       step of the run (0 done, SCCSUM_EIDLE if the grid gave up first)
+ *   sccsum_engine_destroy(e)            stops and synchronises a running engine;
+ *       SCCSUM_EIDLE if its last run gave up with steps unfinished
  *
  * Sharing the device.  The grid holds the device's compute units while it
  * runs (every CU, all of their LDS): kernels that other threads or streams

@@ -3589,6 +3589,10 @@ int sccsum_engine_destroy(sccsum_engine* e) {
     } else if (e->stream) {
         rc = static_cast<int>(hipStreamSynchronize(e->stream));
     }
+    // the grid has left: a give-up after the stop is visible now
+    if (rc == SCCSUM_OK && e->launched && __atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE)) {
+        rc = SCCSUM_EIDLE;
+    }
     (void)hipHostFree(e->ring_h);
     (void)hipHostFree(e->ctl_h);
     (void)hipFree(e->blk);
