@@ -74,6 +74,15 @@ def _default_knobs(dev):
     lib.sccsum_set_dynamic_tiles(1)
     lib.sccsum_set_blocks_per_cu(8)
     lib.sccsum_set_fill_single_max(native.FILL_SINGLE_MAX)
+    lib.sccsum_set_engine_sync_every(-1)
+
+
+def _engine_sync(case, lib, knobs):
+    """A random barrier period for an engine case (-1 auto, 0 never, k every k-th
+    step), from a generator of its own so the case's other draws stay as they were."""
+    k = int(np.random.default_rng(9000 + case).choice([-1, -1, 0, 1, 2, 3, 10]))
+    native.check(lib.sccsum_set_engine_sync_every(k), "sync_every")
+    knobs["sync_every"] = k
 
 
 def _lengths(rng, n, huge=True, lo=0):
@@ -371,6 +380,7 @@ def test_fuzz_engine_steps(dev, case):
     lib = native.load()
     fill = case % 2 == 1
     knobs = _knobs(rng, lib, fill=True)
+    _engine_sync(case, lib, knobs)
     # every step's batches are built before the run: while the grid runs, a
     # device-wide synchronize (or any kernel) would wait for its stop
     plan = []
@@ -661,6 +671,7 @@ def test_fuzz_engine_spans(dev, case):
     rng = np.random.default_rng(9900 + case)
     lib = native.load()
     knobs = _knobs(rng, lib, fill=True)
+    _engine_sync(case + 500, lib, knobs)
     plan = []
     for _ in range(int(rng.integers(5, 30))):
         items, wants = [], []
