@@ -520,7 +520,9 @@ int sccsum_gather(const sccsum_gather_desc* d_desc, uint64_t n, void* d_dst, voi
  * device batch; d_stage may be NULL when no fragment uses it).  A packet whose
  * fragments do not tile it gets result 0 and status SCCSUM_ST_RANGE; the
  * d_first entries themselves must index inside d_desc (not checked: the
- * descriptor count is not an argument).
+ * descriptor count is not an argument).  d_desc may be NULL when no packet has
+ * a fragment (every packet empty): each packet then has zero fragments, so an
+ * empty one gets the empty sum and a non-empty one 0 + SCCSUM_ST_RANGE.
  * Results and status as sccsum_spans / sccsum_ipv4_frames (frames: IPv4
  * header + L4, the header may be split across fragments).  d_desc, d_first,
  * d_off, d_len, d_seed, d_out, d_status: device arrays (aligned to their

@@ -256,9 +256,11 @@ def spans_multi(items, stream=None) -> list:
 def ipv4_fill(batch: PacketBatch, mode: int = native.FILL_IP | native.FILL_L4, out2: torch.Tensor | None = None,
               status: torch.Tensor | None = None, stream=None) -> torch.Tensor | None:
     """sccsum_ipv4_fill: generate checksums and store them in batch.data in
-    place.  FILL_L4 / FILL_ICMP_ECHO run two kernels on the stream (the
-    generate pass into out2, then the field-store pass); the header-only
-    modes one.  out2 / status are optional reports of what was stored;
+    place.  FILL_L4 / FILL_ICMP_ECHO read every byte: up to 524 288 frames
+    (sccsum_set_fill_single_max) in one pass whose tiles store the fields
+    themselves, a larger fill as two kernels on the stream (the generate pass
+    into out2, then the field-store pass); the header-only modes read only
+    the headers.  out2 / status are optional reports of what was stored;
     without out2 the generate pass's words go through a scratch buffer from
     torch's caching allocator (not the library's stream-ordered hipMallocAsync,
     which sits outside torch's pool and can fail when torch has cached most of
@@ -370,15 +372,15 @@ def _desc_call(name, desc, first, off, length, max_len, width, seeds, stage, out
     lib = native.load()
     n = int(off.numel())
     dev = off.device
-    if int(first.numel()) != n + 1 or first.dtype != torch.int32 or desc.dtype != torch.uint8:
-        raise ValueError(f"{name}: first must be int32 [n + 1] and desc uint8 records")
+    if int(first.numel()) != n + 1 or first.dtype != torch.int32 or (desc is not None and desc.dtype != torch.uint8):
+        raise ValueError(f"{name}: first must be int32 [n + 1] and desc uint8 records (or None: no fragments)")
     if out is None:
         out = _scratch(max(width * n, width), dev, stream, torch.int16)
     _need(length, n, torch.int32, "length", dev)
     _need(seeds, n, torch.int32, "seeds", dev)
     _need(out, width * n, torch.int16, "out", dev)
     _need(status, n, torch.uint8, "status", dev)
-    args = [ctypes_ptr(desc), ctypes_ptr(first), ctypes_ptr(off), ctypes_ptr(length)]
+    args = [_ptr(desc), ctypes_ptr(first), ctypes_ptr(off), ctypes_ptr(length)]
     if width == 1:
         args.append(_ptr(seeds))
     args += [None if stage is None else ctypes_ptr(stage), ctypes_ptr(out), _ptr(status), n, max_len, _stream(stream)]

@@ -767,6 +767,14 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
         u32x4 hs[4] = {picks[lane][0], picks[lane][1], picks[lane][2], FILL ? picks[lane][3] : u32x4{0, 0, 0, 0}};
         const u32x4 hl = picks[lane][kPick - 1];
         __builtin_amdgcn_wave_barrier();  // this tile's reads precede the next tile's writes
+        if (FILL && huge) {
+            // a frame over 128 KiB was not streamed (no row loaded it, so its
+            // picks hold another tile's bytes): its header straight from the
+            // frame — 64 bytes from a0, inside it — for the decisions below,
+            // and phase D sums it exactly (max_len is only a hint: ADVICE r05)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) hs[u] = load_unit(reinterpret_cast<const uint8_t*>(a0) + 16u * u);
+        }
         // a fill's ICMP echo request: the reply's sum skips type, code and checksum (as flat_body)
         const bool icmp_lane = FILL && (flags & kFlagFillIcmp) && mine && !range_bad && !short_frame &&
                                ((header_dword(hs, head, 2) >> 8) & 0xffu) == 1u;
@@ -782,8 +790,8 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
         uint32_t word = 0, st = 0, ipc = 0, pseudo = 0, fpos = 0, srs = 0, sre = 0;
         bool slow = huge;  // (not streamed: phase D decodes its header from the frame)
         if (FILL) {
-            // in-place generate, one pass (the launch keeps huge frames off this
-            // kernel): flat_body's fill finish (phase C), then the stores below
+            // in-place generate, one pass: flat_body's fill finish (phase C), then
+            // the stores below (a huge frame's L4 sum is phase D's exact redo)
             const uint32_t h0 = header_dword(hs, head, 0), h1 = header_dword(hs, head, 1);
             const uint32_t h2 = header_dword(hs, head, 2), h3 = header_dword(hs, head, 3);
             const uint32_t h4 = header_dword(hs, head, 4);
@@ -815,7 +823,7 @@ __global__ __launch_bounds__(kBlock) void csum_row_kernel(
             const bool fill_ip = (flags & kFlagFillIp) != 0u;
             word = (fill_ip ? ipc : 0u) | (has_field ? rr << 16 : 0u);
             st |= (fill_ip ? SCCSUM_ST_OK : 0u) | (has_field ? SCCSUM_ST_L4_OK : 0u);
-            slow = need && has_field;
+            slow = (need || huge) && has_field;
         } else if (IPV4) {
             const uint32_t h0 = header_dword(hs, head, 0), h1 = header_dword(hs, head, 1);
             const uint32_t h2 = header_dword(hs, head, 2), h3 = header_dword(hs, head, 3);
@@ -2817,8 +2825,9 @@ int launch(const void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const
     // flat kernel's plan, scan and pick-up (dense 1500 B batches, eager: 32
     // packets 4.2 against 6.4 us, 1 024 4.5 against 6.9, 16 384 8.4 against
     // 11.3, 65 536 22.5 against 23.8; level at 262 144, 10 % slower at 1 M;
-    // profiles/r05_ab_rows_small.log).  In-place fills and fused RSS stay on
-    // the flat kernel, and multi launches too (the row kernel takes one batch).
+    // profiles/r05_ab_rows_small.log).  In-place fills (sccsum_ipv4_fill picks
+    // its own kernel) and fused RSS stay on the flat kernel here; small multi
+    // launches take the row kernel's several-batch form (launch_multi).
     if (t_knobs.variant == 0 && variant != 2 && n <= kSmallRowsMax && !(flags & kFillFlags) && rss.hash == nullptr) {
         variant = 2;
     }
@@ -3002,7 +3011,7 @@ __global__ __launch_bounds__(kBlock) void csum_desc_kernel(
             m_off = off[q];
             m_len = len[q];
             m_f0 = first[q];
-            m_f1 = first[q + 1];
+            m_f1 = desc ? first[q + 1] : m_f0;  // no descriptor array: no packet has fragments
         }
         if (q < n && m_f1 > m_f0) {
             const sccsum_gather_desc d = desc[m_f0];
@@ -3149,7 +3158,10 @@ int launch_desc(const sccsum_gather_desc* d_desc, const uint32_t* d_first, const
                 const uint32_t* d_len, const uint32_t* d_seed, const void* d_stage, uint16_t* d_out, uint8_t* d_status,
                 uint64_t n, uint32_t max_len, void* stream) {
     if (n == 0) return SCCSUM_OK;
-    if (!d_desc || !d_first || !d_off || !d_len || !d_out || (reinterpret_cast<uintptr_t>(d_desc) & 7u) ||
+    // d_desc may be NULL (an rx burst of empty packets has no fragments): the
+    // kernel then gives every packet zero fragments, so an empty one sums to
+    // the empty sum and a non-empty one is SCCSUM_ST_RANGE
+    if (!d_first || !d_off || !d_len || !d_out || (reinterpret_cast<uintptr_t>(d_desc) & 7u) ||
         (reinterpret_cast<uintptr_t>(d_first) & 3u) || (reinterpret_cast<uintptr_t>(d_off) & 7u) ||
         (reinterpret_cast<uintptr_t>(d_len) & 3u) || (reinterpret_cast<uintptr_t>(d_seed) & 3u) ||
         (reinterpret_cast<uintptr_t>(d_out) & (IPV4 ? 3u : 1u))) {
@@ -3790,9 +3802,10 @@ int sccsum_ipv4_fill(void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, c
         const uint32_t flags = ((mode & SCCSUM_FILL_L4) ? sccsum::kFlagFillL4 : 0u) |
                                ((mode & SCCSUM_FILL_ICMP_ECHO) ? sccsum::kFlagFillIcmp : 0u) |
                                ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u) | sccsum::kFlagFillNow;
-        // a small one (and no frame over the exact fast path's 128 KiB: the row
-        // kernel's fill finish reads each header from its picks) on the row kernel,
-        // as small verifies run (launch())
+        // a small one on the row kernel, as small verifies run (launch()), when
+        // max_len says its frames fit the exact fast path (128 KiB).  max_len is
+        // only a hint: a longer frame there is summed by the row kernel's exact
+        // redo, its header read from the frame, just more slowly
         if (sccsum::t_knobs.variant == 0 && n <= sccsum::kSmallRowsMax && max_len != 0 && max_len <= sccsum::kExactMax) {
             return static_cast<int>(sccsum::launch_rows<true, false, true>(
                 max_len, s, dev, static_cast<const uint8_t*>(d_bytes), bytes_len, d_off, d_len, nullptr, d_out2,

@@ -55,8 +55,11 @@ static void checks() {
     // fragment lists: nothing to do, then null / misaligned arrays
     EXPECT(sccsum_ipv4_frames_desc(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr) ==
            SCCSUM_OK);
-    EXPECT(sccsum_ipv4_frames_desc(nullptr, static_cast<const uint32_t*>(d16), static_cast<const uint64_t*>(d16),
+    EXPECT(sccsum_ipv4_frames_desc(nullptr, nullptr, static_cast<const uint64_t*>(d16),
                                    static_cast<const uint32_t*>(d16), nullptr, static_cast<uint16_t*>(d16), nullptr, 2,
+                                   64, nullptr) == SCCSUM_EINVAL);
+    EXPECT(sccsum_ipv4_frames_desc(nullptr, static_cast<const uint32_t*>(d16), static_cast<const uint64_t*>(d16),
+                                   static_cast<const uint32_t*>(d16), nullptr, static_cast<uint16_t*>(odd), nullptr, 2,
                                    64, nullptr) == SCCSUM_EINVAL);
     EXPECT(sccsum_spans_desc(static_cast<const sccsum_gather_desc*>(odd), static_cast<const uint32_t*>(d16),
                              static_cast<const uint64_t*>(d16), static_cast<const uint32_t*>(d16), nullptr, nullptr,
@@ -175,6 +178,14 @@ static void checks() {
                                 static_cast<uint16_t*>(d16), nullptr, 3, 0, SCCSUM_FILL_IP | SCCSUM_FILL_L4,
                                 nullptr) > 0);
         EXPECT(sccsum_read_probe(d16, 64, static_cast<uint64_t*>(d16), nullptr) > 0);
+        // a NULL descriptor array is accepted (no packet has fragments: an empty rx burst), so the
+        // call gets as far as the launch device
+        EXPECT(sccsum_ipv4_frames_desc(nullptr, static_cast<const uint32_t*>(d16), static_cast<const uint64_t*>(d16),
+                                       static_cast<const uint32_t*>(d16), nullptr, static_cast<uint16_t*>(d16),
+                                       nullptr, 2, 64, nullptr) > 0);
+        EXPECT(sccsum_spans_desc(nullptr, static_cast<const uint32_t*>(d16), static_cast<const uint64_t*>(d16),
+                                 static_cast<const uint32_t*>(d16), nullptr, nullptr, static_cast<uint16_t*>(d16),
+                                 nullptr, 2, 0, nullptr) > 0);
     }
     // host arithmetic and strings
     EXPECT(sccsum_pseudo_seed(1, 2, 17, 8) == 28u);

@@ -149,7 +149,9 @@ def test_desc_argument_validation_without_device():
     lib = native.load()
     p = 0x10000
     assert lib.sccsum_ipv4_frames_desc(None, None, None, None, None, None, None, 0, 0, None) == native.SCCSUM_OK
-    assert lib.sccsum_ipv4_frames_desc(None, p, p, p, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
+    # a NULL descriptor array is accepted (no packet has fragments), the other arrays are still checked
+    assert lib.sccsum_ipv4_frames_desc(None, p, p, p, None, p + 2, None, 4, 64, None) == native.SCCSUM_EINVAL
+    assert lib.sccsum_ipv4_frames_desc(None, None, p, p, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
     assert lib.sccsum_ipv4_frames_desc(p, None, p, p, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
     assert lib.sccsum_spans_desc(p + 4, p, p, p, None, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL
     assert lib.sccsum_spans_desc(p, p + 2, p, p, None, None, p, None, 4, 64, None) == native.SCCSUM_EINVAL

@@ -278,7 +278,8 @@ def _fuzz_multi(dev, case, rng, default_form):
     items, wants = [], []
     for _ in range(nb):
         n = int(rng.choice([0, 1, 40, 300, 1200] if not default_form else [0, 1, 7, 64, 65, 300, 4000]))
-        L = _lengths(rng, n, huge=not default_form and case % 4 == 0)
+        # (default form: huge frames reach the several-batch row kernel's exact redo)
+        L = _lengths(rng, n, huge=case % 4 == 0)
         off, total, kind = _layout(rng, L)
         if kind == "shuffled":
             off, L = _shuffle_pairs(rng, off, L)
@@ -297,6 +298,8 @@ def _fuzz_multi(dev, case, rng, default_form):
             w[ok] = oracle.batch_spans(buf, off[ok], L[ok], seeds[ok])
             want = (w, seeds, bad)
         b = batch.PacketBatch.from_host(buf[:total], off, L, device=dev)
+        if default_form and case % 8 == 0:
+            b.max_len = min(b.max_len, 1500)  # a hint only (include/sccsum.h): understated, still exact
         st = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
         out = torch.empty(max((2 if frames else 1) * n, 2), dtype=torch.int16, device=dev)
         if frames:
@@ -356,6 +359,12 @@ def test_fuzz_fill(dev, case):
     mode = FILL_MODES[case % len(FILL_MODES)]
     knobs = _knobs(rng, lib, fill=True)
     b = batch.PacketBatch.from_host(buf[:total], off, L, device=dev)
+    if case % 8 == 0:
+        # max_len is a hint (include/sccsum.h): understated below frames over 128 KiB, a small
+        # fill still takes the row kernel, whose exact redo must read those headers from the
+        # frames themselves
+        b.max_len = int(rng.choice([64, 1500, 9000, 131072]))
+        knobs["max_len"] = b.max_len
     out2 = torch.empty(2 * n, dtype=torch.int16, device=dev)
     st = torch.empty(n, dtype=torch.uint8, device=dev)
     batch.ipv4_fill(b, mode, out2=out2, status=st)
@@ -539,8 +548,8 @@ def test_fuzz_desc(dev, case):
     desc, first, lay_off, pool, stage = _scatter(rng, buf, off, L, pool_t.data_ptr(), pool_len,
                                                  stage_frac=0.3 if case % 3 == 0 else 0.0)
     pool_t.copy_(torch.from_numpy(pool))
-    # (no descriptors at all when every packet is empty: the C-ABI still wants a descriptor array)
-    dd = torch.from_numpy(desc.view(np.uint8) if desc.size else np.zeros(16, np.uint8)).to(dev)
+    # no descriptors at all when every packet is empty: the C-ABI then takes a NULL array
+    dd = torch.from_numpy(desc.view(np.uint8)).to(dev) if desc.size else None
     df = torch.from_numpy(first).to(dev)
     doff = torch.from_numpy(lay_off.view(np.int64)).to(dev)
     dlen = torch.from_numpy(L.view(np.int32)).to(dev)
