@@ -447,6 +447,18 @@ def default_launch(args, launches: str) -> str:
     return launches if args.share_devices else "engine"
 
 
+def launch_form(args) -> str:
+    """The launch form a config's timed run uses (per_rank's "launch": an
+    N-GPU line says what each rank ran, VERDICT r05 #4)."""
+    if args.config == "udp1500":
+        return args.launch or default_launch(args, "multi")
+    if args.config == "mixed":
+        return args.launch or default_launch(args, "single")
+    if args.config == "fill":
+        return "engine" if args.launch == "engine" else "single"
+    return {"tcp64k": "single", "slots": "single", "frags": "single", "e2e": "pipeline", "sweep": "sweep"}[args.config]
+
+
 def make_streams(args, dev):
     """The step's launch streams: step k goes to streams[k % S].  Default 1 =
     the current stream, one launch at a time, so a launch's duration is the
@@ -463,14 +475,16 @@ def make_streams(args, dev):
 OWN = {}  # this rank's own timing of the last timed() region (per_rank diagnostics)
 
 
-def timed(step, steps, warmup, world, streams, begin=None, end=None):
+def timed(step, steps, warmup, world, streams, begin=None, end=None, between=None):
     """Warm up, then time `steps` calls bracketed by barrier + sync; returns
     (max-over-ranks wall seconds, seconds per step from ONE pair of HIP events
     around the timed launches: the start event on streams[0], which every other
     stream waits on, the end event on streams[0] after it has waited on every
     other stream).  An event between every two launches leaves the GPU idle
     ~5 us at each (a timestamp packet), which per-launch events would add to
-    the wall time."""
+    the wall time.  between(): called after the warm-up, before
+    the timed region (outside it): e.g. poisoning outputs the timed steps must
+    rewrite, so a check afterwards sees that they ran."""
     import gc
 
     streams = streams if isinstance(streams, (list, tuple)) else [streams]
@@ -481,12 +495,12 @@ def timed(step, steps, warmup, world, streams, begin=None, end=None):
     gc.collect()
     gc.disable()
     try:
-        return _timed(step, steps, warmup, world, streams, s0, begin, end)
+        return _timed(step, steps, warmup, world, streams, s0, begin, end, between)
     finally:
         gc.enable()
 
 
-def _timed(step, steps, warmup, world, streams, s0, begin, end):
+def _timed(step, steps, warmup, world, streams, s0, begin, end, between):
     if warmup:
         if begin:  # (--launch engine: a run of its own)
             begin()
@@ -495,6 +509,9 @@ def _timed(step, steps, warmup, world, streams, s0, begin, end):
         if end:
             end()
     torch.cuda.synchronize()
+    if between:
+        between()
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world)
     torch.cuda.synchronize()
@@ -658,9 +675,10 @@ def run_udp1500(args, world, rank, dev):
     if R % len(streams):  # a batch (and its status buffer) must always come back to the same stream
         streams = streams[:1]
     ns = len(streams)
-    # one result buffer per stream: steps on different streams may overlap
+    # one result buffer pair per rotation (a rotation always comes back to the same stream), so the
+    # timed run's outputs of every rotation can be checked against the warm-up's afterwards
     outs = [(torch.empty(2 * n, dtype=torch.int16, device=dev), torch.empty(2 * n, dtype=torch.int16, device=dev))
-            for _ in range(ns)]
+            for _ in range(R)]
     out_tx = outs[0][0]
     g = torch.Generator(device=dev)
     g.manual_seed(SEED + rank)
@@ -689,37 +707,33 @@ def run_udp1500(args, world, rank, dev):
     pre = {}
     if multi:
         for r in range(R):
-            for i in range(ns):
-                o_tx, o_rx = outs[i]
-                pre[(r, i)] = batch.prepare_ipv4_frames_multi([(txs[r], o_tx, None),
-                                                               (rxs[r], o_rx if args.rx_out2 else None, sts[r])])
+            o_tx, o_rx = outs[r]
+            pre[r] = batch.prepare_ipv4_frames_multi([(txs[r], o_tx, None),
+                                                      (rxs[r], o_rx if args.rx_out2 else None, sts[r])])
 
     warm = max(args.warmup, R)
     eng = begin = end = None
     if engine:
-        eng = batch.Engine(dev.index or 0, frames=True, max_steps=max(warm, args.steps) + 4,
-                           max_in_flight=args.engine_in_flight)
-        o_tx, o_rx = outs[0]
-        pre = {r: eng.prepare([(txs[r], o_tx, None), (rxs[r], o_rx if args.rx_out2 else None, sts[r])])
+        eng = batch.Engine(dev.index or 0, frames=True, ring_slots=1024, max_in_flight=args.engine_in_flight)
+        pre = {r: eng.prepare([(txs[r], outs[r][0], None), (rxs[r], outs[r][1] if args.rx_out2 else None, sts[r])])
                for r in range(R)}
 
         def begin():
             eng.start(streams[0])
 
         def end():
-            eng.stop()
+            eng.finish()  # waits on the run's last step (a give-up raises), then stops the grid
 
     def step(k):
         r = k % R
         s = streams[k % ns]
-        o_tx, o_rx = outs[k % ns]
         if engine:
             eng.submit_prepared(pre[r])
         elif multi:
-            pre[(r, k % ns)](s)
+            pre[r](s)
         else:
-            batch.ipv4_frames(txs[r], out2=o_tx, stream=s)
-            batch.ipv4_frames(rxs[r], out2=o_rx, status=sts[r], stream=s)
+            batch.ipv4_frames(txs[r], out2=outs[r][0], stream=s)
+            batch.ipv4_frames(rxs[r], out2=outs[r][1], status=sts[r], stream=s)
 
     torch.cuda.synchronize()  # the batches were built on the default stream
     if begin:
@@ -734,11 +748,32 @@ def run_udp1500(args, world, rank, dev):
     for st_rx in sts:
         n_fail = int(((st_rx & 2) == 0).sum())
         assert args.no_check or n_fail == bad.numel(), f"verify failures {n_fail} != corrupted {bad.numel()}"
+    # the warm-up's results per rotation; the timed run's are checked against them afterwards (VERDICT r05:
+    # the timed region itself was never checked), its outputs poisoned first so that a step that never ran
+    # shows: 0xFFFF is no IPv4 or UDP checksum of these frames (~fold(sum) is 0xFFFF only for a zero sum)
+    want_tx = [o[0].clone() for o in outs]
+    want_st = [s.clone() for s in sts]
+    ran = sorted({k % R for k in range(args.steps)})
+
+    def poison():
+        for r in ran:
+            outs[r][0].fill_(-1)
+            sts[r].fill_(0xEE)
+
     sel = LAUNCHES.select(kern, 1 if engine else per_step * args.steps)
-    wall, step_s = timed(step, args.steps, 0, world, streams, begin, end)
+    wall, step_s = timed(step, args.steps, 0, world, streams, begin, end, between=None if args.no_check else poison)
     LAUNCHES.add(kern, 1 if engine else per_step * args.steps)
     avg_launch_s = step_s / per_step
     stream = streams[0]
+    if engine:
+        eng.close()  # raises if the run left a published step undone (sccsum_engine_destroy)
+    if not args.no_check:  # outside the timed region
+        torch.cuda.synchronize()
+        for r in ran:
+            n_fail = int(((sts[r] & 2) == 0).sum())
+            assert n_fail == bad.numel(), f"timed run, rotation {r}: verify failures {n_fail} != {bad.numel()}"
+            assert torch.equal(sts[r], want_st[r]), f"timed run, rotation {r}: rx status differs from the warm-up's"
+            assert torch.equal(outs[r][0], want_tx[r]), f"timed run, rotation {r}: tx checksums differ from the warm-up's"
 
     value = world * 2 * n * FRAME * args.steps / wall / 2**30
     # per launch: every frame byte + 12 B metadata + the results written: tx 4 B (IP, UDP checksums), rx 1 B
@@ -748,10 +783,9 @@ def run_udp1500(args, world, rank, dev):
     roof_alg, roof_s = alg, avg_launch_s
     if engine:  # the launch is the run: every step's bytes over the run's time (the same ratio)
         roof_alg, roof_s = alg * args.steps, avg_launch_s * args.steps
-        eng.close()
     ceiling = read_ceiling(txs[0].data, txs[0].bytes_len, stream)
     ranks = per_rank(world, rank, dev, **rank_rate(2 * n * FRAME, args.steps), avg_launch_us=avg_launch_s * 1e6,
-                     read_ceiling_GBps=ceiling, frac=alg / avg_launch_s / 1e9 / HBM_PEAK_GBPS)
+                     read_ceiling_GBps=ceiling, frac=alg / avg_launch_s / 1e9 / HBM_PEAK_GBPS, launch=args.launch)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(txs[0], args.cpu_seconds)
@@ -765,6 +799,11 @@ def run_udp1500(args, world, rank, dev):
                                f"batches submitted into it as one step, at most {args.engine_in_flight} steps in flight" if engine
                                else "one sccsum_ipv4_frames launch per batch (2 per step)")),
               "rotation": f"{R} distinct tx/rx batch pairs launched in turn ({2 * R * n * FRAME / 1e9:.1f} GB per GPU)",
+              "timed_run_checked": (None if args.no_check else
+                                    "after the timed region: every rotation's rx status and tx checksums equal the "
+                                    "warm-up's (outputs poisoned before it), failures == corrupted frames"
+                                    + ("; the run waited on its last step and its engine closed clean" if engine
+                                       else "")),
               "streams": f"{ns} (step k on stream k % {ns})",
               "global_batch": n * world, "parallelism": f"{world} independent shards, no collective"},
              roofline(roof_alg, roof_s, "udp1500" if not engine else "udp1500_engine",
@@ -870,8 +909,7 @@ def run_mixed(args, world, rank, dev):
     step, begin, end, eng = (lambda k: pre[(k % R, k % ns)](streams[k % ns])), None, None, None
     if engine:  # the single form's steps, submitted into one resident grid per run
         kern = "csum_engine_kernel<16, true, false>"
-        eng = batch.Engine(dev.index or 0, frames=True, max_steps=max(warm, args.steps) + 4,
-                           max_in_flight=args.engine_in_flight)
+        eng = batch.Engine(dev.index or 0, frames=True, ring_slots=1024, max_in_flight=args.engine_in_flight)
         pre_e = {r: eng.prepare([(rxs[r], None, sts[r]) if vonly else (rxs[r], outs[0][1], None)]) for r in range(R)}
 
         def step(k):
@@ -880,10 +918,25 @@ def run_mixed(args, world, rank, dev):
         def begin():
             eng.start(streams[0])
 
-        end = eng.stop
+        end = eng.finish  # waits on the run's last step (a give-up raises), then stops the grid
     LAUNCHES.add(kern, 1 if engine else warm)
     sel = LAUNCHES.select(kern, 1 if engine else args.steps)
-    wall, launch_s = timed(step, args.steps, warm, world, streams, begin, end)
+    # the timed run's statuses are checked afterwards (every frame verifies): poisoned before it, so
+    # a step that never ran shows (the single form's status-only steps)
+    ran = sorted({k % R for k in range(warm, warm + args.steps)})
+    check_st = vonly and not args.no_check
+
+    def poison():
+        for r in ran:
+            sts[r].fill_(0xEE)
+
+    wall, launch_s = timed(step, args.steps, warm, world, streams, begin, end, between=poison if check_st else None)
+    if engine:
+        eng.close()  # raises if the run left a published step undone
+    if check_st:
+        torch.cuda.synchronize()
+        for r in ran:
+            assert int((sts[r] != 3).sum()) == 0, f"timed run, rotation {r}: frames that do not verify"
     # per launch: every frame byte + 12 B metadata + the results: 4 B per frame, except a multi step's rx
     # half, which writes 1 B of status bits (+ 4 B with --rx-out2)
     alg = (total + n * (META_BYTES + 4) + n * (META_BYTES + 1 + (4 if args.rx_out2 else 0)) if multi
@@ -891,10 +944,9 @@ def run_mixed(args, world, rank, dev):
     roof_alg, roof_s = alg, launch_s
     if engine:  # the launch is the run: every step's bytes over the run's time (the same ratio)
         roof_alg, roof_s = alg * args.steps, launch_s * args.steps
-        eng.close()
     ceiling = read_ceiling(rxs[0].data, rxs[0].bytes_len, stream)
     ranks = per_rank(world, rank, dev, **rank_rate(nbytes, args.steps), avg_launch_us=launch_s * 1e6,
-                     read_ceiling_GBps=ceiling, frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS)
+                     read_ceiling_GBps=ceiling, frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS, launch=args.launch)
     # the gap bytes a step's batches hold between their frames (--align 64: layout (ii))
     gap = (rxs[0].bytes_len + (txs[0].bytes_len if multi else 0)) - total
     lay = layout_traffic(alg, gap, total, alg / launch_s / 1e9 / HBM_PEAK_GBPS)
@@ -1087,7 +1139,7 @@ def run_fill(args, world, rank, dev):
     begin = end = eng = None
     if engine:  # one resident grid per timed run; each step = one fill (generate step + store step)
         kern = "csum_engine_kernel<16, true, true>"
-        eng = batch.Engine(dev.index or 0, frames=True, fill=True, max_steps=2 * max(warm, args.steps) + 4,
+        eng = batch.Engine(dev.index or 0, frames=True, fill=True, ring_slots=1024,
                            max_in_flight=max(2, args.engine_in_flight))
         # one out2 per batch: a fill's store step reads its generate step's values from out2 while
         # the next fills run (sccsum.h: no other step may write a fill's d_out until it is done)
@@ -1100,7 +1152,7 @@ def run_fill(args, world, rank, dev):
         def begin():
             eng.start(streams[0])
 
-        end = eng.stop
+        end = eng.finish  # waits on the run's last step (a give-up raises), then stops the grid
     else:
         pre = {(r, i): batch.prepare_call("sccsum_ipv4_fill", bs[r].data, bs[r].bytes_len, bs[r].off,
                                           bs[r].length, outs2[i], None, bs[r].n, bs[r].max_len, mode)
@@ -1110,18 +1162,31 @@ def run_fill(args, world, rank, dev):
             pre[(k % R, k % ns)](streams[k % ns])
     LAUNCHES.add(kern, 1 if engine else warm)
     sel = LAUNCHES.select(kern, 1 if engine else args.steps)
-    wall, launch_s = timed(step, args.steps, warm, world, streams, begin, end)
+    # the fields the timed fills must write are cleared before the timed region (outside it), so the check
+    # after it sees that every fill ran: a cleared frame does not verify
+    ran = sorted({k % R for k in range(warm, warm + args.steps)})
+
+    def clear_fields():
+        for r in ran:
+            fv = bs[r].data[: n * FRAME].view(n, FRAME)
+            fv[:, 10:12] = 0  # IPv4 header checksum
+            fv[:, 26:28] = 0  # UDP checksum (20-byte header + 6)
+
+    wall, launch_s = timed(step, args.steps, warm, world, streams, begin, end,
+                           between=None if args.no_check else clear_fields)
+    if engine:
+        eng.close()  # raises if the run left a published step undone
+    if not args.no_check:  # outside the timed region: every timed fill stored its fields
+        for r in ran:
+            batch.ipv4_frames(bs[r], status=st)
+            torch.cuda.synchronize()
+            assert int((st != 3).sum()) == 0, f"timed run, rotation {r}: filled frames do not verify"
     alg = n * (FRAME + META_BYTES + 4)  # read every byte + metadata, write the two 2-byte fields
     roof_alg, roof_s = alg, launch_s
     if engine:  # the launch is the run: every step's bytes over the run's time (the same ratio)
         roof_alg, roof_s = alg * args.steps, launch_s * args.steps
-        eng.close()
-        for b in bs:  # the engine's fills verify too
-            batch.ipv4_frames(b, status=st)
-            torch.cuda.synchronize()
-            assert args.no_check or int((st != 3).sum()) == 0, "engine-filled frames do not verify"
     ranks = per_rank(world, rank, dev, **rank_rate(n * FRAME, args.steps), avg_launch_us=launch_s * 1e6,
-                     frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS)
+                     frac=alg / launch_s / 1e9 / HBM_PEAK_GBPS, launch=launch_form(args))
     if rank == 0:
         emit("GiB/s device-resident Internet checksum, 1500B-packet batches, in-place generate (cfg 2 tx)",
              world * n * FRAME * args.steps / wall / 2**30, "GiB/s", args, world, wall, "u8",
@@ -1334,7 +1399,7 @@ def run_dry(args, world, rank):
         dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid(), "local": os.environ.get("LOCAL_RANK")})
     # the per_rank block of a real line, with the figures a device-less rank has
     pr = per_rank(world, rank, None, wall_s=time.perf_counter() - t0, GiBps=None, avg_launch_us=None,
-                  read_ceiling_GBps=None)
+                  read_ceiling_GBps=None, launch=launch_form(args))
     if rank == 0:
         print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "ranks": ranks, "per_rank": pr,
                           "barrier_s": round(wall, 6)}), flush=True)

@@ -70,7 +70,8 @@
  * threads may call concurrently, each on its own streams (the counter pool
  * is shared under a per-device lock held for a few ring probes per launch).
  * Diagnostic knobs (sccsum_diag.h) are per thread.  A burst queue or a
- * pipeline object belongs to one thread.
+ * pipeline object belongs to one thread; a resident engine takes steps from
+ * any number of threads (its "Producers" paragraph below).
  */
 #ifndef SCCSUM_H
 #define SCCSUM_H
@@ -90,8 +91,13 @@ extern "C" {
  * gained SCCSUM_EIDLE, fill steps (SCCSUM_ENGINE_FILL,
  * sccsum_engine_submit_fill), one running engine per device
  * (sccsum_engine_start: SCCSUM_EBUSY), and sccsum_engine_create no longer
- * changes the caller's current device. */
-#define SCCSUM_ABI_VERSION 3
+ * changes the caller's current device.
+ * 4 (round 6): engine runs are unbounded (max_steps sizes a descriptor ring),
+ * any number of threads may submit into one engine, sccsum_engine_create_opts
+ * (idle and dependency limits), SCCSUM_EFAULT; the desc calls accept a NULL
+ * descriptor array when no packet has fragments; sccsum_engine_stop / _destroy
+ * report SCCSUM_EIDLE only when a published step was left undone. */
+#define SCCSUM_ABI_VERSION 4
 
 #define SCCSUM_OK 0
 #define SCCSUM_EINVAL (-1)   /* bad argument (null pointer, misalignment) */
@@ -99,6 +105,8 @@ extern "C" {
 #define SCCSUM_EBUSY  (-3)   /* burst queue: every batch slot is in flight; poll and retry.  engine: the
                                 run's steps are used up, a wait timed out, or another engine runs on the device */
 #define SCCSUM_EIDLE  (-4)   /* engine: its grid gave up waiting for steps (idle limit); start a new run */
+#define SCCSUM_EFAULT (-5)   /* engine: its grid stopped on an internal fault (a wait on a dependency past its
+                                limit, a step it could not find); the run is over.  Never expected */
 
 /* per-packet status bits (d_status) */
 #define SCCSUM_ST_OK        0x01u /* spans: result == 0; frames: IPv4 header verifies */
@@ -221,19 +229,23 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  *   sccsum_engine_create(device, mode, max_steps, max_in_flight, &e)
  *       mode SCCSUM_PIPE_IPV4 (frames) or SCCSUM_PIPE_SPANS, frames may add
  *       SCCSUM_ENGINE_FILL (the run also takes fill steps; max_in_flight >= 2);
- *       at most max_steps (1..65536) steps per run (descriptors are never
- *       reused within a run: max_steps x 512 B of pinned memory and as much
- *       device memory), at most max_in_flight (1..64) submitted and not yet
- *       done.  Allocates on `device`; the calling thread's current device is
- *       left as it was.
+ *       max_steps (1..65536, rounded up to a power of two, at least 2) = the
+ *       slots of the engine's descriptor RING (512 B of pinned memory and as
+ *       much device memory each): a run takes any number of steps, a slot
+ *       being reused once its step is done; at most min(max_in_flight (1..64),
+ *       max_steps) steps submitted and not yet done.  Allocates on `device`;
+ *       the calling thread's current device is left as it was.
+ *   sccsum_engine_create_opts(device, mode, &opts, &e)   the same with every
+ *       limit given (sccsum_engine_opts; a 0 field takes its default)
  *   sccsum_engine_start(e, stream)      launch the grid on `stream` (a run);
  *       `stream` belongs to the engine's device, which must be the calling
  *       thread's current device (sccsum_init(device)).  SCCSUM_EBUSY when
  *       another engine of this process runs on the device.
  *   sccsum_engine_submit(e, batches, nbatch, max_len, timeout_ns, &step)
- *       publish one step; waits (spinning, up to timeout_ns) while
- *       max_in_flight steps are pending.  SCCSUM_EBUSY: the run already took
- *       max_steps steps (stop and start a new run) or the wait timed out.
+ *       publish one step; waits (spinning, up to timeout_ns) while the
+ *       in-flight limit's steps are pending.  SCCSUM_EBUSY: the wait timed
+ *       out; SCCSUM_EINVAL: the engine is not running (never started, or
+ *       stopped); SCCSUM_EIDLE / SCCSUM_EFAULT: the run is over.
  *       max_len (0 = unknown) caps the mean packet length the step's tiles
  *       are sized by (bytes_len / n otherwise, too big for a batch that is a
  *       slice of a larger buffer).  The engine always runs the flat kernel, so
@@ -245,37 +257,59 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  *       (d_bytes is written; each batch's d_out, required here, gets the
  *       values stored and d_status the status bits).  A fill of at most
  *       524 288 frames (sccsum_set_fill_single_max) is ONE step whose tiles
- *       store the fields themselves; a larger one is two: a generate step into
- *       d_out and a store step whose tiles wait for it and write the values
- *       into the frames' fields (both or neither are published: such a fill
- *       takes 2 of the run's max_steps).  *step = the fill's last step: once
- *       it is done the frames are wire-ready in device memory and d_out holds
- *       the values stored.  No other step may write a fill's d_out (nor its
- *       frames) before the fill is done.  max_len as for submit.
- *   sccsum_engine_wait(e, step, timeout_ns)   0 once the step is done
+ *       store the fields themselves; a larger one is two consecutive steps: a
+ *       generate step into d_out and a store step whose tiles wait for it and
+ *       write the values into the frames' fields (both or neither are
+ *       published).  *step = the fill's last step: once it is done the frames
+ *       are wire-ready in device memory and d_out holds the values stored.  No
+ *       other step may write a fill's d_out (nor its frames) before the fill is
+ *       done.  max_len as for submit.
+ *   sccsum_engine_wait(e, step, timeout_ns)   0 once the step is done;
+ *       SCCSUM_EBUSY on time out, SCCSUM_EIDLE / SCCSUM_EFAULT if the grid
+ *       gave up before the step was done
  *   sccsum_engine_stop(e)               no more steps: the grid leaves once the
- *       published steps are done (synchronise `stream` to wait for it).  Its
- *       SCCSUM_EIDLE only covers a give-up seen before the call: after the
- *       stream sync, sccsum_engine_wait(e, step, 0) still answers for every
- *       step of the run (0 done, SCCSUM_EIDLE if the grid gave up first)
+ *       published steps are done (synchronise `stream` to wait for it).
+ *       SCCSUM_EIDLE (SCCSUM_EFAULT) when the grid had already given up with a
+ *       published step not done: after the stream sync,
+ *       sccsum_engine_wait(e, step, 0) still answers for every step of the
+ *       run's last max_steps (0 done, the give-up's code otherwise)
  *   sccsum_engine_destroy(e)            stops and synchronises a running engine;
- *       SCCSUM_EIDLE if its last run gave up with steps unfinished
+ *       SCCSUM_EIDLE (SCCSUM_EFAULT) if its last run left a published step
+ *       undone (a give-up after every step was done loses nothing: 0)
+ *
+ * Producers.  Any number of host threads may submit into one running engine
+ * and wait on its steps — the shards that share a GPU, each with its own
+ * batches: a step's number, first tile and descriptor are taken and published
+ * under the engine's lock (a few hundred ns, no device call), so steps are
+ * published in the order their submits took the lock, and a submit that waits
+ * for room waits outside it.  The in-flight limit is the engine's, shared by
+ * every producer.  Start, stop and destroy belong to the engine's owner (a
+ * submit after stop returns SCCSUM_EINVAL; destroy only after every producer's
+ * last call has returned).
  *
  * Sharing the device.  The grid holds the device's compute units while it
  * runs (every CU, all of their LDS): kernels that other threads or streams
  * launch on the device — this library's launches included — queue until the
  * run stops, and then complete.  So one engine runs per device at a time
  * (per process: a second start returns SCCSUM_EBUSY until the first run's
- * stop), and a shard that shares its GPU with other shards should use
- * launches, or own the engine's device for the run.  A grid given no new step
- * (and no stop) for 1 s leaves on its own, and every later call on that run
- * returns SCCSUM_EIDLE: the limit counts from the last step the grid
- * received, so steady light traffic never trips it.  One engine belongs to
- * one host thread, like a burst queue. */
+ * stop), and the shards of a GPU submit into its one engine (Producers) or
+ * use launches while no engine runs there.  A grid given no new step (and no
+ * stop) for its idle limit (default 1 s) leaves on its own, and every later
+ * call on that run returns SCCSUM_EIDLE: the limit counts from the last step
+ * the grid received, so steady light traffic never trips it. */
 #define SCCSUM_ENGINE_MAX_BATCHES 4
 #define SCCSUM_ENGINE_FILL 0x100 /* sccsum_engine_create mode flag: the run takes fill steps too */
 typedef struct sccsum_engine sccsum_engine;
+typedef struct sccsum_engine_opts {
+    uint32_t ring_slots;    /* descriptor ring slots, 1..65536 (a power of two, at least 2, above); 0 = 1024 */
+    uint32_t max_in_flight; /* steps submitted and not yet done, 1..64 (fill engines: >= 2); 0 = 8 */
+    uint32_t idle_ms;       /* the grid leaves after this long without a new step (SCCSUM_EIDLE),
+                               1..3 600 000; 0 = 1000 */
+    uint32_t dep_ms;        /* limit of a step's wait on the step it depends on (a fill's store step on its
+                               generate step, a barrier; SCCSUM_EFAULT past it), 1..3 600 000; 0 = 2000 */
+} sccsum_engine_opts;
 int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, sccsum_engine** out);
+int sccsum_engine_create_opts(int device, int mode, const sccsum_engine_opts* opts, sccsum_engine** out);
 int sccsum_engine_start(sccsum_engine* e, void* stream);
 int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
                          uint64_t timeout_ns, uint64_t* step);

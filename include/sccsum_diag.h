@@ -64,7 +64,8 @@ int sccsum_set_out_policy(int policy);
 int sccsum_set_engine_write_through(int on);
 /* Engine runs started later by this thread: how long the grid may go without
  * a new step before its waiting waves give up and the run reports
- * SCCSUM_EIDLE (default 1000 ms; 1 .. 3 600 000).  Tests shorten it. */
+ * SCCSUM_EIDLE, overriding the engine's own limit (sccsum_engine_opts.idle_ms)
+ * when > 0 (1 .. 3 600 000 ms; 0, the default, = no override). */
 int sccsum_set_engine_idle_ms(int ms);
 /* Engine steps submitted later by this thread: every k-th step's tiles wait
  * until the step before it is done (a barrier that lines up dequeue groups

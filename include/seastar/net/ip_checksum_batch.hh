@@ -217,15 +217,18 @@ public:
 };
 
 // Resident engine (<sccsum.h> sccsum_engine_*): one grid kept on the GPU
-// while a shard streams steps into it, as the reactor keeps polling its
+// while the shards stream steps into it, as the reactor keeps polling its
 // queues (reactor.cc:3543-3550); each step is up to 4 batches, computed
-// exactly as the one-launch calls compute them.  Frames engines may take
-// in-place fills (fill = true).  One engine runs per device at a time:
+// exactly as the one-launch calls compute them.  A run takes any number of
+// steps (their descriptors cycle through a ring of ring_slots slots), and
+// any number of threads may submit into it and wait — the shards that share
+// the GPU; start / stop / the destructor are the owner's.  Frames engines may
+// take in-place fills (fill = true).  One engine runs per device at a time:
 // try_start() is false while another engine of the process runs there.
-//   resident_engine eng(gpu, SCCSUM_PIPE_IPV4, /*max_steps=*/4096, /*in flight=*/8, /*fill=*/true);
+//   resident_engine eng(gpu, SCCSUM_PIPE_IPV4, /*ring_slots=*/1024, /*in flight=*/8, /*fill=*/true);
 //   eng.start(stream);
 //   sccsum_batch tx = {...}, rx = {...};
-//   uint64_t a = eng.submit_fill(&tx, 1, SCCSUM_FILL_IP | SCCSUM_FILL_L4);
+//   uint64_t a = eng.submit_fill(&tx, 1, SCCSUM_FILL_IP | SCCSUM_FILL_L4);   // from any shard
 //   uint64_t b = eng.submit(&rx, 1);
 //   eng.wait(b); eng.wait(a); eng.stop();
 class resident_engine {
@@ -238,13 +241,24 @@ class resident_engine {
     }
 
 public:
-    resident_engine(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, bool fill = false) {
-        check(sccsum_engine_create(device, mode | (fill ? SCCSUM_ENGINE_FILL : 0), max_steps, max_in_flight, &_e),
+    resident_engine(int device, int mode, uint32_t ring_slots, uint32_t max_in_flight, bool fill = false) {
+        check(sccsum_engine_create(device, mode | (fill ? SCCSUM_ENGINE_FILL : 0), ring_slots, max_in_flight, &_e),
               "sccsum_engine_create");
+    }
+    // every limit (ring, in flight, idle and dependency limits; 0 fields = defaults)
+    resident_engine(int device, int mode, const sccsum_engine_opts& opts, bool fill = false) {
+        check(sccsum_engine_create_opts(device, mode | (fill ? SCCSUM_ENGINE_FILL : 0), &opts, &_e),
+              "sccsum_engine_create_opts");
     }
     resident_engine(const resident_engine&) = delete;
     resident_engine& operator=(const resident_engine&) = delete;
     ~resident_engine() { sccsum_engine_destroy(_e); }
+    // destroy now, reporting a run that left a published step undone (the destructor cannot)
+    void close() {
+        sccsum_engine* e = _e;
+        _e = nullptr;
+        check(sccsum_engine_destroy(e), "sccsum_engine_destroy");
+    }
 
     // launch the grid on `stream` (the calling thread's current device, the engine's)
     void start(void* stream) { check(sccsum_engine_start(_e, stream), "sccsum_engine_start"); }

@@ -433,11 +433,16 @@ class Engine:
     launch's ramp, drain and kernel boundary are paid once per run instead of
     once per step (include/sccsum.h, "Resident engine").
 
-        eng = Engine(device=0, frames=True, max_steps=1024, max_in_flight=2)
+        eng = Engine(device=0, frames=True, ring_slots=1024, max_in_flight=2)
         eng.start(stream)
         step = eng.submit([(tx, out2, None), (rx, None, status)])   # like prepare_ipv4_frames_multi's items
         eng.wait(step)                                               # results readable by a D2H copy
-        eng.stop(); stream.synchronize()
+        eng.finish(); stream.synchronize()                           # wait on the last step, then stop
+
+    A run takes any number of steps: their descriptors cycle through a ring
+    of ring_slots slots (max_steps is its old name).  Any number of threads
+    may submit into a running engine and wait on its steps (the shards of one
+    GPU); start / stop / finish / close belong to its owner.
 
     fill=True (frames): the run also takes in-place fills, each as a generate
     step and a store step (sccsum_engine_submit_fill):
@@ -448,26 +453,35 @@ class Engine:
     (start raises SccsumError(SCCSUM_EBUSY) while another engine's run holds
     it); while it runs, every other kernel on the device waits for its stop."""
 
-    def __init__(self, device: int = 0, frames: bool = True, max_steps: int = 1024, max_in_flight: int = 2,
-                 fill: bool = False):
+    def __init__(self, device: int = 0, frames: bool = True, max_steps: int | None = None, max_in_flight: int = 2,
+                 fill: bool = False, ring_slots: int | None = None, idle_ms: int = 0, dep_ms: int = 0):
+        import threading
+
         self._lib = native.load()
         h = ctypes.c_void_p()
         mode = (native.PIPE_IPV4 if frames else native.PIPE_SPANS) | (native.ENGINE_FILL if fill else 0)
-        native.check(self._lib.sccsum_engine_create(int(device), mode, int(max_steps), int(max_in_flight),
-                                                     ctypes.byref(h)),
-                     "sccsum_engine_create")
+        ring = ring_slots if ring_slots is not None else (max_steps if max_steps is not None else 1024)
+        opts = native.EngineOpts(int(ring), int(max_in_flight), int(idle_ms), int(dep_ms))
+        if ring <= 0 or max_in_flight <= 0:  # (0 would mean "the default" to the C-ABI)
+            raise ValueError("ring_slots and max_in_flight must be >= 1")
+        native.check(self._lib.sccsum_engine_create_opts(int(device), mode, ctypes.byref(opts), ctypes.byref(h)),
+                     "sccsum_engine_create_opts")
         self._h = h
         self.frames = frames
         self.fill = fill
         self.max_in_flight = int(max_in_flight)
         self._keep: dict[int, tuple] = {}
+        self._mu = threading.Lock()  # _keep and _last: producers may be several threads
+        self._last = -1  # the run's latest step
         self._stream = None
 
     def start(self, stream=None):
         s = torch.cuda.current_stream() if stream is None else stream
         native.check(self._lib.sccsum_engine_start(self._h, s.cuda_stream), "sccsum_engine_start")
         self._stream = s
-        self._keep.clear()
+        with self._mu:
+            self._keep.clear()
+            self._last = -1
 
     def prepare(self, items, fill_mode: int = 0):
         """A step's descriptor array, checked once (items as for
@@ -510,10 +524,15 @@ class Engine:
             native.check(self._lib.sccsum_engine_submit(self._h, ctypes.cast(arr, ctypes.c_void_p), nb, ml,
                                                          int(timeout_s * 1e9), ctypes.byref(step)),
                          "sccsum_engine_submit")
-        self._keep[step.value] = prep
-        for s in [k for k in self._keep if k + self.max_in_flight < step.value]:
-            del self._keep[s]  # done: submit waited for it
-        return step.value
+        s = step.value
+        with self._mu:
+            self._keep[s] = prep
+            self._last = max(self._last, s)
+            if len(self._keep) > 4 * self.max_in_flight + 8:
+                # done: a step max_in_flight (+ 1 for a fill's pair) before the newest was waited for by a submit
+                for k in [k for k in self._keep if k + self.max_in_flight + 1 < self._last]:
+                    del self._keep[k]
+        return s
 
     def submit(self, items, timeout_s: float = 10.0) -> int:
         return self.submit_prepared(self.prepare(items), timeout_s)
@@ -526,14 +545,32 @@ class Engine:
     def wait(self, step: int, timeout_s: float = 10.0) -> None:
         native.check(self._lib.sccsum_engine_wait(self._h, int(step), int(timeout_s * 1e9)), "sccsum_engine_wait")
 
+    @property
+    def last_step(self) -> int:
+        """The run's latest submitted step (-1: none yet)."""
+        return self._last
+
     def stop(self) -> None:
         native.check(self._lib.sccsum_engine_stop(self._h), "sccsum_engine_stop")
 
+    def finish(self, timeout_s: float = 10.0) -> None:
+        """Wait until the run's latest step is done, then stop: a give-up
+        (EIDLE) or fault (EFAULT) before it raises here instead of passing
+        unseen (a timed run that only stopped never looked)."""
+        try:
+            if self._last >= 0:
+                self.wait(self._last, timeout_s)
+        finally:
+            self.stop()
+
     def close(self) -> None:
+        """Destroy the engine (stopping and synchronising a running one).
+        Raises SccsumError when its last run left a published step undone
+        (SCCSUM_EIDLE / SCCSUM_EFAULT from sccsum_engine_destroy)."""
         if self._h:
-            self._lib.sccsum_engine_destroy(self._h)
-            self._h = None
+            h, self._h = self._h, None
             self._keep.clear()
+            native.check(self._lib.sccsum_engine_destroy(h), "sccsum_engine_destroy")
 
     def __del__(self):
         try:

@@ -1168,9 +1168,26 @@ struct QueueSrc {
 // wait on itself: a store tile is only ever waited on by a wave that holds
 // nothing older, and every generate tile precedes it in its group's claim
 // order, so the chain of waits runs to strictly older tiles and ends.
+//
+// Unbounded runs: the descriptors live in a RING of 2^k slots (step s in slot
+// s & ring_mask), host and device alike, and so do the steps' done words.  The
+// host publishes step s only once every step up to s - ring is done, so a
+// step that is not done always has its slot; a wave looking for the step of
+// its claimed tile (not done: the wave holds it) finds it by probing slots
+// (walk(): galloping and binary search from its cursor), where a slot that
+// holds another step means that step is done, and every step before it.  The
+// polling wave rewrites a slot seqlock-style (step word invalid, then the
+// other words, then the step word), and a probe reads the step word twice
+// around the descriptor, so a torn read is never taken for a valid one.
 constexpr uint32_t kEngineSlotWords = 64;  // 512-byte descriptors
 constexpr uint32_t kEngineCountSlots = 64;  // completion counters: steps in flight at most
-constexpr uint32_t kEngineMaxSteps = 1u << 16;  // steps per run (2 x 32 MiB of descriptor rings at most)
+constexpr uint32_t kEngineMaxRing = 1u << 16;  // descriptor ring slots (2 x 32 MiB of descriptor rings at most)
+constexpr uint32_t kEngineDefaultRing = 1024;
+// descriptors the polling wave copies per round of its store phases (4 or 8
+// held in registers across the phases pushed the fill engine kernel into
+// scratch: 224 B of spills, where 2 leave it at 214 VGPRs and none)
+constexpr uint32_t kPollGroup = 2;
+constexpr uint64_t kSlotInvalid = ~0ull;  // a slot's step word while the poller rewrites it
 // descriptor words
 constexpr uint32_t kEdFirst = 0;   // the step's first tile in the run
 constexpr uint32_t kEdTiles = 1;   // tiles | B (packets per tile) << 32
@@ -1197,17 +1214,19 @@ constexpr bool kStoreWT = true;
 #endif
 // ctl words (pinned): each on its own 64-byte line
 constexpr uint32_t kEcPublished = 0, kEcStop = 8, kEcError = 16, kEcDone = 24;  // done[s] at 24 + 8 s
-// kEcError values: the grid gave up waiting for a step (idle), or on a dependency (a fault: never expected)
-constexpr uint64_t kErrIdle = 1, kErrDepWait = 2;
+// kEcError values: the grid gave up waiting for a step (idle), or on a dependency, or a wave found no
+// step holding its published tile (the last two are faults: never expected)
+constexpr uint64_t kErrIdle = 1, kErrDepWait = 2, kErrWalk = 3;
 // mirror words (device): published tiles, steps copied, stop seen, poll token, time of the last new step
 constexpr uint32_t kMpTiles = 0, kMpSteps = 8, kMpStop = 16, kMpToken = 24, kMpStamp = 32, kMirrorWords = 40;
 
 struct EngineArgs {
-    const uint64_t* hring;  // descriptors as the host writes them, kEngineSlotWords words per step (pinned)
+    const uint64_t* hring;  // descriptors as the host writes them, kEngineSlotWords words per slot (pinned)
     uint64_t* dring;        // the same descriptors, copied by the polling wave (device)
+    uint64_t ring_mask;     // ring slots - 1 (a power of two): step s lives in slot s & ring_mask
     uint64_t* ctl;          // control words (device view of pinned memory)
     uint64_t* mirror;       // kMirrorWords (device)
-    uint32_t* claims;       // kGroups claim counters, kHeadStride apart (device)
+    uint64_t* claims;       // kGroups 64-bit claim counters, 256 B apart (device; a run never wraps one)
     uint32_t* counts;       // kEngineCountSlots x kGroups completion counters, kHeadStride apart (device)
     uint32_t* gdone;        // kEngineCountSlots groups-done counters, kHeadStride apart (device)
     uint64_t* sdone;        // kEngineCountSlots words, 8 apart: 1 + the latest step done in each count slot (device)
@@ -1257,16 +1276,16 @@ struct EngineSrc {
     }
     __device__ uint64_t end() const { return ~0ull; }
     struct Claim {
-        uint32_t raw;
+        uint64_t raw;
     };
     __device__ Claim claim_issue(uint64_t) {
         Claim c{0u};
-        if (lane == 0) c.raw = __hip_atomic_fetch_add(E.claims + grp * kHeadStride, 1u, __ATOMIC_RELAXED,
+        if (lane == 0) c.raw = __hip_atomic_fetch_add(E.claims + grp * (kHeadStride / 2), 1ull, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT);
         return c;
     }
     __device__ uint64_t claim_resolve(const Claim& c) {
-        const uint32_t d = __builtin_amdgcn_readfirstlane(c.raw);
+        const uint64_t d = rfl64(c.raw);
         return grp + static_cast<uint64_t>(kGroups) * d;
     }
     __device__ uint64_t claim(uint64_t prev) { return claim_resolve(claim_issue(prev)); }
@@ -1301,16 +1320,59 @@ struct EngineSrc {
         uint64_t ms = mload(kMpSteps);
         const uint64_t ms0 = ms;
         uint64_t tiles = mload(kMpTiles);
-        for (; ms < hs; ++ms) {
-            const uint64_t w = __hip_atomic_load(E.hring + ms * kEngineSlotWords + lane, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(E.dring + ms * kEngineSlotWords + lane, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            tiles = rl64(w, kEdFirst) + static_cast<uint32_t>(rl64(w, kEdTiles));
+        // Copy the new descriptors in groups: a group's host reads are in
+        // flight together (one PCIe round trip), then its slots are rewritten
+        // in three store phases — step word invalid (only a slot that held a
+        // step of this run: a probe of this run reads no other), the other
+        // words, the step word — each phase complete before the next begins.
+        auto dslot = [&](uint64_t s) { return E.dring + (s & E.ring_mask) * kEngineSlotWords + lane; };
+        auto put = [&](uint64_t s, uint64_t x) {
+            __hip_atomic_store(dslot(s), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
+        while (ms < hs) {
+            const uint64_t g = hs - ms < kPollGroup ? hs - ms : kPollGroup;
+            uint64_t w[kPollGroup];
+#pragma unroll
+            for (uint32_t k = 0; k < kPollGroup; ++k) {
+                w[k] = k < g ? __hip_atomic_load(E.hring + ((ms + k) & E.ring_mask) * kEngineSlotWords + lane,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                             : 0ull;
+            }
+            const bool reuse = ms + g > E.ring_mask + 1;  // some slot of the group held a step of this run
+            if (!reuse) {  // fresh slots (no probe reads them before the mirror says so): one phase
+#pragma unroll
+                for (uint32_t k = 0; k < kPollGroup; ++k) {
+                    if (k < g) put(ms + k, w[k]);
+                }
+            } else {
+#pragma unroll
+                for (uint32_t k = 0; k < kPollGroup; ++k) {
+                    if (k < g && lane == kEdStep) put(ms + k, kSlotInvalid);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                for (uint32_t k = 0; k < kPollGroup; ++k) {
+                    if (k < g && lane != kEdStep) put(ms + k, w[k]);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                for (uint32_t k = 0; k < kPollGroup; ++k) {
+                    if (k < g && lane == kEdStep) put(ms + k, w[k]);
+                }
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kPollGroup; ++k) {
+                if (k + 1 == g) tiles = rl64(w[k], kEdFirst) + static_cast<uint32_t>(rl64(w[k], kEdTiles));
+            }
+            ms += g;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the descriptors are in the device ring
+        // steps before tiles: a wave that sees a tile published then sees its
+        // step copied (walk()'s upper bound is the mirror's step count)
+        if (lane == 0) __hip_atomic_store(E.mirror + kMpSteps, hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) {
             __hip_atomic_store(E.mirror + kMpTiles, tiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(E.mirror + kMpSteps, hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // the grid's progress clock: waiting waves give up only when no new
             // step arrived for idle_ticks (timing each wave's own
             // wait let a wave holding a claim far ahead leave under steady light
@@ -1403,27 +1465,95 @@ struct EngineSrc {
         const uint64_t v = claim(0);
         return wait_ready(v) ? v : end();
     }
-    // tile v (published) -> its step, batch and packets.  Steps are walked in
-    // order: a run never reuses a descriptor, so a step passed over stays valid.
-    __device__ void walk(uint64_t v) {
+    // Probe step t (< the mirror's step count: copied) for tile v: 0 = v lies
+    // in t (w = its descriptor, lane i word i), 1 = t lies before v's step,
+    // 2 = after it.  A slot that holds another step (or is being rewritten)
+    // means t is done, and every step before it (the host reuses a slot only
+    // then), while v's step is not (v is this wave's, unprocessed): so t lies
+    // before.  The step word is read again after the descriptor: equal both
+    // times, every word read belongs to t (the poller marks the slot invalid
+    // before it writes any other word).
+    __device__ uint32_t probe(uint64_t t, uint64_t v, uint64_t& w) {
 #ifdef SCCSUM_AB_TIMELINE
-        const uint64_t w0 = (step == ~0ull || v >= slast) ? static_cast<uint64_t>(wall_clock64()) : 0;
+        ++ab[3];
 #endif
-        while (step == ~0ull || v >= slast) {
+        const uint64_t* const slot = E.dring + (t & E.ring_mask) * kEngineSlotWords;
+        w = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (rl64(w, kEdStep) != t) return 1u;
+        asm volatile("" ::: "memory");  // the second read issues after the first has returned
+        uint64_t again = 0;
+        if (lane == kEdStep) again = __hip_atomic_load(slot + kEdStep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (rl64(again, kEdStep) != t) return 1u;
+        const uint64_t f = rl64(w, kEdFirst);
+        if (v < f) return 2u;
+        return v < f + static_cast<uint32_t>(rl64(w, kEdTiles)) ? 0u : 1u;
+    }
+    __device__ void set_cursor(uint64_t t, uint64_t w) {
+        step = t;
+        dw = w;
+        sfirst = rl64(w, kEdFirst);
+        slast = sfirst + static_cast<uint32_t>(rl64(w, kEdTiles));
+        skind = rl64(w, kEdKind);
+        sdep = rl64(w, kEdDep);
+    }
+    // A fault ends the wave where it stands (reported first; the host sees
+    // SCCSUM_EFAULT).  (Returning it up through ready() / wait_ready() cost
+    // the kernel ~40 VGPRs of merged control flow in the tile loop.)
+    __device__ bool fault(uint64_t code) {
+        if (lane == 0) __hip_atomic_store(E.ctl + kEcError, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_endpgm();
+    }
+    // tile v (published) -> the cursor on its step.  Claims only rise, so v's
+    // step is the cursor's or a later one: the next step first (a wave's next
+    // tile is mostly there), then galloping from the cursor and a binary
+    // search, every probe on a slot the ring may have reused since (probe()).
+    __device__ bool walk(uint64_t v) {
+        if (step != ~0ull && v < slast) return true;
 #ifdef SCCSUM_AB_TIMELINE
-            ++ab[3];
+        const uint64_t w0 = static_cast<uint64_t>(wall_clock64());
+        struct Walked {
+            unsigned long long* a;
+            uint64_t t0;
+            __device__ ~Walked() { a[4] += static_cast<uint64_t>(wall_clock64()) - t0; }
+        } walked{ab, w0};
 #endif
-            step = step + 1;  // (~0 + 1 = step 0)
-            dw = __hip_atomic_load(E.dring + step * kEngineSlotWords + lane, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            sfirst = rl64(dw, kEdFirst);
-            slast = sfirst + static_cast<uint32_t>(rl64(dw, kEdTiles));
-            skind = rl64(dw, kEdKind);
-            sdep = rl64(dw, kEdDep);
+        uint64_t w = 0;
+        uint64_t below = step + 1;  // (~0 + 1 = step 0)
+        uint32_t r = probe(below, v, w);
+        if (r == 0u) {
+            set_cursor(below, w);
+            return true;
         }
-#ifdef SCCSUM_AB_TIMELINE
-        if (w0) ab[4] += static_cast<uint64_t>(wall_clock64()) - w0;
-#endif
+        if (r == 2u) return fault(kErrWalk);  // v before the step after the cursor's: never
+        uint64_t above = mload(kMpSteps);       // below < step(v) < above
+        for (uint64_t d = 1; below + d < above; d <<= 1) {
+            const uint64_t t = below + d;
+            r = probe(t, v, w);
+            if (r == 0u) {
+                set_cursor(t, w);
+                return true;
+            }
+            if (r == 2u) {
+                above = t;
+                break;
+            }
+            below = t;
+        }
+        while (above - below > 1) {
+            const uint64_t t = below + (above - below) / 2;
+            r = probe(t, v, w);
+            if (r == 0u) {
+                set_cursor(t, w);
+                return true;
+            }
+            if (r == 1u) {
+                below = t;
+            } else {
+                above = t;
+            }
+        }
+        return fault(kErrWalk);  // a published tile in no published step: never
     }
     __device__ Ref ref(uint64_t v) {
         walk(v);
@@ -1523,7 +1653,9 @@ struct EngineSrc {
         // the device's copy first (steps that depend on this one read it), then the host's
         __hip_atomic_store(E.sdone + 8u * slot, pend_step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(E.ctl + kEcDone + 8u * pend_step, pend_step + 1, __ATOMIC_RELAXED,
+        // (a ring of done words like the descriptors': the slot's value only
+        // rises, and a value past s + 1 also says s is done)
+        __hip_atomic_store(E.ctl + kEcDone + 8u * (pend_step & E.ring_mask), pend_step + 1, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
 #ifdef SCCSUM_AB_TIMELINE
@@ -2468,7 +2600,7 @@ struct Knobs {
     int short_chunks = 1;            // flat kernel (no chunk in flight): a run's last chunk covers only its rows
     int run_align = kRunAlign;       // flat kernel: run extents start on 1 / 4 / 8-unit (16 / 64 / 128 B) boundaries
     int engine_wt = 1;               // engine: results written through (1) or stored as a launch stores them (0)
-    int engine_idle_ms = 1000;       // engine: a run given no new step for this long gives up (SCCSUM_EIDLE)
+    int engine_idle_ms = 0;          // engine: overrides the engine's idle limit (ms) for runs this thread starts
     uint32_t fill_single_max = kFillSingleMax;  // in-place fills of at most this many frames run in one pass
     int engine_sync_every = -1;      // engine: every k-th step waits for the step before it (0 = never,
                                      // -1 = every kEngineSyncEvery steps of >= 2 tiles per wave)
@@ -3204,19 +3336,31 @@ hipError_t launch_engine(hipStream_t s, int dev, const EngineArgs& E, uint32_t f
 struct sccsum_engine {
     int device = 0;
     bool frames = true, fill = false;
-    uint32_t max_steps = 0, max_in_flight = 0;
+    uint32_t ring = 0;           // descriptor ring slots (a power of two >= 2)
+    uint32_t max_in_flight = 0;
+    uint32_t limit = 0;          // steps submitted and not done at most: min(max_in_flight, ring)
+    uint64_t idle_ticks = 0, dep_ticks = 0;  // the create options, in 100 MHz ticks
     uint64_t* ring_h = nullptr;  // pinned descriptors (host view)
     uint64_t* ctl_h = nullptr;   // pinned control words (host view)
     sccsum::EngineArgs args{};   // device views + device counters
     hipStream_t stream = nullptr;
     hipEvent_t left = nullptr;   // recorded after the last run's grid: it has left once this completes
-    bool running = false, launched = false, left_recorded = false;
+    bool launched = false, left_recorded = false;
     uint64_t waves = 0;          // the running grid's waves (tile sizing)
-    uint64_t next_step = 0, next_first = 0;
-    uint64_t last_tiled = ~0ull;  // the latest published step with tiles (a barrier's target), ~0 = none yet
-    uint64_t done_floor = 0;     // every step below it is known done (engine_room)
     void* blk = nullptr;         // the device block: claims | mirror | sdone | counts | gdone (EngineBlock)
     bool dirty = true;           // the counts / gdone words may be nonzero (a run that gave up, or none yet)
+    // Producers — any number of host threads, Seastar's shards on this GPU —
+    // meet under mu: a step's number, its first tile and its descriptor are
+    // taken, written and published in one short critical section (no device
+    // call, no wait), so steps are published in order and the grid's poller
+    // never sees a hole.  Waiting for room under the in-flight limit happens
+    // outside it.
+    std::mutex mu;
+    bool running = false;                // under mu
+    std::atomic<uint64_t> next_step{0};  // written under mu; sccsum_engine_wait reads it without
+    uint64_t next_first = 0;             // under mu
+    uint64_t last_tiled = ~0ull;         // under mu: the latest published step with tiles (a barrier's target)
+    uint64_t done_floor = 0;             // under mu: every step below it is known done
 };
 
 namespace {
@@ -3228,7 +3372,7 @@ namespace {
 // last count resets them), so they are cleared only after a run that gave up
 // with steps unfinished, and at the first run.
 struct EngineBlock {
-    static constexpr size_t kClaims = 0;
+    static constexpr size_t kClaims = 0;  // 64-bit claim counters, 256 B apart
     static constexpr size_t kMirror = kClaims + size_t(sccsum::kGroups) * sccsum::kHeadStride * 4u;
     static constexpr size_t kSdone = kMirror + 512u;
     static constexpr size_t kReset = kSdone + size_t(sccsum::kEngineCountSlots) * 8u * 8u;  // cleared every run
@@ -3241,9 +3385,10 @@ struct EngineBlock {
 // One running engine per device in this process.  A grid holds every CU of
 // its device and all of their LDS while it runs, so a second grid there could
 // only queue behind it (and a step submitted to it would wait on the first
-// run's stop): sccsum_engine_start refuses it with SCCSUM_EBUSY.  (Seastar
-// runs one process with a reactor thread per core, src/core/reactor.cc:4163,
-// so shards sharing a GPU meet here.)
+// run's stop): sccsum_engine_start refuses it with SCCSUM_EBUSY.  The shards
+// of one GPU share its engine instead: any number of threads may submit into
+// a running engine (Seastar runs one process with a reactor thread per core,
+// src/core/reactor.cc:4163; ~16 of them per GPU on an 8-GPU box).
 std::mutex g_live_mu;
 sccsum_engine* g_live[sccsum::kMaxDevices] = {};
 
@@ -3271,15 +3416,36 @@ uint64_t now_ns() {
                                      .count());
 }
 
+// Step s is done.  Its done word is a ring slot shared with s + ring,
+// s + 2 ring, ...: the slot's value only rises, and s + ring is published
+// only once s is done, so any value past s says so too.
+bool engine_done(const sccsum_engine* e, uint64_t s) {
+    return __atomic_load_n(e->ctl_h + sccsum::kEcDone + 8u * (s & (e->ring - 1u)), __ATOMIC_ACQUIRE) >= s + 1;
+}
+
+// The grid's give-up, as an error code: SCCSUM_EIDLE (no new step for the
+// idle limit) or SCCSUM_EFAULT (a dependency or step lookup that could not
+// finish: never expected)
+int engine_error(const sccsum_engine* e) {
+    const uint64_t v = __atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE);
+    return v == 0 ? SCCSUM_OK : (v == sccsum::kErrIdle ? SCCSUM_EIDLE : SCCSUM_EFAULT);
+}
+
 // spin until step s is done, the grid gave up, or the deadline passes
-int engine_wait_done(sccsum_engine* e, uint64_t s, uint64_t timeout_ns) {
+int engine_wait_done(const sccsum_engine* e, uint64_t s, uint64_t timeout_ns) {
     const uint64_t t0 = now_ns();
-    uint64_t* const w = e->ctl_h + sccsum::kEcDone + 8u * s;
     for (uint32_t k = 0;; ++k) {
-        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == s + 1) return SCCSUM_OK;
-        if (__atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE)) return SCCSUM_EIDLE;
+        if (engine_done(e, s)) return SCCSUM_OK;
+        if (const int rc = engine_error(e)) return rc;
         if ((k & 255u) == 255u && now_ns() - t0 > timeout_ns) return SCCSUM_EBUSY;
     }
+}
+
+// Every published step of the run is done (under mu; steps below done_floor are)
+bool engine_all_done(sccsum_engine* e) {
+    const uint64_t n = e->next_step.load(std::memory_order_relaxed);
+    while (e->done_floor < n && engine_done(e, e->done_floor)) ++e->done_floor;
+    return e->done_floor >= n;
 }
 
 // The batches of one step, checked as the launches check them.
@@ -3298,36 +3464,30 @@ int engine_check(const sccsum_engine* e, const sccsum_batch* batches, uint32_t n
     return SCCSUM_OK;
 }
 
-// Room to publish k more steps now: pacing by max_in_flight, max_steps, a
-// live grid.  Every step up to max_in_flight before the last of them must be
-// done, not only that one: steps can finish out of order (a small step behind
-// a big one's last tile), and a step's completion counters and done word are
-// slot step % kEngineCountSlots, which the step kEngineCountSlots later takes
-// over (max_in_flight <= kEngineCountSlots).  The caller may also free an
-// older step's buffers once a later submit returns.
-int engine_room(sccsum_engine* e, uint32_t k, uint64_t timeout_ns) {
-    if (__atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE)) return SCCSUM_EIDLE;
-    const uint64_t last = e->next_step + k - 1;
-    if (last >= e->max_steps) return SCCSUM_EBUSY;  // the run's descriptors are used up: stop, start again
-    if (last < e->max_in_flight) return SCCSUM_OK;
-    const uint64_t target = last - e->max_in_flight, t0 = now_ns();
-    for (; e->done_floor <= target; ++e->done_floor) {
-        const uint64_t spent = now_ns() - t0;
-        const int rc = engine_wait_done(e, e->done_floor, spent < timeout_ns ? timeout_ns - spent : 0);
-        if (rc != SCCSUM_OK) return rc;
-    }
-    return SCCSUM_OK;
+// Room (under mu) to publish k more steps now: every step up to `limit`
+// before the last of them is done — not only that one: steps finish out of
+// order (a small step behind a big one's last tile).  That also frees what
+// the new steps take over: their descriptor ring slots and done words (slot
+// s & (ring - 1), limit <= ring) and their completion counters (slot s %
+// kEngineCountSlots, limit <= kEngineCountSlots).  Else *need = the step to
+// wait for.  A caller may also free an older step's buffers once a later
+// submit returns.
+bool engine_room(sccsum_engine* e, uint32_t k, uint64_t* need) {
+    const uint64_t last = e->next_step.load(std::memory_order_relaxed) + k - 1;
+    if (last < e->limit) return true;
+    const uint64_t target = last - e->limit;
+    while (e->done_floor <= target && engine_done(e, e->done_floor)) ++e->done_floor;
+    if (e->done_floor > target) return true;
+    *need = e->done_floor;
+    return false;
 }
 
-// Write one step's descriptor over checked batches (nbatch 0: an empty step,
-// done at once) and publish it; engine_room made the room.  kind = the
-// descriptor's kind word, dep = 0 or 1 + the step its tiles wait for.
 // Packets per tile of a summing step, as a launch picks them (launch_flat):
 // about tile_bytes of packets, at most 64, and no fewer tiles than the grid
 // has waves.  The mean packet is the batches' bytes over their packets, capped
 // by max_len when the caller gives it: a batch that is a slice of a larger
 // buffer (bytes_len covers the whole buffer) would otherwise look sparse and
-// get tiles of a packet or two.
+// get tiles of a packet or two.  (The knobs are the submitting thread's.)
 uint64_t engine_tile(const sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len) {
     uint64_t n_total = 0, bytes_total = 0;
     for (uint32_t i = 0; i < nbatch; ++i) {
@@ -3347,13 +3507,16 @@ uint64_t engine_tile(const sccsum_engine* e, const sccsum_batch* batches, uint32
     return B < 1 ? 1 : (B > bmax ? bmax : B);
 }
 
-// B: packets per tile of a summing step (engine_tile); a store step's tiles
-// always hold kStoreTilePackets frames.
+// Write one step's descriptor over checked batches (nbatch 0: an empty step,
+// done at once) into its ring slot and publish it (under mu; engine_room made
+// the room).  kind = the descriptor's kind word, dep = 0 or 1 + the step its
+// tiles wait for, B = packets per tile of a summing step (engine_tile); a
+// store step's tiles always hold kStoreTilePackets frames.
 uint64_t engine_put(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint64_t kind, uint64_t dep,
                     uint64_t B) {
     if ((kind & 0xffu) == sccsum::kStepFillStore) B = sccsum::kStoreTilePackets;  // four frames per lane
-    const uint64_t s = e->next_step;
-    uint64_t* const d = e->ring_h + s * sccsum::kEngineSlotWords;
+    const uint64_t s = e->next_step.load(std::memory_order_relaxed);
+    uint64_t* const d = e->ring_h + (s & (e->ring - 1u)) * sccsum::kEngineSlotWords;
     uint64_t tile0[SCCSUM_ENGINE_MAX_BATCHES + 1] = {};
     uint32_t nq = 0;
     for (uint32_t i = 0; i < nbatch; ++i) {
@@ -3396,28 +3559,64 @@ uint64_t engine_put(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbat
         d[sccsum::kEdDep] = e->last_tiled + 1;
     }
     if (ntiles) e->last_tiled = s;
-    if (ntiles == 0) {  // nothing to sum: done at once (the descriptor still keeps the walk in order)
-        __atomic_store_n(e->ctl_h + sccsum::kEcDone + 8u * s, s + 1, __ATOMIC_RELEASE);
+    if (ntiles == 0) {  // nothing to sum: done at once (the descriptor still keeps the step numbering)
+        __atomic_store_n(e->ctl_h + sccsum::kEcDone + 8u * (s & (e->ring - 1u)), s + 1, __ATOMIC_RELEASE);
     }
     e->next_first += ntiles;
-    e->next_step = s + 1;
+    e->next_step.store(s + 1, std::memory_order_release);
     // publish: the descriptor is complete before the grid's poller can see the step
-    __atomic_store_n(e->ctl_h + sccsum::kEcPublished, e->next_step, __ATOMIC_SEQ_CST);
+    __atomic_store_n(e->ctl_h + sccsum::kEcPublished, s + 1, __ATOMIC_SEQ_CST);
     return s;
+}
+
+// Publish k (1 or 2) steps together through put() once there is room,
+// waiting for room outside the lock (other producers publish meanwhile).
+template <class Put>
+int engine_publish(sccsum_engine* e, uint32_t k, uint64_t timeout_ns, const Put& put) {
+    const uint64_t t0 = now_ns();
+    for (;;) {
+        uint64_t need = 0;
+        {
+            std::lock_guard<std::mutex> g(e->mu);
+            if (!e->running) return SCCSUM_EINVAL;  // not started, or stopped: nothing would run the step
+            if (const int rc = engine_error(e)) return rc;
+            if (engine_room(e, k, &need)) {
+                put();
+                return SCCSUM_OK;
+            }
+        }
+        const uint64_t spent = now_ns() - t0;
+        const int rc = engine_wait_done(e, need, spent < timeout_ns ? timeout_ns - spent : 0);
+        if (rc != SCCSUM_OK) return rc;
+    }
+}
+
+int engine_ms(uint32_t ms, uint32_t dflt, uint64_t* ticks) {
+    const uint64_t v = ms ? ms : dflt;
+    if (v > 3600000u) return SCCSUM_EINVAL;
+    *ticks = v * 100000ull;  // the constant 100 MHz clock
+    return SCCSUM_OK;
 }
 
 }  // namespace
 
 extern "C" {
 
-int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, sccsum_engine** out) {
+int sccsum_engine_create_opts(int device, int mode, const sccsum_engine_opts* opts, sccsum_engine** out) {
     const int base = mode & ~SCCSUM_ENGINE_FILL;
     const bool fill = (mode & SCCSUM_ENGINE_FILL) != 0;
-    if (!out || (base != SCCSUM_PIPE_IPV4 && base != SCCSUM_PIPE_SPANS) || (fill && base != SCCSUM_PIPE_IPV4) ||
-        max_steps == 0 || max_steps > sccsum::kEngineMaxSteps || max_in_flight == 0 ||
-        max_in_flight > sccsum::kEngineCountSlots || (fill && max_in_flight < 2)) {
+    if (!out || !opts || (base != SCCSUM_PIPE_IPV4 && base != SCCSUM_PIPE_SPANS) || (fill && base != SCCSUM_PIPE_IPV4)) {
         return SCCSUM_EINVAL;
     }
+    const uint32_t ring_req = opts->ring_slots ? opts->ring_slots : sccsum::kEngineDefaultRing;
+    const uint32_t mif = opts->max_in_flight ? opts->max_in_flight : 8u;
+    uint64_t idle_ticks = 0, dep_ticks = 0;
+    if (ring_req > sccsum::kEngineMaxRing || mif > sccsum::kEngineCountSlots || (fill && mif < 2) ||
+        engine_ms(opts->idle_ms, 1000u, &idle_ticks) != SCCSUM_OK || engine_ms(opts->dep_ms, 2000u, &dep_ticks) != SCCSUM_OK) {
+        return SCCSUM_EINVAL;
+    }
+    uint32_t ring = 2;
+    while (ring < ring_req) ring <<= 1;
     *out = nullptr;
     int n = 0;
     hipError_t e0 = hipGetDeviceCount(&n);
@@ -3430,10 +3629,13 @@ int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_
     e->device = device;
     e->frames = base == SCCSUM_PIPE_IPV4;
     e->fill = fill;
-    e->max_steps = max_steps;
-    e->max_in_flight = max_in_flight;
-    const uint64_t ring_bytes = uint64_t(max_steps) * sccsum::kEngineSlotWords * 8u;
-    const uint64_t ctl_bytes = (sccsum::kEcDone + 8u * uint64_t(max_steps)) * 8u;
+    e->ring = ring;
+    e->max_in_flight = mif;
+    e->limit = mif < ring ? mif : ring;
+    e->idle_ticks = idle_ticks;
+    e->dep_ticks = dep_ticks;
+    const uint64_t ring_bytes = uint64_t(ring) * sccsum::kEngineSlotWords * 8u;
+    const uint64_t ctl_bytes = (sccsum::kEcDone + 8u * uint64_t(ring)) * 8u;
     const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
     void *rh = nullptr, *ch = nullptr, *rd = nullptr, *cd = nullptr, *bk = nullptr, *dr = nullptr;
     hipError_t r = hipHostMalloc(&rh, ring_bytes, fl);
@@ -3455,28 +3657,37 @@ int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_
     e->ctl_h = static_cast<uint64_t*>(ch);
     e->args.hring = static_cast<const uint64_t*>(rd);
     e->args.dring = static_cast<uint64_t*>(dr);
+    e->args.ring_mask = ring - 1u;
     e->args.ctl = static_cast<uint64_t*>(cd);
     e->blk = bk;
     uint8_t* const b = static_cast<uint8_t*>(bk);
-    e->args.claims = reinterpret_cast<uint32_t*>(b + EngineBlock::kClaims);
+    e->args.claims = reinterpret_cast<uint64_t*>(b + EngineBlock::kClaims);
     e->args.mirror = reinterpret_cast<uint64_t*>(b + EngineBlock::kMirror);
     e->args.sdone = reinterpret_cast<uint64_t*>(b + EngineBlock::kSdone);
     e->args.counts = reinterpret_cast<uint32_t*>(b + EngineBlock::kCounts);
     e->args.gdone = reinterpret_cast<uint32_t*>(b + EngineBlock::kGdone);
-    e->args.idle_ticks = 100000000ull;  // 1 s at the constant 100 MHz clock
-    e->args.dep_ticks = 200000000ull;   // 2 s
+    e->args.idle_ticks = idle_ticks;
+    e->args.dep_ticks = dep_ticks;
     *out = e;
     return SCCSUM_OK;
 }
 
+int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, sccsum_engine** out) {
+    if (max_steps == 0 || max_in_flight == 0) return SCCSUM_EINVAL;
+    const sccsum_engine_opts o = {max_steps, max_in_flight, 0u, 0u};
+    return sccsum_engine_create_opts(device, mode, &o, out);
+}
+
 int sccsum_engine_start(sccsum_engine* e, void* stream) {
-    if (!e || e->running) return SCCSUM_EINVAL;
+    if (!e) return SCCSUM_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (e->running) return SCCSUM_EINVAL;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     int dev = 0;
     if (const int rc = sccsum::launch_device(s, &dev); rc != SCCSUM_OK) return rc;
     if (dev != e->device) return SCCSUM_EINVAL;
     {
-        std::lock_guard<std::mutex> g(g_live_mu);
+        std::lock_guard<std::mutex> gl(g_live_mu);
         if (g_live[dev] != nullptr) return SCCSUM_EBUSY;  // another engine's run holds the device
         g_live[dev] = e;
     }
@@ -3489,9 +3700,10 @@ int sccsum_engine_start(sccsum_engine* e, void* stream) {
         }
     }
     // a new run: no step published, none done, counters zero (stream-ordered before the grid).
-    // A run that gave up (EIDLE, a dependency fault) may have left completion counters behind.
+    // A run that gave up (EIDLE, a fault) may have left completion counters behind.
     if (__atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE)) e->dirty = true;
-    std::memset(e->ctl_h, 0, (sccsum::kEcDone + 8u * e->next_step) * 8u);  // the words the last run wrote
+    const uint64_t used = e->next_step.load(std::memory_order_relaxed);  // the done words the last run wrote
+    std::memset(e->ctl_h, 0, (sccsum::kEcDone + 8u * (used < e->ring ? used : e->ring)) * 8u);
     std::atomic_thread_fence(std::memory_order_seq_cst);
     hipError_t r = hipMemsetAsync(e->blk, 0, e->dirty ? EngineBlock::kBytes : EngineBlock::kReset, s);
     if (r != hipSuccess) {
@@ -3503,7 +3715,8 @@ int sccsum_engine_start(sccsum_engine* e, void* stream) {
     if (K.engine_wt) flags |= sccsum::kFlagEngineWT;
     if (!K.short_chunks) flags |= sccsum::kFlagFullChunks;
     flags |= static_cast<uint32_t>(K.run_align == 8 ? 2 : (K.run_align == 4 ? 1 : 0)) << sccsum::kRunAlignShift;
-    e->args.idle_ticks = static_cast<uint64_t>(K.engine_idle_ms) * 100000ull;  // 100 MHz ticks
+    // the engine's idle limit, unless this thread's diagnostic knob overrides it
+    e->args.idle_ticks = K.engine_idle_ms > 0 ? static_cast<uint64_t>(K.engine_idle_ms) * 100000ull : e->idle_ticks;
     r = e->fill ? sccsum::launch_engine<true, true>(s, dev, e->args, flags, &e->waves)
                 : (e->frames ? sccsum::launch_engine<true>(s, dev, e->args, flags, &e->waves)
                              : sccsum::launch_engine<false>(s, dev, e->args, flags, &e->waves));
@@ -3515,7 +3728,7 @@ int sccsum_engine_start(sccsum_engine* e, void* stream) {
     e->launched = true;
     e->stream = s;
     e->running = true;
-    e->next_step = 0;
+    e->next_step.store(0, std::memory_order_release);
     e->next_first = 0;
     e->last_tiled = ~0ull;
     e->done_floor = 0;
@@ -3525,11 +3738,11 @@ int sccsum_engine_start(sccsum_engine* e, void* stream) {
 
 int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
                          uint64_t timeout_ns, uint64_t* step) {
-    if (!e || !e->running || !step) return SCCSUM_EINVAL;
+    if (!e || !step) return SCCSUM_EINVAL;
     if (const int rc = engine_check(e, batches, nbatch, false); rc != SCCSUM_OK) return rc;
-    if (const int rc = engine_room(e, 1, timeout_ns); rc != SCCSUM_OK) return rc;
-    *step = engine_put(e, batches, nbatch, sccsum::kStepSum, 0, engine_tile(e, batches, nbatch, max_len));
-    return SCCSUM_OK;
+    return engine_publish(e, 1, timeout_ns, [&] {
+        *step = engine_put(e, batches, nbatch, sccsum::kStepSum, 0, engine_tile(e, batches, nbatch, max_len));
+    });
 }
 
 // In-place fill as two steps published together: the generate step, then the
@@ -3544,8 +3757,7 @@ int sccsum_engine_submit(sccsum_engine* e, const sccsum_batch* batches, uint32_t
 int sccsum_engine_submit_fill(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbatch, uint32_t max_len,
                               uint32_t mode, uint64_t timeout_ns, uint64_t* step) {
     constexpr uint32_t kEngineModes = SCCSUM_FILL_IP | SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO;
-    if (!e || !e->running || !step || !e->fill || (mode & ~kEngineModes) ||
-        !(mode & (SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO))) {
+    if (!e || !step || !e->fill || (mode & ~kEngineModes) || !(mode & (SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO))) {
         return SCCSUM_EINVAL;
     }
     if (const int rc = engine_check(e, batches, nbatch, true); rc != SCCSUM_OK) return rc;
@@ -3555,55 +3767,61 @@ int sccsum_engine_submit_fill(sccsum_engine* e, const sccsum_batch* batches, uin
     // step, no wait on the generate step: a store step's waves hold the next
     // fill's tiles while they wait, which chained small fills one after another)
     const bool single = n_total <= sccsum::t_knobs.fill_single_max;
-    if (const int rc = engine_room(e, single ? 1 : 2, timeout_ns); rc != SCCSUM_OK) return rc;
     const uint64_t kflags = ((mode & SCCSUM_FILL_L4) ? sccsum::kFlagFillL4 : 0u) |
                             ((mode & SCCSUM_FILL_ICMP_ECHO) ? sccsum::kFlagFillIcmp : 0u) |
                             ((mode & SCCSUM_FILL_IP) ? sccsum::kFlagFillIp : 0u) |
                             (single ? sccsum::kFlagFillNow : 0u);
+    const uint64_t gen_kind = sccsum::kStepFillGen | (kflags << 8) | (uint64_t(mode) << 16);
     if (single) {
-        *step = engine_put(e, batches, nbatch, sccsum::kStepFillGen | (kflags << 8) | (uint64_t(mode) << 16), 0,
-                           engine_tile(e, batches, nbatch, max_len));
-        return SCCSUM_OK;
+        return engine_publish(e, 1, timeout_ns, [&] {
+            *step = engine_put(e, batches, nbatch, gen_kind, 0, engine_tile(e, batches, nbatch, max_len));
+        });
     }
     // (cutting a 1 Mi-frame fill into two one-pass steps of 512 Ki did not help:
     // 343.6 us a fill against 330 in two passes; profiles/r05_fill_one_pass.log)
-    const uint64_t gen = engine_put(e, batches, nbatch, sccsum::kStepFillGen | (kflags << 8) | (uint64_t(mode) << 16),
-                                    0, engine_tile(e, batches, nbatch, max_len));
     // the store half: no status (the generate half reported it)
     sccsum_batch st[SCCSUM_ENGINE_MAX_BATCHES];
     for (uint32_t i = 0; i < nbatch; ++i) {
         st[i] = batches[i];
         st[i].d_status = nullptr;
     }
-    *step = engine_put(e, st, nbatch, sccsum::kStepFillStore | (uint64_t(mode) << 16), gen + 1, 0);
-    return SCCSUM_OK;
+    return engine_publish(e, 2, timeout_ns, [&] {
+        const uint64_t gen = engine_put(e, batches, nbatch, gen_kind, 0, engine_tile(e, batches, nbatch, max_len));
+        *step = engine_put(e, st, nbatch, sccsum::kStepFillStore | (uint64_t(mode) << 16), gen + 1, 0);
+    });
 }
 
 int sccsum_engine_wait(sccsum_engine* e, uint64_t step, uint64_t timeout_ns) {
-    if (!e || step >= e->next_step) return SCCSUM_EINVAL;
+    if (!e || step >= e->next_step.load(std::memory_order_acquire)) return SCCSUM_EINVAL;
     return engine_wait_done(e, step, timeout_ns);
 }
 
 int sccsum_engine_stop(sccsum_engine* e) {
-    if (!e || !e->running) return SCCSUM_EINVAL;
-    __atomic_store_n(e->ctl_h + sccsum::kEcStop, 1ull, __ATOMIC_SEQ_CST);
+    if (!e) return SCCSUM_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!e->running) return SCCSUM_EINVAL;
+    __atomic_store_n(e->ctl_h + sccsum::kEcStop, 1ull, __ATOMIC_SEQ_CST);  // after every published step (mu)
     e->running = false;
     release_live(e);  // the grid leaves once the published steps are done
-    return __atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE) ? SCCSUM_EIDLE : SCCSUM_OK;
+    // the grid gave up before the call with published steps not (yet) done
+    const int err = engine_error(e);
+    return err && !engine_all_done(e) ? err : SCCSUM_OK;
 }
 
 int sccsum_engine_destroy(sccsum_engine* e) {
     if (!e) return SCCSUM_OK;
-    int rc = SCCSUM_OK;
-    if (e->running) {
-        (void)sccsum_engine_stop(e);
-        rc = static_cast<int>(hipStreamSynchronize(e->stream));
-    } else if (e->stream) {
-        rc = static_cast<int>(hipStreamSynchronize(e->stream));
+    bool running;
+    {
+        std::lock_guard<std::mutex> g(e->mu);
+        running = e->running;
     }
-    // the grid has left: a give-up after the stop is visible now
-    if (rc == SCCSUM_OK && e->launched && __atomic_load_n(e->ctl_h + sccsum::kEcError, __ATOMIC_ACQUIRE)) {
-        rc = SCCSUM_EIDLE;
+    if (running) (void)sccsum_engine_stop(e);
+    int rc = e->stream ? static_cast<int>(hipStreamSynchronize(e->stream)) : SCCSUM_OK;
+    // The grid has left: a published step that is not done was lost (ADVICE
+    // r05: an idle give-up after every step was done loses nothing)
+    if (rc == SCCSUM_OK && e->launched) {
+        std::lock_guard<std::mutex> g(e->mu);
+        if (!engine_all_done(e)) rc = engine_error(e) ? engine_error(e) : SCCSUM_EFAULT;
     }
     (void)hipHostFree(e->ring_h);
     (void)hipHostFree(e->ctl_h);
@@ -3622,6 +3840,7 @@ const char* sccsum_strerror(int err) {
     if (err == SCCSUM_ENODEV) return "no such HIP device";
     if (err == SCCSUM_EBUSY) return "busy: every batch slot or engine step is in flight, or the device's engine is running";
     if (err == SCCSUM_EIDLE) return "the engine's grid gave up waiting for steps";
+    if (err == SCCSUM_EFAULT) return "the engine's grid stopped on an internal fault";
     if (err > 0) return hipGetErrorString(static_cast<hipError_t>(err));
     return "unknown sccsum error";
 }
@@ -3912,7 +4131,7 @@ int sccsum_set_engine_sync_every(int steps) {
 }
 
 int sccsum_set_engine_idle_ms(int ms) {
-    if (ms < 1 || ms > 3600000) return SCCSUM_EINVAL;
+    if (ms < 0 || ms > 3600000) return SCCSUM_EINVAL;
     sccsum::t_knobs.engine_idle_ms = ms;
     return SCCSUM_OK;
 }

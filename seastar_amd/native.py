@@ -22,6 +22,7 @@ SCCSUM_EINVAL = -1
 SCCSUM_ENODEV = -2
 SCCSUM_EBUSY = -3
 SCCSUM_EIDLE = -4
+SCCSUM_EFAULT = -5
 ST_OK = 0x01
 ST_L4_OK = 0x02
 ST_MALFORMED = 0x04
@@ -32,7 +33,7 @@ FILL_L4 = 0x02
 FILL_L4_PSEUDO = 0x04
 FILL_TSO = 0x08
 FILL_ICMP_ECHO = 0x10
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class SccsumError(RuntimeError):
@@ -101,6 +102,7 @@ _PROTOS = {
     "sccsum_host_alloc": (ctypes.c_int, [ctypes.POINTER(_vp), _u64]),
     "sccsum_host_free": (ctypes.c_int, [_vp]),
     "sccsum_engine_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _u32, _u32, ctypes.POINTER(_vp)]),
+    "sccsum_engine_create_opts": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, ctypes.POINTER(_vp)]),
     "sccsum_engine_start": (ctypes.c_int, [_vp, _vp]),
     "sccsum_engine_submit": (ctypes.c_int, [_vp, _vp, _u32, _u32, _u64, ctypes.POINTER(_u64)]),
     "sccsum_engine_submit_fill": (ctypes.c_int, [_vp, _vp, _u32, _u32, _u32, _u64, ctypes.POINTER(_u64)]),
@@ -132,6 +134,12 @@ class Batch(ctypes.Structure):
 MAX_BATCHES = 16
 FILL_SINGLE_MAX = 524288  # in-place fills of at most this many frames run in one pass (sccsum_diag.h)
 ENGINE_MAX_BATCHES = 4
+
+
+class EngineOpts(ctypes.Structure):
+    """sccsum_engine_opts: a resident engine's limits (0 = the default)."""
+    _fields_ = [("ring_slots", ctypes.c_uint32), ("max_in_flight", ctypes.c_uint32), ("idle_ms", ctypes.c_uint32),
+                ("dep_ms", ctypes.c_uint32)]
 
 
 class Fragment(ctypes.Structure):

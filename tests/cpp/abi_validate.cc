@@ -128,8 +128,20 @@ static void checks() {
     EXPECT(sccsum_engine_stop(nullptr) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_destroy(nullptr) == SCCSUM_OK);
     EXPECT(sccsum_set_engine_write_through(0) == SCCSUM_OK && sccsum_set_engine_write_through(1) == SCCSUM_OK);
-    EXPECT(sccsum_set_engine_idle_ms(0) == SCCSUM_EINVAL && sccsum_set_engine_idle_ms(3600001) == SCCSUM_EINVAL);
-    EXPECT(sccsum_set_engine_idle_ms(250) == SCCSUM_OK && sccsum_set_engine_idle_ms(1000) == SCCSUM_OK);
+    EXPECT(sccsum_set_engine_idle_ms(-1) == SCCSUM_EINVAL && sccsum_set_engine_idle_ms(3600001) == SCCSUM_EINVAL);
+    EXPECT(sccsum_set_engine_idle_ms(250) == SCCSUM_OK && sccsum_set_engine_idle_ms(0) == SCCSUM_OK);
+    // create with every limit (ABI 4): ranges are checked before any runtime call
+    const sccsum_engine_opts big_ring = {65537, 8, 0, 0}, many = {1024, 65, 0, 0}, idle = {1024, 8, 3600001, 0},
+                             dep = {1024, 8, 0, 3600001}, fill1 = {1024, 1, 0, 0};
+    EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4, nullptr, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4, &big_ring, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4, &many, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_SPANS, &idle, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_SPANS, &dep, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4 | SCCSUM_ENGINE_FILL, &fill1, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_SPANS | SCCSUM_ENGINE_FILL, &many, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4, &big_ring, nullptr) == SCCSUM_EINVAL);
+    EXPECT(eng == nullptr);
     EXPECT(sccsum_set_engine_sync_every(-2) == SCCSUM_EINVAL && sccsum_set_engine_sync_every(65537) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_engine_sync_every(20) == SCCSUM_OK && sccsum_set_engine_sync_every(0) == SCCSUM_OK);
     EXPECT(sccsum_set_engine_sync_every(-1) == SCCSUM_OK);
@@ -193,6 +205,7 @@ static void checks() {
     EXPECT(std::strcmp(sccsum_strerror(SCCSUM_EBUSY),
                        "busy: every batch slot or engine step is in flight, or the device's engine is running") == 0);
     EXPECT(std::strcmp(sccsum_strerror(-99), "unknown sccsum error") == 0);
+    EXPECT(std::strcmp(sccsum_strerror(SCCSUM_EFAULT), "the engine's grid stopped on an internal fault") == 0);
     EXPECT(sccsum_abi_version() == SCCSUM_ABI_VERSION);
 }
 

@@ -10,6 +10,14 @@
 // (a new stream may get the old one's address while that launch still runs).
 // Every result is checked against the oracle (test infrastructure, linked
 // into this test program only).  Usage: shards_gpu [threads] [rounds].
+//
+// shards_gpu engine [threads] [steps]: the shards of ONE GPU feeding its one
+// resident engine (include/sccsum.h, "Producers"; Seastar's per-core
+// reactors, src/core/reactor.cc:3437-3441, forwarding to the GPU's owner,
+// src/net/net.cc:309-322): a frames + fill engine with a 64-slot ring, then a
+// spans engine, each taking random steps from every thread at once — frames
+// (generate, verify-only, both), in-place fills, seeded spans — every step's
+// results against the oracle.
 #include <hip/hip_runtime.h>
 
 #include "sccsum.h"
@@ -17,6 +25,7 @@
 #include "sccsum_oracle.h"
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -31,6 +40,7 @@ std::atomic<int> g_bad{0};
 std::mutex g_print;
 unsigned long long g_devices_used = 0;  // under g_print
 std::atomic<int> g_cross_checked{0};    // launches refused on another device's stream
+long g_engine_steps = 0;                // under g_print: steps the engine producers checked
 
 void fail(int shard, const char* what, long i) {
     if (g_bad.fetch_add(1) < 20) {
@@ -288,9 +298,187 @@ void shard_main(int shard, int rounds) {
     release(dB);
 }
 
+// ---- the shards of one GPU feeding its one resident engine ---------------------
+
+// A start line every producer waits at (C++17: no std::barrier).
+struct Gate {
+    std::mutex mu;
+    std::condition_variable cv;
+    int waiting = 0, generation = 0;
+    void arrive(int parties) {
+        std::unique_lock<std::mutex> l(mu);
+        const int gen = generation;
+        if (++waiting == parties) {
+            waiting = 0;
+            ++generation;
+            cv.notify_all();
+        } else {
+            cv.wait(l, [&] { return generation != gen; });
+        }
+    }
+};
+
+struct ProducerStep {
+    int kind;          // 0 frames (A generate + B verify-only), 1 A verify-only, 2 fill of copy r, 3 spans
+    int round;
+    uint64_t step;
+};
+
+// One shard: its own frames and buffers (uploaded before the run: while the
+// grid runs, a device-to-device copy would queue behind it), `steps` random
+// steps submitted into the shared engine (sometimes waiting on one), and after
+// the owner's stop every result against the oracle.  gate: 0 = buffers ready,
+// 1 = submits done, 2 = the run has stopped.
+void producer_main(int shard, sccsum_engine* e, bool spans, int steps, Gate* gate, int parties) {
+    std::mt19937_64 rng(0xE61E5ull + 104729ull * shard + (spans ? 7 : 0));
+    if (!ok(sccsum_init(0), shard, "sccsum_init")) {
+        for (int k = 0; k < 4; ++k) gate->arrive(parties);
+        return;
+    }
+    const uint32_t n = 200 + static_cast<uint32_t>(rng() % 600);
+    Frames A = make_frames(rng, n), B = make_frames(rng, n / 3 + 1);
+    std::vector<uint16_t> wantA(2 * n), wantB(2 * B.off.size()), want_sp(n), want_fout(2 * n);
+    std::vector<uint8_t> wstA(n), wstB(B.off.size()), want_fst(n), want_fill = A.bytes;
+    std::vector<uint32_t> seeds(n);
+    for (auto& s : seeds) s = static_cast<uint32_t>(rng() & 0xffff);
+    const uint32_t fmode = SCCSUM_FILL_IP | SCCSUM_FILL_L4 | SCCSUM_FILL_ICMP_ECHO;
+    oracle_batch_ipv4(A.bytes.data(), A.off.data(), A.len.data(), wantA.data(), wstA.data(), n, 1);
+    oracle_batch_ipv4(B.bytes.data(), B.off.data(), B.len.data(), wantB.data(), wstB.data(), B.off.size(), 1);
+    oracle_batch_spans(A.bytes.data(), A.off.data(), A.len.data(), seeds.data(), want_sp.data(), n, 1);
+    oracle_batch_ipv4_fill(want_fill.data(), A.off.data(), A.len.data(), want_fout.data(), want_fst.data(), n, fmode);
+    DevBatch dA, dB;
+    const size_t cap = (A.bytes.size() + 15) & ~size_t(15);
+    uint8_t *fills = nullptr, *st = nullptr;
+    uint16_t* outs = nullptr;
+    uint32_t* d_seed = nullptr;
+    // per step: 2n + 2|B| values, n + 1 status bytes; a fill copy of A per step
+    const size_t per_out = 2 * (size_t(n) + B.off.size()), per_st = n;
+    bool good = upload(A, dA, shard) && upload(B, dB, shard) &&
+                hip_ok(hipMalloc(&fills, cap * steps), shard, "malloc") &&
+                hip_ok(hipMalloc(&outs, 2 * per_out * steps), shard, "malloc") &&
+                hip_ok(hipMalloc(&st, per_st * steps), shard, "malloc") &&
+                hip_ok(hipMalloc(&d_seed, 4 * n), shard, "malloc") &&
+                hip_ok(hipMemcpy(d_seed, seeds.data(), 4 * n, hipMemcpyHostToDevice), shard, "copy") &&
+                hip_ok(hipMemset(outs, 0xEE, 2 * per_out * steps), shard, "memset") &&
+                hip_ok(hipMemset(st, 0xEE, per_st * steps), shard, "memset");
+    for (int r = 0; good && r < steps; ++r) {
+        good = hip_ok(hipMemcpy(fills + cap * r, A.bytes.data(), A.bytes.size(), hipMemcpyHostToDevice), shard,
+                      "copy");
+    }
+    good = good && hip_ok(hipDeviceSynchronize(), shard, "sync");
+    std::vector<ProducerStep> done;
+    gate->arrive(parties);  // 0: every shard's buffers are in place; the owner starts the run
+    gate->arrive(parties);  // (the run is started)
+    for (int r = 0; good && r < steps; ++r) {
+        uint16_t* o = outs + per_out * r;
+        uint8_t* s = st + per_st * r;
+        ProducerStep ps{spans ? 3 : static_cast<int>(rng() % 3), r, 0};
+        int rc;
+        if (ps.kind == 3) {
+            const sccsum_batch b = {dA.bytes, dA.bytes_len, dA.off, dA.len, d_seed, o, s, n};
+            rc = sccsum_engine_submit(e, &b, 1, 3100, 10'000'000'000ull, &ps.step);
+        } else if (ps.kind == 0) {
+            const sccsum_batch b[2] = {{dA.bytes, dA.bytes_len, dA.off, dA.len, nullptr, o, nullptr, n},
+                                       {dB.bytes, dB.bytes_len, dB.off, dB.len, nullptr, o + 2 * n, s, dB.n}};
+            rc = sccsum_engine_submit(e, b, 2, 3100, 10'000'000'000ull, &ps.step);
+        } else if (ps.kind == 1) {
+            const sccsum_batch b = {dA.bytes, dA.bytes_len, dA.off, dA.len, nullptr, nullptr, s, n};
+            rc = sccsum_engine_submit(e, &b, 1, 3100, 10'000'000'000ull, &ps.step);
+        } else {
+            const sccsum_batch b = {fills + cap * r, dA.bytes_len, dA.off, dA.len, nullptr, o, s, n};
+            rc = sccsum_engine_submit_fill(e, &b, 1, 3100, fmode, 10'000'000'000ull, &ps.step);
+        }
+        if (!ok(rc, shard, "engine submit")) break;
+        done.push_back(ps);
+        if (rng() % 8 == 0) ok(sccsum_engine_wait(e, ps.step, 10'000'000'000ull), shard, "engine wait");
+    }
+    for (const ProducerStep& ps : done) ok(sccsum_engine_wait(e, ps.step, 10'000'000'000ull), shard, "engine wait");
+    gate->arrive(parties);  // 1: submits done
+    gate->arrive(parties);  // 2: the owner stopped the run (device copies run again)
+    if (good) {
+        const std::vector<uint16_t> ho = fetch(outs, per_out * steps, shard);
+        const std::vector<uint8_t> hs = fetch(st, per_st * steps, shard);
+        const std::vector<uint8_t> hf = fetch(fills, cap * steps, shard);
+        for (const ProducerStep& ps : done) {
+            const uint16_t* o = ho.data() + per_out * ps.round;
+            const uint8_t* s = hs.data() + per_st * ps.round;
+            bool same = true;
+            if (ps.kind == 3) {
+                same = std::memcmp(o, want_sp.data(), 2 * size_t(n)) == 0;
+                for (uint32_t i = 0; same && i < n; ++i) same = s[i] == (want_sp[i] == 0 ? 1 : 0);
+            } else if (ps.kind == 0) {
+                same = std::memcmp(o, wantA.data(), 4 * size_t(n)) == 0 &&
+                       std::memcmp(o + 2 * n, wantB.data(), 4 * B.off.size()) == 0 &&
+                       std::memcmp(s, wstB.data(), B.off.size()) == 0;
+            } else if (ps.kind == 1) {
+                same = std::memcmp(s, wstA.data(), n) == 0;
+            } else {
+                same = std::memcmp(o, want_fout.data(), 4 * size_t(n)) == 0 &&
+                       std::memcmp(s, want_fst.data(), n) == 0 &&
+                       std::memcmp(hf.data() + cap * ps.round, want_fill.data(), A.bytes.size()) == 0;
+            }
+            if (!same) fail(shard, ps.kind == 3 ? "engine spans step" : (ps.kind == 2 ? "engine fill step"
+                                                                        : "engine frames step"), ps.round);
+        }
+    }
+    for (void* q : {static_cast<void*>(fills), static_cast<void*>(outs), static_cast<void*>(st),
+                    static_cast<void*>(d_seed)}) {
+        (void)hipFree(q);
+    }
+    release(dA);
+    release(dB);
+    std::lock_guard<std::mutex> l(g_print);
+    g_engine_steps += static_cast<long>(done.size());
+}
+
+// One engine run fed by `threads` producers: frames + fills, or spans.
+int engine_run(int threads, int steps, bool spans) {
+    if (sccsum_init(0) != SCCSUM_OK) return 1;
+    sccsum_engine* e = nullptr;
+    const sccsum_engine_opts o = {64, 16, 0, 0};  // a 64-slot ring: every slot reused many times
+    if (!ok(sccsum_engine_create_opts(0, spans ? SCCSUM_PIPE_SPANS : (SCCSUM_PIPE_IPV4 | SCCSUM_ENGINE_FILL), &o, &e),
+            -1, "engine create")) {
+        return 1;
+    }
+    hipStream_t s;
+    if (!hip_ok(hipStreamCreate(&s), -1, "stream")) return 1;
+    Gate gate;
+    const int parties = threads + 1;
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t) ts.emplace_back(producer_main, t, e, spans, steps, &gate, parties);
+    gate.arrive(parties);  // 0: buffers in place
+    const bool started = ok(sccsum_engine_start(e, s), -1, "engine start");
+    gate.arrive(parties);  // the run is started (a producer's submit on a stopped engine is SCCSUM_EINVAL)
+    gate.arrive(parties);  // 1: every producer's steps are done
+    if (started) {
+        ok(sccsum_engine_stop(e), -1, "engine stop");
+        hip_ok(hipStreamSynchronize(s), -1, "sync");
+    }
+    gate.arrive(parties);  // 2
+    for (auto& t : ts) t.join();
+    ok(sccsum_engine_destroy(e), -1, "engine destroy");
+    (void)hipStreamDestroy(s);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
+    if (argc > 1 && std::strcmp(argv[1], "engine") == 0) {
+        const int threads = argc > 2 ? std::atoi(argv[2]) : 8;
+        const int steps = argc > 3 ? std::atoi(argv[3]) : 40;
+        engine_run(threads, steps, false);
+        const long frame_steps = g_engine_steps;
+        engine_run(threads, steps, true);
+        if (g_bad.load()) {
+            std::printf("shards_gpu engine: FAILED (%d)\n", g_bad.load());
+            return 1;
+        }
+        std::printf("shards_gpu engine: OK (%d producer threads into one engine per run: %ld frame / fill steps, "
+                    "then %ld span steps, every result against the oracle)\n",
+                    threads, frame_steps, g_engine_steps - frame_steps);
+        return 0;
+    }
     const int threads = argc > 1 ? std::atoi(argv[1]) : 8;
     const int rounds = argc > 2 ? std::atoi(argv[2]) : 6;
     std::vector<std::thread> ts;

@@ -33,7 +33,9 @@ def test_launcher_starts_n_ranks_without_device(n):
     # the per_rank block a real N > 1 line carries: one entry per rank, in rank order
     assert [r["rank"] for r in d["per_rank"]] == list(range(n))
     assert all({"device", "pci_bus_id", "host", "wall_s", "GiBps", "avg_launch_us", "read_ceiling_GBps", "numa_node",
-                "cpus", "affinity", "mempolicy"} <= set(r) for r in d["per_rank"])
+                "cpus", "affinity", "mempolicy", "launch"} <= set(r) for r in d["per_rank"])
+    # what each rank runs: the headline's default, one resident engine per rank
+    assert [r["launch"] for r in d["per_rank"]] == ["engine"] * n
 
 
 def test_ranks_land_on_distinct_devices_in_the_dry_run():
@@ -49,6 +51,8 @@ def test_ranks_land_on_distinct_devices_in_the_dry_run():
     d = _bench("--gpus", "2", "--dry-run", "--numa", "off", "--share-devices",
                extra_env={"SCCSUM_DRY_RUN_BDFS": "0000:05:00.0", "SCCSUM_DRY_RUN_NDEV": "1"})
     assert [r["device"] for r in d["per_rank"]] == [0, 0]
+    # ranks sharing a device launch (an engine grid would hold the device for one rank)
+    assert [r["launch"] for r in d["per_rank"]] == ["multi", "multi"]
 
 
 def test_shared_device_without_the_flag_stops_every_rank():
@@ -94,6 +98,7 @@ def test_launcher_two_ranks_on_the_gpu():
     assert [r["rank"] for r in pr] == [0, 1]
     for r in pr:  # real figures per rank: the device it ran on, its own rate, launch time and read ceiling
         assert r["pci_bus_id"] and r["GiBps"] > 0 and r["avg_launch_us"] > 0 and r["read_ceiling_GBps"] > 0
+        assert r["launch"] == "multi"  # ranks sharing the one device launch (no engine grid per rank)
         assert 0 < r["frac"] < 1
         # locality: the GPU's NUMA node (-1 on a one-node host) and the CPUs the rank was bound to
         assert isinstance(r["numa_node"], int) and r["cpus"] and r["affinity"] and r["mempolicy"]

@@ -38,7 +38,7 @@ def test_library_loads_and_binds_every_symbol():
     lib = native.load()
     for s in native.header_symbols():
         assert hasattr(lib, s)
-    assert lib.sccsum_abi_version() == native.ABI_VERSION == 3
+    assert lib.sccsum_abi_version() == native.ABI_VERSION == 4
     assert lib.sccsum_strerror(0) == b"success"
     assert lib.sccsum_strerror(native.SCCSUM_EINVAL) == b"invalid argument"
 

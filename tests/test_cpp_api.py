@@ -177,3 +177,17 @@ def test_shards_cpp_program_on_gpu(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK" in r.stdout
     print(r.stdout)
+
+
+@pytest.mark.gpu
+def test_shards_feed_one_engine_on_gpu(tmp_path):
+    """The shards of one GPU feeding its ONE resident engine (VERDICT r05 #2;
+    include/sccsum.h "Producers"): 8 host threads submit random frame,
+    verify-only, fill and (second run) seeded span steps into one engine with
+    a 64-slot ring at once, each waiting on its own steps; every step's
+    results against the oracle."""
+    exe = _shards_exe(tmp_path)
+    r = subprocess.run([exe, "engine", "8", "40"], capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout
+    print(r.stdout)

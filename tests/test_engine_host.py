@@ -8,10 +8,34 @@ import torch
 from seastar_amd import batch, native
 
 
-def _engine(frames: bool, fill: bool = False) -> batch.Engine:
+def _engine(frames: bool, fill: bool = False, lib=None) -> batch.Engine:
+    import threading
+
     e = object.__new__(batch.Engine)  # no device here: skip sccsum_engine_create
     e.frames, e.fill, e.max_in_flight, e._keep, e._h = frames, fill, 2, {}, None
+    e._mu, e._last, e._lib = threading.Lock(), -1, lib
     return e
+
+
+class _FakeLib:
+    """Stands in for libsccsum's engine entry points: records the calls and
+    returns the codes a run that went wrong would."""
+
+    def __init__(self, destroy=0, wait=0, stop=0):
+        self.codes = {"destroy": destroy, "wait": wait, "stop": stop}
+        self.calls = []
+
+    def sccsum_engine_destroy(self, h):
+        self.calls.append(("destroy", h))
+        return self.codes["destroy"]
+
+    def sccsum_engine_wait(self, h, step, timeout_ns):
+        self.calls.append(("wait", step))
+        return self.codes["wait"]
+
+    def sccsum_engine_stop(self, h):
+        self.calls.append(("stop", h))
+        return self.codes["stop"]
 
 
 def _batch(n=4, step=64):
@@ -62,3 +86,47 @@ def test_close_without_a_handle_is_a_no_op():
     e = _engine(True)
     e.close()
     e.close()
+
+
+@pytest.mark.parametrize("code", [native.SCCSUM_EIDLE, native.SCCSUM_EFAULT])
+def test_close_raises_when_the_run_left_a_step_undone(code):
+    """sccsum_engine_destroy's report of a run that left a
+    published step undone (SCCSUM_EIDLE, SCCSUM_EFAULT) raises from close()
+    instead of being dropped; the handle is released either way, and a
+    second close is a no-op."""
+    lib = _FakeLib(destroy=code)
+    e = _engine(True, lib=lib)
+    e._h = 0x1234
+    with pytest.raises(native.SccsumError) as err:
+        e.close()
+    assert err.value.code == code
+    assert lib.calls == [("destroy", 0x1234)] and e._h is None
+    e.close()
+    assert lib.calls == [("destroy", 0x1234)]
+    ok = _FakeLib()
+    e2 = _engine(True, lib=ok)
+    e2._h = 0x99
+    e2.close()
+    assert ok.calls == [("destroy", 0x99)]
+
+
+def test_finish_waits_on_the_last_step_then_stops():
+    """finish(): wait on the run's latest step, then stop — and a give-up seen
+    by the wait raises after the stop was still made (the grid must leave)."""
+    lib = _FakeLib()
+    e = _engine(True, lib=lib)
+    e._h, e._last = 0x10, 41
+    e.finish()
+    assert lib.calls == [("wait", 41), ("stop", 0x10)]
+    bad = _FakeLib(wait=native.SCCSUM_EIDLE)
+    e = _engine(True, lib=bad)
+    e._h, e._last = 0x11, 7
+    with pytest.raises(native.SccsumError) as err:
+        e.finish()
+    assert err.value.code == native.SCCSUM_EIDLE
+    assert bad.calls == [("wait", 7), ("stop", 0x11)]
+    none = _FakeLib()
+    e = _engine(True, lib=none)
+    e._h = 0x12
+    e.finish()  # no step submitted: nothing to wait on
+    assert none.calls == [("stop", 0x12)]

@@ -57,7 +57,7 @@ def test_engine_frames_steps_match_oracle_and_multi(dev):
             wants.append((want, want_st))
         steps.append((items, wants))
     torch.cuda.synchronize()
-    eng = batch.Engine(0, frames=True, max_steps=64, max_in_flight=2)
+    eng = batch.Engine(0, frames=True, ring_slots=64, max_in_flight=2)
     stream = torch.cuda.Stream(device=dev)
     eng.start(stream)
     ids = [eng.submit(items) for items, _ in steps]
@@ -84,7 +84,7 @@ def test_engine_spans_with_seeds(dev):
     """Seeded spans (the cfg 4 shape, smaller): steps of Zipf spans and 64 KiB
     segments with pseudo-header seeds, against the oracle."""
     rng = np.random.default_rng(0xE2)
-    eng = batch.Engine(0, frames=False, max_steps=32, max_in_flight=3)
+    eng = batch.Engine(0, frames=False, ring_slots=32, max_in_flight=3)
     stream = torch.cuda.Stream(device=dev)
     steps = []
     for s in range(12):
@@ -115,34 +115,38 @@ def test_engine_spans_with_seeds(dev):
     eng.close()
 
 
-def test_engine_runs_restart_and_limits(dev):
-    """A run takes at most max_steps steps (then EBUSY); stop and start begin a
-    new run on the same engine; empty steps complete at once and the grid walks
-    past them; wait on a step never submitted is refused."""
+def test_engine_runs_restart_and_outlast_their_ring(dev):
+    """A run takes any number of steps: with a ring of 5 (rounded up to 8)
+    descriptor slots, 3 runs of 30 steps each (real and empty ones) all
+    complete exact (ABI 4; a run of max_steps steps used to end in EBUSY);
+    stop and start begin a new run on the same engine; empty steps complete at
+    once and the grid walks past them; wait on a step never submitted is
+    refused."""
     rng = np.random.default_rng(0xE3)
     b, want, want_st = _frames_step(rng, dev, 0)
-    eng = batch.Engine(0, frames=True, max_steps=5, max_in_flight=2)
+    eng = batch.Engine(0, frames=True, ring_slots=5, max_in_flight=2)
     stream = torch.cuda.Stream(device=dev)
     empty = batch.PacketBatch(data=torch.zeros(16, dtype=torch.uint8, device=dev),
                               off=torch.zeros(0, dtype=torch.int64, device=dev),
                               length=torch.zeros(0, dtype=torch.int32, device=dev), bytes_len=0, max_len=0)
+    empty_st = torch.empty(1, dtype=torch.uint8, device=dev)
     outs = []
     for run in range(3):
-        o = [torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev) for _ in range(4)]
+        o = [torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev) for _ in range(20)]
         torch.cuda.synchronize()
         eng.start(stream)
-        ids = [eng.submit([(b, o[0], None)]), eng.submit([(empty, None, torch.empty(1, dtype=torch.uint8,
-                                                                                       device=dev))]),
-               eng.submit([(b, o[1], None), (b, o[2], None)]), eng.submit([(b, o[3], None)])]
-        eng.submit([(empty, None, torch.empty(1, dtype=torch.uint8, device=dev))])
-        with pytest.raises(native.SccsumError) as e:  # the 6th step of a 5-step run
-            eng.submit([(b, o[0], None)])
-        assert e.value.code == native.SCCSUM_EBUSY
+        ids = []
+        for k in range(10):
+            ids.append(eng.submit([(b, o[2 * k], None)]))
+            ids.append(eng.submit([(empty, None, empty_st)]))
+            ids.append(eng.submit([(b, o[2 * k + 1], None), (empty, None, empty_st)]))
+        assert ids == list(range(30))
         for i in ids:
             eng.wait(i)
-        with pytest.raises(native.SccsumError):
+        with pytest.raises(native.SccsumError) as e:
             eng.wait(99)
-        eng.stop()
+        assert e.value.code == native.SCCSUM_EINVAL
+        eng.finish()
         stream.synchronize()
         outs.extend(o)
     for o in outs:
@@ -152,11 +156,11 @@ def test_engine_runs_restart_and_limits(dev):
 
 def test_engine_grid_left_idle_leaves_on_its_own(dev):
     """A run started and never given a step nor a stop: its grid gives up after
-    its idle limit (1 s), the stream drains, and the run reports SCCSUM_EIDLE;
-    a new run then works."""
+    its idle limit (1 s), the stream drains, and a submit reports SCCSUM_EIDLE
+    (stop does not: no published step was lost); a new run then works."""
     rng = np.random.default_rng(0xE4)
     b, want, _ = _frames_step(rng, dev, 0)
-    eng = batch.Engine(0, frames=True, max_steps=4, max_in_flight=1)
+    eng = batch.Engine(0, frames=True, ring_slots=4, max_in_flight=1)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize()
     eng.start(stream)
@@ -164,8 +168,7 @@ def test_engine_grid_left_idle_leaves_on_its_own(dev):
     with pytest.raises(native.SccsumError) as e:
         eng.submit([(b, torch.empty(2 * b.n, dtype=torch.int16, device=dev), None)])
     assert e.value.code == native.SCCSUM_EIDLE
-    with pytest.raises(native.SccsumError):
-        eng.stop()
+    eng.stop()  # the give-up left no published step undone: nothing lost, 0
     out = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
     eng.start(stream)
     eng.wait(eng.submit([(b, out, None)]))
@@ -194,7 +197,7 @@ def test_engine_large_steps_property(dev):
     outs = [torch.empty(2 * n, dtype=torch.int16, device=dev) for _ in range(R)]
     sts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(R)]
     torch.cuda.synchronize()
-    eng = batch.Engine(0, frames=True, max_steps=64, max_in_flight=2)
+    eng = batch.Engine(0, frames=True, ring_slots=64, max_in_flight=2)
     stream = torch.cuda.Stream(device=dev)
     preps = [eng.prepare([(txs[r], outs[r], None), (rxs[r], None, sts[r])]) for r in range(R)]
     eng.start(stream)
@@ -218,7 +221,7 @@ def test_engine_results_readable_while_the_grid_runs(dev):
         b, want, want_st = _frames_step(rng, dev, 0)
         items.append((b, torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev), want))
     torch.cuda.synchronize()
-    eng = batch.Engine(0, frames=True, max_steps=8, max_in_flight=2)
+    eng = batch.Engine(0, frames=True, ring_slots=8, max_in_flight=2)
     stream = torch.cuda.Stream(device=dev)
     side = torch.cuda.Stream(device=dev)
     eng.start(stream)
@@ -282,7 +285,7 @@ def test_engine_fill_steps_match_oracle(dev, mode, fill_passes):
         out = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
         verifies.append((b, out, want))
     torch.cuda.synchronize()
-    eng = batch.Engine(0, frames=True, fill=True, max_steps=64, max_in_flight=4)
+    eng = batch.Engine(0, frames=True, fill=True, ring_slots=64, max_in_flight=4)
     stream = torch.cuda.Stream(device=dev)
     eng.start(stream)
     ids = []
@@ -327,7 +330,7 @@ def test_engine_fill_full_scale(dev):
         f[:, 26:28] = 0x3C
     outs = [torch.empty(2 * n, dtype=torch.int16, device=dev) for _ in range(R)]
     torch.cuda.synchronize()
-    eng = batch.Engine(0, frames=True, fill=True, max_steps=64, max_in_flight=8)
+    eng = batch.Engine(0, frames=True, fill=True, ring_slots=64, max_in_flight=8)
     stream = torch.cuda.Stream(device=dev)
     preps = [eng.prepare([(bs[r], outs[r], None)], fill_mode=native.FILL_IP | native.FILL_L4) for r in range(R)]
     eng.start(stream)
@@ -358,8 +361,8 @@ def test_second_engine_on_the_device_is_refused(dev):
     o1 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
     o2 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
     torch.cuda.synchronize()
-    e1 = batch.Engine(0, frames=True, max_steps=8, max_in_flight=2)
-    e2 = batch.Engine(0, frames=True, max_steps=8, max_in_flight=2)
+    e1 = batch.Engine(0, frames=True, ring_slots=8, max_in_flight=2)
+    e2 = batch.Engine(0, frames=True, ring_slots=8, max_in_flight=2)
     s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
     e1.start(s1)
     with pytest.raises(native.SccsumError) as e:
@@ -392,7 +395,7 @@ def test_launch_from_another_thread_completes_after_stop(dev):
     o_thr = torch.full((2 * b2.n,), -1, dtype=torch.int16, device=dev)
     st_thr = torch.full((b2.n,), 0xEE, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    eng = batch.Engine(0, frames=True, max_steps=8, max_in_flight=2)
+    eng = batch.Engine(0, frames=True, ring_slots=8, max_in_flight=2)
     stream = torch.cuda.Stream(device=dev)
     eng.start(stream)
     eng.wait(eng.submit([(b, o_eng, None)]))
@@ -437,7 +440,7 @@ def test_engine_create_keeps_the_callers_device(dev):
     torch.cuda.set_device(0)
     native.check(lib.sccsum_init(0), "sccsum_init")
     before = torch.cuda.current_device()
-    eng = batch.Engine(target, frames=True, max_steps=4, max_in_flight=1)
+    eng = batch.Engine(target, frames=True, ring_slots=4, max_in_flight=1)
     assert torch.cuda.current_device() == before == 0
     eng.close()
 
@@ -459,7 +462,7 @@ def test_engine_low_rate_steps_all_complete(dev):
     torch.cuda.synchronize()
     native.check(lib.sccsum_set_engine_idle_ms(300), "idle")
     try:
-        eng = batch.Engine(0, frames=True, max_steps=steps + 1, max_in_flight=4)
+        eng = batch.Engine(0, frames=True, ring_slots=steps + 1, max_in_flight=4)
         stream = torch.cuda.Stream(device=dev)
         eng.start(stream)
         t0 = time.perf_counter()
@@ -473,7 +476,7 @@ def test_engine_low_rate_steps_all_complete(dev):
         eng.stop()  # raises SccsumError(EIDLE) if any wave had given up
         stream.synchronize()
     finally:
-        lib.sccsum_set_engine_idle_ms(1000)
+        lib.sccsum_set_engine_idle_ms(0)
     for o in outs:
         assert np.array_equal(batch.as_u16(o).reshape(-1, 2), want)
     eng.close()
@@ -502,7 +505,7 @@ def test_engine_reads_bytes_rewritten_during_the_run(dev):
     outs = [torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev) for _ in contents]
     sts = [torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev) for _ in contents]
     torch.cuda.synchronize()
-    eng = batch.Engine(0, frames=True, max_steps=32, max_in_flight=2)
+    eng = batch.Engine(0, frames=True, ring_slots=32, max_in_flight=2)
     stream, side = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
     eng.start(stream)
     for rep in range(2):
@@ -520,8 +523,8 @@ def test_engine_reads_bytes_rewritten_during_the_run(dev):
 
 
 def test_engine_fill_limits_and_empty_batches(dev):
-    """A fill takes two of the run's steps, both or neither: with one step
-    left, submit_fill is SCCSUM_EBUSY and publishes nothing; a fill step may
+    """A fill takes two consecutive steps of the run, published together once
+    the in-flight limit has room for both; a fill step may
     hold empty batches beside real ones; a fill on an engine created without
     SCCSUM_ENGINE_FILL, or without out2, or in a header-only mode, is refused
     (SCCSUM_EINVAL); the step a fill returns is its store step, done once
@@ -552,7 +555,7 @@ def _fill_limits_two_steps(dev, rng, buf, off, length, m, want):
     st = torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     lib = native.load()
-    plain = batch.Engine(0, frames=True, max_steps=4, max_in_flight=2)
+    plain = batch.Engine(0, frames=True, ring_slots=4, max_in_flight=2)
     arr = (native.Batch * 1)()
     arr[0] = native.Batch(b.data.data_ptr(), b.bytes_len, b.off.data_ptr(), b.length.data_ptr(), None,
                           out2.data_ptr(), None, b.n)
@@ -564,7 +567,7 @@ def _fill_limits_two_steps(dev, rng, buf, off, length, m, want):
     plain.stop()
     stream.synchronize()
     plain.close()
-    eng = batch.Engine(0, frames=True, fill=True, max_steps=3, max_in_flight=2)
+    eng = batch.Engine(0, frames=True, fill=True, ring_slots=2, max_in_flight=2)
     eng.start(stream)
     no_out = (native.Batch * 1)()
     no_out[0] = native.Batch(b.data.data_ptr(), b.bytes_len, b.off.data_ptr(), b.length.data_ptr(), None, None,
@@ -576,10 +579,12 @@ def _fill_limits_two_steps(dev, rng, buf, off, length, m, want):
                                          ctypes.byref(step)) == native.SCCSUM_EINVAL  # header-only mode
     s1 = eng.submit_fill([(empty, torch.empty(2, dtype=torch.int16, device=dev), None), (b, out2, st)], m)
     assert s1 == 1  # the store step (the generate step is step 0)
-    with pytest.raises(native.SccsumError) as e:  # one step left: both or neither
-        eng.submit_fill([(b, out2, st)], m)
-    assert e.value.code == native.SCCSUM_EBUSY
-    eng.wait(s1)
+    # the same fill again (a fill is idempotent): its two steps come after the first fill's, once the
+    # in-flight limit (2) has the first fill done — so it never writes the frames under the first one
+    s3 = eng.submit_fill([(b, out2, st)], m)
+    assert s3 == 3
+    eng.wait(s1, timeout_s=0)  # done: the second fill's submit waited for it
+    eng.wait(s3)
     eng.stop()
     stream.synchronize()
     got = b.data.cpu().numpy()[: b.bytes_len]
@@ -616,7 +621,7 @@ def test_engine_fill_stress_small_steps(dev, in_flight, fill_passes):
         vout = torch.full((2 * vb.n,), -1, dtype=torch.int16, device=dev)
         verifies.append((vb, vout, oracle.batch_ipv4(buf, off, length)[0]))
     torch.cuda.synchronize()
-    eng = batch.Engine(0, frames=True, fill=True, max_steps=512, max_in_flight=in_flight)
+    eng = batch.Engine(0, frames=True, fill=True, ring_slots=512, max_in_flight=in_flight)
     stream = torch.cuda.Stream(device=dev)
     eng.start(stream)
     last = 0
@@ -664,7 +669,7 @@ def test_engine_barrier_period(dev, sync_every):
     torch.cuda.synchronize()
     native.check(lib.sccsum_set_engine_sync_every(sync_every), "sync_every")
     try:
-        eng = batch.Engine(0, frames=True, fill=True, max_steps=128, max_in_flight=16)
+        eng = batch.Engine(0, frames=True, fill=True, ring_slots=128, max_in_flight=16)
         stream = torch.cuda.Stream(device=dev)
         eng.start(stream)
         last = 0
@@ -711,7 +716,7 @@ def test_engine_barrier_behind_empty_steps(dev):
         steps.append((b, st, want_st))
     torch.cuda.synchronize()
     native.check(lib.sccsum_set_engine_sync_every(2), "sync_every")
-    eng = batch.Engine(0, frames=True, max_steps=64, max_in_flight=8)
+    eng = batch.Engine(0, frames=True, ring_slots=64, max_in_flight=8)
     try:
         stream = torch.cuda.Stream(device=dev)
         eng.start(stream)
@@ -756,7 +761,7 @@ def test_engine_pacing_counts_every_older_step(dev):
     tiny = batch.PacketBatch.from_host(buf, off, length, device=dev)
     tiny_st = torch.empty(tiny.n, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    eng = batch.Engine(0, frames=True, fill=True, max_steps=64, max_in_flight=2)
+    eng = batch.Engine(0, frames=True, fill=True, ring_slots=64, max_in_flight=2)
     stream = torch.cuda.Stream(device=dev)
     late = []
     for rep in range(3):
@@ -797,7 +802,7 @@ def test_engine_slices_of_one_buffer_with_max_len(dev):
     out = torch.full((2 * n_all,), -1, dtype=torch.int16, device=dev)
     st = torch.full((n_all,), 0xEE, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    eng = batch.Engine(0, frames=True, max_steps=256, max_in_flight=8)
+    eng = batch.Engine(0, frames=True, ring_slots=256, max_in_flight=8)
     stream = torch.cuda.Stream(device=dev)
     sizes = [1024, 4096, 16384, 1, 33]
     for max_len in (L, 0):
@@ -825,52 +830,114 @@ def test_engine_slices_of_one_buffer_with_max_len(dev):
     eng.close()
 
 
-def test_engine_run_of_max_steps(dev):
-    """One run of the most steps a run takes (65 536): every step a batch of
-    1-3 frames (a tiny step: most waves claim past the published tiles and
-    wait), results into a rotating set of outputs; the 65 537th submit is
-    SCCSUM_EBUSY; the last outputs of every slot equal the oracle.  Covers the
-    step-indexed words at their limit (done words, descriptor ring, the 64
-    completion slots wrapping 1 024 times)."""
+@pytest.mark.parametrize("ring,in_flight,steps", [(1024, 32, 262144), (64, 64, 65536), (2, 2, 8192)])
+def test_engine_unbounded_run_on_a_small_ring(dev, ring, in_flight, steps):
+    """One run of many more steps than its descriptor ring has slots (VERDICT
+    r05 #3: 262 144 steps of 32 frames on a 1 024-slot ring, 256 laps; a
+    64-slot ring with the in-flight limit at the ring, 1 024 laps; a 2-slot
+    ring, every step waiting for the one two before it).  Each step is one
+    DPDK-sized burst of 32 frames (src/net/dpdk.cc:2190-2204) from a pool of
+    1 024 distinct bursts, its results into its own slice of one output
+    array: every step's every frame exact against the oracle.  Tiny steps put
+    most waves' claims far past the published tiles, so the walk from a
+    wave's cursor to its tile's step crosses slots the ring has reused."""
     import ctypes
 
     lib = native.load()
-    buf, off, lens, _ = synth.udp_ipv4_frames(3, 600, seed=41)
-    want, _ = oracle.batch_ipv4(buf, off, lens)
+    B, pool = 32, 1024
+    buf, off, lens, _ = synth.udp_ipv4_frames(B * pool, 600, seed=43)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
     b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
-    slots = 64
-    outs = torch.full((slots, 6), -1, dtype=torch.int16, device=dev)
+    out = torch.full((steps * B * 2,), -1, dtype=torch.int16, device=dev)
+    st = torch.full((steps * B,), 0xEE, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    max_steps = 65536
-    eng = batch.Engine(0, frames=True, max_steps=max_steps, max_in_flight=32)
+    eng = batch.Engine(0, frames=True, ring_slots=ring, max_in_flight=in_flight)
     stream = torch.cuda.Stream(device=dev)
-    eng.start(stream)
     arr = (native.Batch * 1)()
     step = ctypes.c_uint64()
-    for k in range(max_steps):
-        n = 1 + k % 3
-        arr[0] = native.Batch(b.data.data_ptr(), b.bytes_len, b.off.data_ptr(), b.length.data_ptr(), None,
-                              outs[k % slots].data_ptr(), None, n)
-        rc = lib.sccsum_engine_submit(eng._h, ctypes.cast(arr, ctypes.c_void_p), 1, 600, 10**10, ctypes.byref(step))
-        assert rc == native.SCCSUM_OK, (k, rc)
-    assert step.value == max_steps - 1
-    assert lib.sccsum_engine_submit(eng._h, ctypes.cast(arr, ctypes.c_void_p), 1, 600, 10**9,
-                                    ctypes.byref(step)) == native.SCCSUM_EBUSY
-    eng.wait(max_steps - 1)
-    eng.stop()
-    stream.synchronize()
-    got = batch.as_u16(outs).reshape(slots, 3, 2)
-    for s in range(slots):
-        n = 1 + (max_steps - slots + s) % 3  # the slot's last step's frame count
-        assert np.array_equal(got[s, :n], want[:n]), s
+    fn, h, ap = lib.sccsum_engine_submit, eng._h, ctypes.cast(arr, ctypes.c_void_p)
+    d0, o0, l0 = b.data.data_ptr(), b.off.data_ptr(), b.length.data_ptr()
+    out0, st0 = out.data_ptr(), st.data_ptr()
+    eng.start(stream)
+    try:
+        for k in range(steps):
+            q = k % pool
+            arr[0] = native.Batch(d0, b.bytes_len, o0 + 8 * B * q, l0 + 4 * B * q, None, out0 + 4 * B * k,
+                                  st0 + B * k, B)
+            rc = fn(h, ap, 1, 600, 10**10, ctypes.byref(step))
+            assert rc == native.SCCSUM_OK, (k, rc)
+        assert step.value == steps - 1
+        eng.wait(steps - 1)
+        for k in range(max(0, steps - ring), steps):  # the last lap's done words answer too
+            eng.wait(k, timeout_s=0)
+    finally:
+        eng.stop()
+        stream.synchronize()
     eng.close()
+    got = batch.as_u16(out).reshape(steps // pool, pool * B, 2)
+    gst = st.cpu().numpy().reshape(steps // pool, pool * B)
+    bad = np.nonzero(np.any(got != want[None], axis=(1, 2)) | np.any(gst != want_st[None], axis=1))[0]
+    assert bad.size == 0, f"laps of the burst pool with a wrong frame: {bad[:8].tolist()} of {steps // pool}"
+
+
+def test_engine_dependency_give_up_is_reported(dev):
+    """The dependency limit is a create parameter (sccsum_engine_opts.dep_ms,
+    VERDICT r05 #3).  A spans engine with a 1 ms limit and a barrier on every
+    step (sccsum_set_engine_sync_every(1)): step 0 is one 48 MiB span (one
+    wave sums a span past the fast path's 128 KiB exactly, tens of ms), so
+    step 1's waves give up waiting for it.  wait, stop and destroy each report
+    it (SCCSUM_EFAULT), step 0 itself still completes exact, and the device is
+    free for the next engine."""
+    lib = native.load()
+    rng = np.random.default_rng(0xF0)
+    L = 48 << 20
+    big_buf = rng.integers(0, 256, L, dtype=np.uint8)
+    big = batch.PacketBatch.from_host(big_buf, np.zeros(1, np.uint64), np.array([L], np.uint32), device=dev)
+    big_want = oracle.batch_spans(big_buf, np.zeros(1, np.uint64), np.array([L], np.uint32))
+    small_buf = rng.integers(0, 256, 64 * 100, dtype=np.uint8)
+    small = batch.PacketBatch.from_host(small_buf, np.arange(64, dtype=np.uint64) * 100, np.full(64, 100, np.uint32),
+                                        device=dev)
+    o_big = torch.full((1,), -1, dtype=torch.int16, device=dev)
+    o_small = torch.full((64,), -1, dtype=torch.int16, device=dev)
+    torch.cuda.synchronize()
+    native.check(lib.sccsum_set_engine_sync_every(1), "a barrier on every step")
+    stream = torch.cuda.Stream(device=dev)
+    try:
+        eng = batch.Engine(0, frames=False, ring_slots=8, max_in_flight=4, dep_ms=1)
+        eng.start(stream)
+        s0 = eng.submit([(big, o_big, None)])
+        s1 = eng.submit([(small, o_small, None)])
+        with pytest.raises(native.SccsumError) as e:
+            eng.wait(s1)
+        assert e.value.code == native.SCCSUM_EFAULT
+        with pytest.raises(native.SccsumError) as e:
+            eng.stop()
+        assert e.value.code == native.SCCSUM_EFAULT
+        stream.synchronize()
+        with pytest.raises(native.SccsumError) as e:
+            eng.close()
+        assert e.value.code == native.SCCSUM_EFAULT
+        assert s0 == 0
+    finally:
+        lib.sccsum_set_engine_sync_every(-1)
+    assert np.array_equal(batch.as_u16(o_big), big_want)  # the step that was waited on finished
+    # the device is free: a new engine runs, exact
+    b, want, _ = _frames_step(rng, dev, 0)
+    o = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+    eng2 = batch.Engine(0, frames=True, ring_slots=4, max_in_flight=2)
+    eng2.start(stream)
+    eng2.wait(eng2.submit([(b, o, None)]))
+    eng2.finish()
+    stream.synchronize()
+    eng2.close()
+    assert np.array_equal(batch.as_u16(o).reshape(-1, 2), want)
 
 
 def test_engine_fill_single_pass_takes_one_step(dev):
     """A fill of at most sccsum_set_fill_single_max frames (524 288 by default)
     is ONE engine step whose tiles store the fields themselves: it returns
-    that step, takes one of the run's steps (with one step left it still
-    fits), and leaves the frames exactly as the oracle's writers do."""
+    that step (the one after the verify step before it), and leaves the
+    frames exactly as the oracle's writers do."""
     from test_gpu_parity import _tx_frames
 
     rng = np.random.default_rng(0xEC)
@@ -883,13 +950,13 @@ def test_engine_fill_single_pass_takes_one_step(dev):
     vb, vwant, _ = _frames_step(rng, dev, 1)
     vout = torch.full((2 * vb.n,), -1, dtype=torch.int16, device=dev)
     torch.cuda.synchronize()
-    eng = batch.Engine(0, frames=True, fill=True, max_steps=2, max_in_flight=2)
+    eng = batch.Engine(0, frames=True, fill=True, ring_slots=2, max_in_flight=2)
     stream = torch.cuda.Stream(device=dev)
     eng.start(stream)
     try:
         assert eng.submit([(vb, vout, None)]) == 0
         s1 = eng.submit_fill([(b, out2, st)], m)
-        assert s1 == 1  # one step: the run's last
+        assert s1 == 1  # one step
         eng.wait(s1)
     finally:
         eng.stop()
