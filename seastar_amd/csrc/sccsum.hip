@@ -1183,10 +1183,10 @@ constexpr uint32_t kEngineSlotWords = 64;  // 512-byte descriptors
 constexpr uint32_t kEngineCountSlots = 64;  // completion counters: steps in flight at most
 constexpr uint32_t kEngineMaxRing = 1u << 16;  // descriptor ring slots (2 x 32 MiB of descriptor rings at most)
 constexpr uint32_t kEngineDefaultRing = 1024;
-// descriptors the polling wave copies per round of its store phases (4 or 8
-// held in registers across the phases pushed the fill engine kernel into
-// scratch: 224 B of spills, where 2 leave it at 214 VGPRs and none)
-constexpr uint32_t kPollGroup = 2;
+// descriptors the polling wave copies per round of its store phases (only a
+// waiting wave polls, holding no tile: with the poll inside the tile loop, 4
+// or 8 pushed the fill engine kernel into 224 B of scratch)
+constexpr uint32_t kPollGroup = 8;
 constexpr uint64_t kSlotInvalid = ~0ull;  // a slot's step word while the poller rewrites it
 // descriptor words
 constexpr uint32_t kEdFirst = 0;   // the step's first tile in the run
@@ -1388,13 +1388,19 @@ struct EngineSrc {
             __hip_atomic_store(E.mirror + kMpToken, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    // Tile v is published, as far as the device mirror says (mid-tile: no
+    // host poll here, so the poller's registers never meet a tile's).
     __device__ bool published(uint64_t v) {
         if (v < pub) return true;
 #ifdef SCCSUM_AB_TIMELINE
         ++ab[2];
 #endif
         pub = mload(kMpTiles);
-        if (v < pub) return true;
+        return v < pub;
+    }
+    // ... or after a poll of the host (a waiting wave: it holds no tile)
+    __device__ bool published_polled(uint64_t v) {
+        if (published(v)) return true;
         poll();
         pub = mload(kMpTiles);
         return v < pub;
@@ -1427,7 +1433,7 @@ struct EngineSrc {
 #endif
         for (;;) {
             const uint64_t stop = mload(kMpStop);  // read before the tiles (the poller raises it after them)
-            const bool pubd = published(v);
+            const bool pubd = published_polled(v);
             if (pubd) {
                 // v's step waits on an older step: that always completes (its
                 // tiles come before v in every group's claim order); the limit

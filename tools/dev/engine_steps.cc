@@ -12,6 +12,12 @@
 // (SCCSUM_FILL_IP | SCCSUM_FILL_L4: the tx half, ip.cc:266-278, udp.cc:184-195):
 //   launch  sccsum_ipv4_fill per step (a generate and a store kernel)
 //   engine  a fill engine, sccsum_engine_submit_fill per step (two engine steps)
+// With the argument `producers` (and optionally a thread count, default 8),
+// the engine's steps come from that many host threads at once — the shards of
+// one GPU feeding its one engine (include/sccsum.h "Producers") — each
+// submitting its share of the k steps; the clock runs from a common start to
+// the last thread's last step done.  ENGINE_STEPS_RING sets the engine's ring
+// slots (default 1 024, the library's default).
 // Prints one JSON line per size.  Build (tools/gpu_session.sh bin: step):
 //   hipcc -O2 -std=c++17 -I include tools/dev/engine_steps.cc -L seastar_amd/lib -lsccsum \
 //         -Wl,-rpath,$PWD/seastar_amd/lib -o tools/dev/engine_steps
@@ -19,8 +25,10 @@
 #include <sccsum.h>
 #include <sccsum_diag.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -46,8 +54,56 @@ static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// k steps of B frames from `threads` producer threads into one running engine
+// e: µs per step (aggregate), or a negative value on an error.
+static double producers_run(sccsum_engine* e, void* s, int threads, uint64_t k, uint32_t B, uint64_t slices,
+                            void* d_bytes, uint64_t bytes_len, const uint64_t* d_off, const uint32_t* d_len,
+                            uint8_t* d_st) {
+    if (sccsum_engine_start(e, s) != SCCSUM_OK) return -1;
+    std::atomic<int> ready{0}, bad{0};
+    std::atomic<bool> go{false};
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t) {
+        ts.emplace_back([&, t] {
+            ++ready;
+            while (!go.load()) {
+            }
+            uint64_t step = 0;
+            bool any = false;
+            for (uint64_t j = t; j < k; j += threads) {
+                const uint64_t q = j % slices;
+                sccsum_batch b{};
+                b.d_bytes = d_bytes;
+                b.bytes_len = bytes_len;
+                b.d_off = d_off + q * B;
+                b.d_len = d_len + q * B;
+                b.d_status = d_st + q * B;
+                b.n = B;
+                if (sccsum_engine_submit(e, &b, 1, 1500, 10'000'000'000ull, &step) != SCCSUM_OK) {
+                    ++bad;
+                    return;
+                }
+                any = true;
+            }
+            if (any && sccsum_engine_wait(e, step, 10'000'000'000ull) != SCCSUM_OK) ++bad;
+        });
+    }
+    while (ready.load() < threads) {
+    }
+    const double t0 = now_s();
+    go = true;
+    for (auto& th : ts) th.join();
+    const double dt = now_s() - t0;
+    if (sccsum_engine_stop(e) != SCCSUM_OK) ++bad;
+    if (hipStreamSynchronize(static_cast<hipStream_t>(s)) != hipSuccess) ++bad;
+    return bad.load() ? -1.0 : dt / k * 1e6;
+}
+
 int main(int argc, char** argv) {
     const bool fill = argc > 1 && std::strcmp(argv[1], "fill") == 0;
+    const bool producers = argc > 1 && std::strcmp(argv[1], "producers") == 0;
+    const int nprod = producers && argc > 2 ? std::atoi(argv[2]) : 8;
+    const uint32_t ring = std::getenv("ENGINE_STEPS_RING") ? std::atoi(std::getenv("ENGINE_STEPS_RING")) : 1024;
     const uint32_t mode = SCCSUM_FILL_IP | SCCSUM_FILL_L4;
     const uint64_t n_all = 1 << 18;  // 262 144 frames, 393 MB
     const uint32_t L = 1500;
@@ -86,6 +142,29 @@ int main(int argc, char** argv) {
     if (const char* dy = std::getenv("ENGINE_STEPS_DYNAMIC")) SC_OK(sccsum_set_dynamic_tiles(std::atoi(dy)));  // A/B
     if (const char* va = std::getenv("ENGINE_STEPS_VARIANT")) SC_OK(sccsum_set_kernel_variant(std::atoi(va)));  // A/B
     const uint32_t sizes[] = {32, 128, 1024, 16384, 65536, 262144};
+    if (producers) {
+        for (uint32_t B : sizes) {
+            if (B > 1024) continue;
+            const uint64_t slices = n_all / B;
+            const uint64_t k = B <= 128 ? 40000 : 10000;
+            sccsum_engine* e = nullptr;
+            SC_OK(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, ring, 64, &e));
+            (void)producers_run(e, s, 1, 256, B, slices, d_bytes, host.size(), d_off, d_len, d_st);  // warm
+            const double one = producers_run(e, s, 1, k, B, slices, d_bytes, host.size(), d_off, d_len, d_st);
+            const double many = producers_run(e, s, nprod, k, B, slices, d_bytes, host.size(), d_off, d_len, d_st);
+            SC_OK(sccsum_engine_destroy(e));
+            if (one < 0 || many < 0) {
+                std::printf("producers: an engine call failed\n");
+                return 4;
+            }
+            std::printf("{\"form\": \"producers\", \"packets_per_step\": %u, \"steps\": %llu, \"ring\": %u, "
+                        "\"one_thread_us_per_step\": %.2f, \"threads\": %d, \"threads_us_per_step\": %.2f, "
+                        "\"threads_GiBps\": %.1f}\n",
+                        B, (unsigned long long)k, ring, one, nprod, many, double(B) * L / (many * 1e-6) / (1u << 30));
+            std::fflush(stdout);
+        }
+        return 0;
+    }
     for (uint32_t B : sizes) {
         if (!fill && B > 16384) continue;
         const uint64_t slices = n_all / B;
@@ -118,8 +197,7 @@ int main(int argc, char** argv) {
         const double launch_s = now_s() - t0;
         // engine
         sccsum_engine* e = nullptr;
-        SC_OK(sccsum_engine_create(0, SCCSUM_PIPE_IPV4 | (fill ? SCCSUM_ENGINE_FILL : 0),
-                                   static_cast<uint32_t>(2 * (k + 64)), 64, &e));
+        SC_OK(sccsum_engine_create(0, SCCSUM_PIPE_IPV4 | (fill ? SCCSUM_ENGINE_FILL : 0), ring, 64, &e));
         double engine_s = 0;
         for (int run = 0; run < 2; ++run) {  // the first run warms up
             const uint64_t kk = run ? k : 64;
@@ -145,9 +223,9 @@ int main(int argc, char** argv) {
         const double bytes = double(k) * B * L;
         std::printf("{\"form\": \"%s\", \"packets_per_step\": %u, \"steps\": %llu, \"launch_us_per_step\": %.2f, "
                     "\"launch_GiBps\": %.1f, \"engine_us_per_step\": %.2f, \"engine_GiBps\": %.1f, "
-                    "\"engine_over_launch\": %.2f}\n",
+                    "\"engine_over_launch\": %.2f, \"ring\": %u}\n",
                     fill ? "fill" : "verify", B, (unsigned long long)k, launch_s / k * 1e6, bytes / launch_s / (1u << 30), engine_s / k * 1e6,
-                    bytes / engine_s / (1u << 30), launch_s / engine_s);
+                    bytes / engine_s / (1u << 30), launch_s / engine_s, ring);
         std::fflush(stdout);
     }
     return 0;
