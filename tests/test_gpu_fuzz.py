@@ -423,7 +423,10 @@ def test_fuzz_engine_steps(dev, case):
             items.append((b, out2, st))
             wants.append(oracle.batch_ipv4(buf, off, L))
         plan.append(("sum", (items, wants)))
-    eng = batch.Engine(0, frames=True, max_steps=256, max_in_flight=int(rng.choice([2, 8, 64])), fill=fill)
+    # a random descriptor ring, often far smaller than the run (slots reused many times, round 6)
+    ring = int(np.random.default_rng(7000 + case).choice([2, 4, 8, 256]))
+    knobs["ring"] = ring
+    eng = batch.Engine(0, frames=True, ring_slots=ring, max_in_flight=int(rng.choice([2, 8, 64])), fill=fill)
     stream = torch.cuda.Stream()
     torch.cuda.synchronize()
     checks = []
@@ -701,7 +704,9 @@ def test_fuzz_engine_spans(dev, case):
             items.append((b, out, st, torch.from_numpy(seeds.view(np.int32)).to(dev)))
             wants.append((w, np.where(bad, native.ST_RANGE, (w == 0).astype(np.uint8))))
         plan.append((items, wants))
-    eng = batch.Engine(0, frames=False, max_steps=64, max_in_flight=int(rng.choice([2, 8, 64])))
+    ring = int(np.random.default_rng(7500 + case).choice([2, 4, 64]))
+    knobs["ring"] = ring
+    eng = batch.Engine(0, frames=False, ring_slots=ring, max_in_flight=int(rng.choice([2, 8, 64])))
     stream = torch.cuda.Stream()
     torch.cuda.synchronize()
     eng.start(stream)
