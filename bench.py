@@ -421,6 +421,30 @@ def pmc_traffic(path: str | None, config: str, kernel: str):
     return None, None, None
 
 
+def fill_floor(alg_bytes: float, fill_s: float):
+    """The in-place fill's measured two-pass floor: the
+    newest committed profiles/rNN_fill_floor.json, from tools/dev/store_probe.hip
+    run on a GPU box — a plain nt read of 1 M x 1500 B frames followed by the
+    cheapest field-writing pass measured (the aligned 64-byte line read and
+    rewritten, `rd;st64rw`), and the register-stash form beside it.  A fill
+    cannot beat a read of every byte plus a pass that writes the fields
+    (DESIGN.md §5.6), so frac against this floor, not only against 8 TB/s, says
+    how much of the fill's gap is the kernel's.  None when no file exists."""
+    for p in reversed(sorted(glob.glob(os.path.join(REPO, "profiles", "*fill_floor.json")))):
+        try:
+            d = json.load(open(p))
+            us = float(d["rd_st64rw_us"])
+        except (OSError, ValueError, KeyError):
+            continue
+        return {"us_per_fill": us, "frac": round(alg_bytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+                "fill_over_floor": round(fill_s * 1e6 / us, 4),
+                "form": "plain nt read of the frames, then a pass rewriting each frame's aligned 64-byte head line "
+                        "(tools/dev/store_probe.hip rd;st64rw: the cheapest two-pass form measured)",
+                "register_stash_us": d.get("rdbar_lineR_us"), "read_only_us": d.get("rd_us"),
+                "source": os.path.relpath(p, REPO), "box": d.get("box")}
+    return None
+
+
 class Launches:
     """Counts this process's launches per kernel, so a line can name which
     dispatches were timed (trace_select)."""
@@ -1201,8 +1225,10 @@ def run_fill(args, world, rank, dev):
                       kern + (" (sccsum_engine_submit_fill: generate + store steps; one launch = the timed run)"
                               if engine else " + fill_store_kernel (sccsum_ipv4_fill: generate pass, "
                                              "then the field-store pass)"), sel, args,
-                      None if engine else {"trace_select_extra": [{"kernel": "fill_store_kernel",
-                                                                   "skip": sel["skip"], "count": sel["count"]}]}),
+                      dict({"floor": fill_floor(alg, launch_s)},
+                           **({} if engine else {"trace_select_extra": [{"kernel": "fill_store_kernel",
+                                                                         "skip": sel["skip"],
+                                                                         "count": sel["count"]}]}))),
              extra={"per_rank": ranks})
 
 
