@@ -63,7 +63,7 @@ def sparse_kernel(args, ipv4: bool, max_len: int) -> str:
     as rocprofv3 names it: the row kernel, V units per lane from max_len."""
     units = (max_len + 30) // 16
     v = 2 if units <= 32 else 4 if units <= 64 else 6 if units <= 96 else 8
-    return f"csum_row_kernel<{v}, {str(ipv4).lower()}>"
+    return f"csum_row_kernel<{v}, {str(ipv4).lower()}, false, false>"  # (MQ, FILL: one batch, no fill)
 
 
 def parse():
@@ -1083,12 +1083,12 @@ def run_frags(args, world, rank, dev):
                                    off=torch.arange(k, device=dev, dtype=torch.int64) * pkt,
                                    length=torch.full((k,), pkt, dtype=torch.int32, device=dev),
                                    bytes_len=k * pkt, max_len=pkt)
-        ref = batch.spans(contig, seeds=seeds[:k])
+        ref = batch.spans(contig, seeds=seeds[:k])  # (a small launch: the same row-kernel form, counted below)
         torch.cuda.synchronize()
         assert torch.equal(got[:k], ref), "fragment lists differ from the contiguous packets"
         want.append(got.clone())
     kern = sparse_kernel(args, False, 2048)  # the raw pass over the fragments (a sparse layout)
-    LAUNCHES.add(kern, R)
+    LAUNCHES.add(kern, 2 * R)  # + the contiguous check launches (<= 65 536 packets: the row kernel, V 8 too)
     stream = torch.cuda.current_stream()
     pre = [batch.prepare_call("sccsum_fragments", pools[r], n * nf * slot, frag_off, frag_len, n * nf, first, seeds,
                               out, None, n, 2048, ws) for r in range(R)]

@@ -464,8 +464,12 @@ class Engine:
         opts = native.EngineOpts(int(ring), int(max_in_flight), int(idle_ms), int(dep_ms))
         if ring <= 0 or max_in_flight <= 0:  # (0 would mean "the default" to the C-ABI)
             raise ValueError("ring_slots and max_in_flight must be >= 1")
-        native.check(self._lib.sccsum_engine_create_opts(int(device), mode, ctypes.byref(opts), ctypes.byref(h)),
-                     "sccsum_engine_create_opts")
+        if hasattr(self._lib, "sccsum_engine_create_opts"):
+            native.check(self._lib.sccsum_engine_create_opts(int(device), mode, ctypes.byref(opts), ctypes.byref(h)),
+                         "sccsum_engine_create_opts")
+        else:  # an ABI 3 build under A/B (SCCSUM_LIB + SCCSUM_ABI_ANY): its runs end at ring_slots steps
+            native.check(self._lib.sccsum_engine_create(int(device), mode, int(ring), int(max_in_flight),
+                                                         ctypes.byref(h)), "sccsum_engine_create")
         self._h = h
         self.frames = frames
         self.fill = fill

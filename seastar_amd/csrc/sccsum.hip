@@ -1186,7 +1186,17 @@ constexpr uint32_t kEngineDefaultRing = 1024;
 // descriptors the polling wave copies per round of its store phases (only a
 // waiting wave polls, holding no tile: with the poll inside the tile loop, 4
 // or 8 pushed the fill engine kernel into 224 B of scratch)
+#ifdef SCCSUM_AB_POLL_GROUP
+constexpr uint32_t kPollGroup = SCCSUM_AB_POLL_GROUP;  // A/B only
+#else
 constexpr uint32_t kPollGroup = 8;
+#endif
+// the engine's per-tile checks: their slow paths placed out of the tile loop
+#ifdef SCCSUM_AB_NO_EXPECT  // A/B only
+#define SCCSUM_HOT(x) (x)
+#else
+#define SCCSUM_HOT(x) __builtin_expect(!!(x), 1)
+#endif
 constexpr uint64_t kSlotInvalid = ~0ull;  // a slot's step word while the poller rewrites it
 // descriptor words
 constexpr uint32_t kEdFirst = 0;   // the step's first tile in the run
@@ -1243,6 +1253,86 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t k) {
     return static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(x), k))) |
            static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(x >> 32), k)))
                << 32;
+}
+
+// Probe step t's slot for tile v: 0 = v lies in t (w = its descriptor, lane
+// i word i), 1 = t lies before v's step, 2 = after it.  A slot that holds
+// another step (or is being rewritten) means t is done, and every step before
+// it (the host reuses a slot only then), while v's step is not (v is the
+// caller's, unprocessed): so t lies before.  The step word is read again
+// after the descriptor: equal both times, every word read belongs to t (the
+// poller marks the slot invalid before it writes any other word).
+__device__ __forceinline__ uint32_t engine_probe(const uint64_t* dring, uint64_t ring_mask, uint32_t lane, uint64_t t,
+                                                 uint64_t v, uint64_t& w) {
+    const uint64_t* const slot = dring + (t & ring_mask) * kEngineSlotWords;
+    w = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (rl64(w, kEdStep) != t) return 1u;
+    asm volatile("" ::: "memory");  // the second read issues after the first has returned
+    uint64_t again = 0;
+    if (lane == kEdStep) again = __hip_atomic_load(slot + kEdStep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (rl64(again, kEdStep) != t) return 1u;
+    const uint64_t f = rl64(w, kEdFirst);
+    if (v < f) return 2u;
+    return v < f + static_cast<uint32_t>(rl64(w, kEdTiles)) ? 0u : 1u;
+}
+
+// A fault ends the wave where it stands (reported first; the host sees
+// SCCSUM_EFAULT).  (Returning it up through ready() / wait_ready() cost the
+// kernel ~40 VGPRs of merged control flow in the tile loop.)
+#ifdef SCCSUM_AB_NO_ENDPGM  // A/B only (a fault then runs on with a wrong cursor)
+__device__ __forceinline__ void engine_fault(uint64_t* ctl, uint32_t lane, uint64_t code) {
+    if (lane == 0) __hip_atomic_store(ctl + kEcError, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#else
+[[noreturn]] __device__ __forceinline__ void engine_fault(uint64_t* ctl, uint32_t lane, uint64_t code) {
+    if (lane == 0) __hip_atomic_store(ctl + kEcError, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_endpgm();
+}
+#endif
+
+struct WalkHit {
+    uint64_t t, w;
+};
+// walk()'s search past the step after the cursor (below: the step probed
+// there, r0 its answer): galloping, bounded by the mirror's step count, then
+// bisection.  Out of line (a call, on a wave's rare long walk), and so are
+// both faults: an s_endpgm anywhere in the kernel body's walk ran cfg 3
+// 1.5-2 % slower on the same box, with or without the search inlined
+// (profiles/r06_walk_ab.log).
+__device__ __attribute__((noinline)) WalkHit engine_walk_far(const uint64_t* dring, uint64_t ring_mask,
+                                                             const uint64_t* mirror, uint64_t* ctl, uint64_t below,
+                                                             uint64_t v, uint32_t r0) {
+    const uint32_t lane = __lane_id();
+    if (r0 == 2u) engine_fault(ctl, lane, kErrWalk);  // v before the step after the cursor's: never
+    uint64_t above = 0;
+    if (lane == 0) above = __hip_atomic_load(mirror + kMpSteps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    above = rfl64(above);  // below < step(v) < above
+    bool bisect = false;
+    uint64_t d = 1;
+    for (;;) {
+        uint64_t t;
+        if (!bisect) {
+            t = below + d;
+            if (t >= above) {
+                bisect = true;
+                continue;
+            }
+        } else {
+            if (above <= below + 1) engine_fault(ctl, lane, kErrWalk);  // a published tile in no published step
+            t = below + (above - below) / 2;
+        }
+        uint64_t w = 0;
+        const uint32_t r = engine_probe(dring, ring_mask, lane, t, v, w);
+        if (r == 0u) return WalkHit{t, w};
+        if (r == 1u) {
+            below = t;
+            d <<= 1;
+        } else {
+            above = t;
+            bisect = true;
+        }
+    }
 }
 
 struct EngineSrc {
@@ -1391,7 +1481,7 @@ struct EngineSrc {
     // Tile v is published, as far as the device mirror says (mid-tile: no
     // host poll here, so the poller's registers never meet a tile's).
     __device__ bool published(uint64_t v) {
-        if (v < pub) return true;
+        if (SCCSUM_HOT(v < pub)) return true;
 #ifdef SCCSUM_AB_TIMELINE
         ++ab[2];
 #endif
@@ -1409,7 +1499,7 @@ struct EngineSrc {
     // depends on is done (device copy of the done words; each slot only rises)
     __device__ bool dep_ready(uint64_t v) {
         walk(v);
-        if (sdep == 0 || sdep <= dep_seen) return true;
+        if (SCCSUM_HOT(sdep == 0 || sdep <= dep_seen)) return true;
         const uint32_t slot = static_cast<uint32_t>((sdep - 1) % kEngineCountSlots);
         uint64_t d = 0;
         if (lane == 0) d = __hip_atomic_load(E.sdone + 8u * slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1471,28 +1561,12 @@ struct EngineSrc {
         const uint64_t v = claim(0);
         return wait_ready(v) ? v : end();
     }
-    // Probe step t (< the mirror's step count: copied) for tile v: 0 = v lies
-    // in t (w = its descriptor, lane i word i), 1 = t lies before v's step,
-    // 2 = after it.  A slot that holds another step (or is being rewritten)
-    // means t is done, and every step before it (the host reuses a slot only
-    // then), while v's step is not (v is this wave's, unprocessed): so t lies
-    // before.  The step word is read again after the descriptor: equal both
-    // times, every word read belongs to t (the poller marks the slot invalid
-    // before it writes any other word).
+    // (engine_probe(): step t copied, i.e. below the mirror's step count)
     __device__ uint32_t probe(uint64_t t, uint64_t v, uint64_t& w) {
 #ifdef SCCSUM_AB_TIMELINE
         ++ab[3];
 #endif
-        const uint64_t* const slot = E.dring + (t & E.ring_mask) * kEngineSlotWords;
-        w = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (rl64(w, kEdStep) != t) return 1u;
-        asm volatile("" ::: "memory");  // the second read issues after the first has returned
-        uint64_t again = 0;
-        if (lane == kEdStep) again = __hip_atomic_load(slot + kEdStep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (rl64(again, kEdStep) != t) return 1u;
-        const uint64_t f = rl64(w, kEdFirst);
-        if (v < f) return 2u;
-        return v < f + static_cast<uint32_t>(rl64(w, kEdTiles)) ? 0u : 1u;
+        return engine_probe(E.dring, E.ring_mask, lane, t, v, w);
     }
     __device__ void set_cursor(uint64_t t, uint64_t w) {
         step = t;
@@ -1502,20 +1576,21 @@ struct EngineSrc {
         skind = rl64(w, kEdKind);
         sdep = rl64(w, kEdDep);
     }
-    // A fault ends the wave where it stands (reported first; the host sees
-    // SCCSUM_EFAULT).  (Returning it up through ready() / wait_ready() cost
-    // the kernel ~40 VGPRs of merged control flow in the tile loop.)
-    __device__ bool fault(uint64_t code) {
-        if (lane == 0) __hip_atomic_store(E.ctl + kEcError, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_endpgm();
-    }
     // tile v (published) -> the cursor on its step.  Claims only rise, so v's
-    // step is the cursor's or a later one: the next step first (a wave's next
-    // tile is mostly there), then galloping from the cursor and a binary
-    // search, every probe on a slot the ring may have reused since (probe()).
+    // step is the cursor's or a later one: the step after the cursor's first
+    // (a wave's next tile is mostly there), else engine_walk_far(); every
+    // probe on a slot the ring may have reused since (engine_probe()).
     __device__ bool walk(uint64_t v) {
-        if (step != ~0ull && v < slast) return true;
+        if (SCCSUM_HOT(step != ~0ull && v < slast)) return true;
+#ifdef SCCSUM_AB_WALK_SEQ  // A/B only (a run shorter than its ring): round 5's walk, step by step
+        while (step == ~0ull || v >= slast) {
+            const uint64_t t = step + 1;
+            const uint64_t w = __hip_atomic_load(E.dring + (t & E.ring_mask) * kEngineSlotWords + lane, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            set_cursor(t, w);
+        }
+        return true;
+#endif
 #ifdef SCCSUM_AB_TIMELINE
         const uint64_t w0 = static_cast<uint64_t>(wall_clock64());
         struct Walked {
@@ -1524,45 +1599,19 @@ struct EngineSrc {
             __device__ ~Walked() { a[4] += static_cast<uint64_t>(wall_clock64()) - t0; }
         } walked{ab, w0};
 #endif
+        const uint64_t t = step + 1;  // (~0 + 1 = step 0)
         uint64_t w = 0;
-        uint64_t below = step + 1;  // (~0 + 1 = step 0)
-        uint32_t r = probe(below, v, w);
-        if (r == 0u) {
-            set_cursor(below, w);
-            return true;
+        const uint32_t r = probe(t, v, w);
+        if (SCCSUM_HOT(r == 0u)) {
+            set_cursor(t, w);
+        } else {
+            const WalkHit h = engine_walk_far(E.dring, E.ring_mask, E.mirror, E.ctl, t, v, r);
+            set_cursor(rfl64(h.t), h.w);
         }
-        if (r == 2u) return fault(kErrWalk);  // v before the step after the cursor's: never
-        uint64_t above = mload(kMpSteps);       // below < step(v) < above
-        for (uint64_t d = 1; below + d < above; d <<= 1) {
-            const uint64_t t = below + d;
-            r = probe(t, v, w);
-            if (r == 0u) {
-                set_cursor(t, w);
-                return true;
-            }
-            if (r == 2u) {
-                above = t;
-                break;
-            }
-            below = t;
-        }
-        while (above - below > 1) {
-            const uint64_t t = below + (above - below) / 2;
-            r = probe(t, v, w);
-            if (r == 0u) {
-                set_cursor(t, w);
-                return true;
-            }
-            if (r == 1u) {
-                below = t;
-            } else {
-                above = t;
-            }
-        }
-        return fault(kErrWalk);  // a published tile in no published step: never
+        return true;
     }
+    // (v passed ready() / wait_ready(): the cursor is on its step)
     __device__ Ref ref(uint64_t v) {
-        walk(v);
         Ref r;
         r.kind = static_cast<uint32_t>(skind);
         const uint64_t t_in = v - sfirst;

@@ -41,6 +41,7 @@ std::mutex g_print;
 unsigned long long g_devices_used = 0;  // under g_print
 std::atomic<int> g_cross_checked{0};    // launches refused on another device's stream
 long g_engine_steps = 0;                // under g_print: steps the engine producers checked
+std::vector<sccsum_burst*> g_queues;    // under g_print: the shards' drained burst queues, destroyed by main
 
 void fail(int shard, const char* what, long i) {
     if (g_bad.fetch_add(1) < 20) {
@@ -282,7 +283,13 @@ void shard_main(int shard, int rounds) {
             if (i % 32 == 31) ok(sccsum_burst_poll(q, nullptr), shard, "poll");
         }
         ok(sccsum_burst_drain(q), shard, "drain");
-        ok(sccsum_burst_destroy(q), shard, "burst destroy");
+        // destroyed by main once every shard has joined: a queue's pinned
+        // staging freed now could be handed to another shard's queue while it
+        // runs, a reuse ThreadSanitizer cannot see through the ROCm allocator
+        {
+            std::lock_guard<std::mutex> l(g_print);
+            g_queues.push_back(q);
+        }
         check2(sink.out, wantA, "burst");
         if (sink.st != wstA) fail(shard, "burst status", 0);
     }
@@ -484,6 +491,7 @@ int main(int argc, char** argv) {
     std::vector<std::thread> ts;
     for (int t = 0; t < threads; ++t) ts.emplace_back(shard_main, t, rounds);
     for (auto& t : ts) t.join();
+    for (sccsum_burst* q : g_queues) ok(sccsum_burst_destroy(q), -1, "burst destroy");
     if (g_bad.load()) {
         std::printf("shards_gpu: FAILED (%d)\n", g_bad.load());
         return 1;

@@ -7,6 +7,9 @@ rx, n frames each) this prints, per step size, the step time, the host's time
 blocked in submit, and those per-wave figures (us).
 
     SCCSUM_LIB=seastar_amd/lib/ab/libsccsum_timeline.so python tools/dev/engine_probe.py
+
+ENGINE_MIXED=1: cfg 3's steps instead (one verify-only batch of Zipf frames,
+ENGINE_FRAMES frames each).
 """
 import ctypes
 import json
@@ -77,7 +80,15 @@ def main():
     for n, in_flight in [(n, f) for n in sizes for f in flights]:
         R = 4
         o_tx = torch.empty(2 * n, dtype=torch.int16, device=dev)
-        if os.environ.get("ENGINE_BENCH_DATA"):  # bench.py's cfg 2 batches: rx = tx with its checksums stored
+        mixed = bool(os.environ.get("ENGINE_MIXED"))  # cfg 3's steps: one verify-only Zipf batch each
+        if mixed:
+            from seastar_amd import synth
+            lens = synth.zipf_lengths(n, seed=1234)
+            txs = []
+            rxs = [devsynth.mixed_frames(lens, seed=7 * r, device=dev) for r in range(R)]
+            for rx in rxs:
+                batch.ipv4_fill(rx, native.FILL_IP | native.FILL_L4)
+        elif os.environ.get("ENGINE_BENCH_DATA"):  # bench.py's cfg 2 batches: rx = tx with its checksums stored
             txs, rxs = [], []
             for r in range(R):
                 txs.append(devsynth.udp_frames(n, 1500, seed=11 + r, device=dev))
@@ -88,7 +99,8 @@ def main():
             rxs = [devsynth.udp_frames(n, 1500, seed=31 + r, device=dev) for r in range(R)]
         sts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(R)]
         eng = batch.Engine(0, frames=True, max_steps=K + 8, max_in_flight=in_flight)
-        preps = [eng.prepare([(txs[r], o_tx, None), (rxs[r], None, sts[r])]) for r in range(R)]
+        preps = [eng.prepare([(rxs[r], None, sts[r])] if mixed else [(txs[r], o_tx, None), (rxs[r], None, sts[r])])
+                 for r in range(R)]
         s = torch.cuda.Stream(device=dev)
         torch.cuda.synchronize()
         for rep in range(2):  # the first run warms
