@@ -1428,7 +1428,11 @@ struct EngineSrc {
                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                              : 0ull;
             }
+#ifdef SCCSUM_AB_ONE_PHASE  // A/B only: reused slots rewritten in one phase too
+            const bool reuse = false;
+#else
             const bool reuse = ms + g > E.ring_mask + 1;  // some slot of the group held a step of this run
+#endif
             if (!reuse) {  // fresh slots (no probe reads them before the mirror says so): one phase
 #pragma unroll
                 for (uint32_t k = 0; k < kPollGroup; ++k) {
