@@ -1197,16 +1197,34 @@ constexpr uint32_t kPollGroup = 8;
 #else
 #define SCCSUM_HOT(x) __builtin_expect(!!(x), 1)
 #endif
-constexpr uint64_t kSlotInvalid = ~0ull;  // a slot's step word while the poller rewrites it
 // descriptor words
 constexpr uint32_t kEdFirst = 0;   // the step's first tile in the run
 constexpr uint32_t kEdTiles = 1;   // tiles | B (packets per tile) << 32
-constexpr uint32_t kEdStep = 2;    // the step's index in the run
+constexpr uint32_t kEdStep = 2;    // the step's seal (engine_seal: its index and where it ends, one word)
 constexpr uint32_t kEdNq = 3;      // batches in the step (1..kEngineQueues)
 constexpr uint32_t kEdTile0 = 4;   // tile0[0..nq]: the batches' first tiles within the step
 constexpr uint32_t kEdQueue = 9;   // + 8 q: bytes, bytes_len, off, len, seed, out, status, n (q < 4: words 9-40)
 constexpr uint32_t kEdKind = 41;   // kind | flat-body fill flags << 8 | public fill mode << 16
 constexpr uint32_t kEdDep = 42;    // 0, or 1 + the step whose completion this step's tiles wait for
+constexpr uint32_t kEdIndex = 43;  // the step's index in the run, whole
+// The seal: the step's index mod 2^28 over its end (first tile + tiles) mod
+// 2^36, so that one 8-byte read -- atomic, where three words of a slot are
+// not -- tells whether a slot holds step t and whether tile v lies past t's
+// end.  It misjudges only if 2^28 steps were published between two tiles of
+// one wave, or if 2^35 tiles lay between v and a probed step's end (2^35 tiles
+// of >= 1 packet carry >= 400 GB of offsets and lengths: more than HBM); then
+// the walk's last check faults (SCCSUM_EFAULT), never a wrong result.
+constexpr uint32_t kSealLastBits = 36;
+constexpr uint64_t kSealLastMask = (1ull << kSealLastBits) - 1;
+__host__ __device__ inline uint64_t engine_seal(uint64_t step, uint64_t end) {
+    return (step << kSealLastBits) | (end & kSealLastMask);
+}
+// step t's seal p says t ends at or before tile v, or that the slot holds
+// another step (then t is done, and v's step, unprocessed, lies after it)
+__host__ __device__ inline bool seal_before(uint64_t p, uint64_t t, uint64_t v) {
+    if ((p >> kSealLastBits) != (t & ((1ull << (64 - kSealLastBits)) - 1))) return true;
+    return ((v - p) & kSealLastMask) < (1ull << (kSealLastBits - 1));
+}
 // step kinds
 constexpr uint32_t kStepSum = 0;        // checksums into out / status (sccsum_engine_submit)
 constexpr uint32_t kStepFillGen = 1;    // fill, generate half: values into out2, status; frames untouched
@@ -1255,27 +1273,6 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t k) {
                << 32;
 }
 
-// Probe step t's slot for tile v: 0 = v lies in t (w = its descriptor, lane
-// i word i), 1 = t lies before v's step, 2 = after it.  A slot that holds
-// another step (or is being rewritten) means t is done, and every step before
-// it (the host reuses a slot only then), while v's step is not (v is the
-// caller's, unprocessed): so t lies before.  The step word is read again
-// after the descriptor: equal both times, every word read belongs to t (the
-// poller marks the slot invalid before it writes any other word).
-__device__ __forceinline__ uint32_t engine_probe(const uint64_t* dring, uint64_t ring_mask, uint32_t lane, uint64_t t,
-                                                 uint64_t v, uint64_t& w) {
-    const uint64_t* const slot = dring + (t & ring_mask) * kEngineSlotWords;
-    w = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (rl64(w, kEdStep) != t) return 1u;
-    asm volatile("" ::: "memory");  // the second read issues after the first has returned
-    uint64_t again = 0;
-    if (lane == kEdStep) again = __hip_atomic_load(slot + kEdStep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (rl64(again, kEdStep) != t) return 1u;
-    const uint64_t f = rl64(w, kEdFirst);
-    if (v < f) return 2u;
-    return v < f + static_cast<uint32_t>(rl64(w, kEdTiles)) ? 0u : 1u;
-}
-
 // A fault ends the wave where it stands (reported first; the host sees
 // SCCSUM_EFAULT).  (Returning it up through ready() / wait_ready() cost the
 // kernel ~40 VGPRs of merged control flow in the tile loop.)
@@ -1294,20 +1291,22 @@ __device__ __forceinline__ void engine_fault(uint64_t* ctl, uint32_t lane, uint6
 struct WalkHit {
     uint64_t t, w;
 };
-// walk()'s search past the step after the cursor (below: the step probed
-// there, r0 its answer): galloping, bounded by the mirror's step count, then
-// bisection.  Out of line (a call, on a wave's rare long walk), and so are
-// both faults: an s_endpgm anywhere in the kernel body's walk ran cfg 3
-// 1.5-2 % slower on the same box, with or without the search inlined
-// (profiles/r06_walk_ab.log).
+// walk()'s search past the step after the cursor (below: a step before v's):
+// galloping, bounded by the mirror's step count, then bisection for the first
+// step whose seal does not lie before v, each probe one 8-byte read of a seal;
+// then that step's whole descriptor, which no rewrite can touch (the step is
+// not done: v is the caller's, unprocessed).  Out of line (a call, on a
+// wave's rare long walk), and so are its faults: an s_endpgm anywhere in the
+// kernel body's walk ran cfg 3 1.5-2 % slower on the same box, with or without
+// the search inlined (profiles/r06_walk_ab.log).
 __device__ __attribute__((noinline)) WalkHit engine_walk_far(const uint64_t* dring, uint64_t ring_mask,
                                                              const uint64_t* mirror, uint64_t* ctl, uint64_t below,
-                                                             uint64_t v, uint32_t r0) {
+                                                             uint64_t v) {
     const uint32_t lane = __lane_id();
-    if (r0 == 2u) engine_fault(ctl, lane, kErrWalk);  // v before the step after the cursor's: never
-    uint64_t above = 0;
-    if (lane == 0) above = __hip_atomic_load(mirror + kMpSteps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    above = rfl64(above);  // below < step(v) < above
+    uint64_t hs = 0;
+    if (lane == 0) hs = __hip_atomic_load(mirror + kMpSteps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hs = rfl64(hs);
+    uint64_t above = hs;  // below lies before v's step; above does not (or is past every copied step)
     bool bisect = false;
     uint64_t d = 1;
     for (;;) {
@@ -1319,13 +1318,14 @@ __device__ __attribute__((noinline)) WalkHit engine_walk_far(const uint64_t* dri
                 continue;
             }
         } else {
-            if (above <= below + 1) engine_fault(ctl, lane, kErrWalk);  // a published tile in no published step
+            if (above <= below + 1) break;
             t = below + (above - below) / 2;
         }
-        uint64_t w = 0;
-        const uint32_t r = engine_probe(dring, ring_mask, lane, t, v, w);
-        if (r == 0u) return WalkHit{t, w};
-        if (r == 1u) {
+        uint64_t p = 0;
+        if (lane == 0) p = __hip_atomic_load(dring + (t & ring_mask) * kEngineSlotWords + kEdStep, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        p = rfl64(p);
+        if (seal_before(p, t, v)) {
             below = t;
             d <<= 1;
         } else {
@@ -1333,6 +1333,13 @@ __device__ __attribute__((noinline)) WalkHit engine_walk_far(const uint64_t* dri
             bisect = true;
         }
     }
+    if (above >= hs) engine_fault(ctl, lane, kErrWalk);  // a published tile in no published step
+    const uint64_t w = __hip_atomic_load(dring + (above & ring_mask) * kEngineSlotWords + lane, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    if (rl64(w, kEdIndex) != above || v < rl64(w, kEdFirst) || seal_before(rl64(w, kEdStep), above, v)) {
+        engine_fault(ctl, lane, kErrWalk);
+    }
+    return WalkHit{above, w};
 }
 
 struct EngineSrc {
@@ -1412,9 +1419,12 @@ struct EngineSrc {
         uint64_t tiles = mload(kMpTiles);
         // Copy the new descriptors in groups: a group's host reads are in
         // flight together (one PCIe round trip), then its slots are rewritten
-        // in three store phases — step word invalid (only a slot that held a
-        // step of this run: a probe of this run reads no other), the other
-        // words, the step word — each phase complete before the next begins.
+        // in one phase, reused or not: a probe of a slot it may be rewriting
+        // reads only the seal (one 8-byte word, engine_seal), and a probe that
+        // takes a whole descriptor does so only for a step that is not done,
+        // whose slot the host has not handed on (round 6's first form wrote
+        // reused slots in three waited phases: 0.1-0.25 us per tiny step,
+        // profiles/r06_poller_phases_ab.log).
         auto dslot = [&](uint64_t s) { return E.dring + (s & E.ring_mask) * kEngineSlotWords + lane; };
         auto put = [&](uint64_t s, uint64_t x) {
             __hip_atomic_store(dslot(s), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1428,31 +1438,9 @@ struct EngineSrc {
                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                              : 0ull;
             }
-#ifdef SCCSUM_AB_ONE_PHASE  // A/B only: reused slots rewritten in one phase too
-            const bool reuse = false;
-#else
-            const bool reuse = ms + g > E.ring_mask + 1;  // some slot of the group held a step of this run
-#endif
-            if (!reuse) {  // fresh slots (no probe reads them before the mirror says so): one phase
 #pragma unroll
-                for (uint32_t k = 0; k < kPollGroup; ++k) {
-                    if (k < g) put(ms + k, w[k]);
-                }
-            } else {
-#pragma unroll
-                for (uint32_t k = 0; k < kPollGroup; ++k) {
-                    if (k < g && lane == kEdStep) put(ms + k, kSlotInvalid);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-                for (uint32_t k = 0; k < kPollGroup; ++k) {
-                    if (k < g && lane != kEdStep) put(ms + k, w[k]);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-                for (uint32_t k = 0; k < kPollGroup; ++k) {
-                    if (k < g && lane == kEdStep) put(ms + k, w[k]);
-                }
+            for (uint32_t k = 0; k < kPollGroup; ++k) {
+                if (k < g) put(ms + k, w[k]);
             }
 #pragma unroll
             for (uint32_t k = 0; k < kPollGroup; ++k) {
@@ -1565,13 +1553,6 @@ struct EngineSrc {
         const uint64_t v = claim(0);
         return wait_ready(v) ? v : end();
     }
-    // (engine_probe(): step t copied, i.e. below the mirror's step count)
-    __device__ uint32_t probe(uint64_t t, uint64_t v, uint64_t& w) {
-#ifdef SCCSUM_AB_TIMELINE
-        ++ab[3];
-#endif
-        return engine_probe(E.dring, E.ring_mask, lane, t, v, w);
-    }
     __device__ void set_cursor(uint64_t t, uint64_t w) {
         step = t;
         dw = w;
@@ -1582,20 +1563,23 @@ struct EngineSrc {
     }
     // tile v (published) -> the cursor on its step.  Claims only rise, so v's
     // step is the cursor's or a later one: the step after the cursor's first
-    // (a wave's next tile is mostly there), else engine_walk_far(); every
-    // probe on a slot the ring may have reused since (engine_probe()).
+    // (a wave's next tile is mostly there).  Steps are contiguous in tiles, so
+    // that step starts where the cursor's ends, at or before v: its seal alone
+    // says whether it holds v.  If it does, the step is not done, its slot not
+    // reused, and every word of the descriptor read with the seal is its own.
+    // Else engine_walk_far().
     __device__ bool walk(uint64_t v) {
         if (SCCSUM_HOT(step != ~0ull && v < slast)) return true;
 #ifdef SCCSUM_AB_WALK_SEQ  // A/B only (a run shorter than its ring): round 5's walk, step by step
         while (step == ~0ull || v >= slast) {
             const uint64_t t = step + 1;
-            const uint64_t w = __hip_atomic_load(E.dring + (t & E.ring_mask) * kEngineSlotWords + lane, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-            set_cursor(t, w);
+            set_cursor(t, __hip_atomic_load(E.dring + (t & E.ring_mask) * kEngineSlotWords + lane, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT));
         }
         return true;
 #endif
 #ifdef SCCSUM_AB_TIMELINE
+        ++ab[3];
         const uint64_t w0 = static_cast<uint64_t>(wall_clock64());
         struct Walked {
             unsigned long long* a;
@@ -1603,13 +1587,13 @@ struct EngineSrc {
             __device__ ~Walked() { a[4] += static_cast<uint64_t>(wall_clock64()) - t0; }
         } walked{ab, w0};
 #endif
-        const uint64_t t = step + 1;  // (~0 + 1 = step 0)
-        uint64_t w = 0;
-        const uint32_t r = probe(t, v, w);
-        if (SCCSUM_HOT(r == 0u)) {
+        const uint64_t t = step + 1;  // (~0 + 1 = step 0, which starts at tile 0)
+        const uint64_t w = __hip_atomic_load(E.dring + (t & E.ring_mask) * kEngineSlotWords + lane, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        if (SCCSUM_HOT(!seal_before(rl64(w, kEdStep), t, v))) {
             set_cursor(t, w);
         } else {
-            const WalkHit h = engine_walk_far(E.dring, E.ring_mask, E.mirror, E.ctl, t, v, r);
+            const WalkHit h = engine_walk_far(E.dring, E.ring_mask, E.mirror, E.ctl, t, v);
             set_cursor(rfl64(h.t), h.w);
         }
         return true;
@@ -3596,7 +3580,8 @@ uint64_t engine_put(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbat
     const uint64_t ntiles = tile0[nq];
     d[sccsum::kEdFirst] = e->next_first;
     d[sccsum::kEdTiles] = ntiles | (B << 32);
-    d[sccsum::kEdStep] = s;
+    d[sccsum::kEdStep] = sccsum::engine_seal(s, e->next_first + ntiles);
+    d[sccsum::kEdIndex] = s;
     d[sccsum::kEdNq] = nq ? nq : 1;
     for (uint32_t q = 0; q <= SCCSUM_ENGINE_MAX_BATCHES; ++q) d[sccsum::kEdTile0 + q] = tile0[q];
     d[sccsum::kEdKind] = kind;
