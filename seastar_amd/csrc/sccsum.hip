@@ -1567,7 +1567,8 @@ struct EngineSrc {
     // that step starts where the cursor's ends, at or before v: its seal alone
     // says whether it holds v.  If it does, the step is not done, its slot not
     // reused, and every word of the descriptor read with the seal is its own.
-    // Else engine_walk_far().
+    // (The whole index is checked too: a seal's 28-bit index could match a
+    // step 2^28 later.)  Else engine_walk_far().
     __device__ bool walk(uint64_t v) {
         if (SCCSUM_HOT(step != ~0ull && v < slast)) return true;
 #ifdef SCCSUM_AB_WALK_SEQ  // A/B only (a run shorter than its ring): round 5's walk, step by step
@@ -1590,7 +1591,7 @@ struct EngineSrc {
         const uint64_t t = step + 1;  // (~0 + 1 = step 0, which starts at tile 0)
         const uint64_t w = __hip_atomic_load(E.dring + (t & E.ring_mask) * kEngineSlotWords + lane, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
-        if (SCCSUM_HOT(!seal_before(rl64(w, kEdStep), t, v))) {
+        if (SCCSUM_HOT(!seal_before(rl64(w, kEdStep), t, v) && rl64(w, kEdIndex) == t)) {
             set_cursor(t, w);
         } else {
             const WalkHit h = engine_walk_far(E.dring, E.ring_mask, E.mirror, E.ctl, t, v);
