@@ -777,15 +777,19 @@ def run_udp1500(args, world, rank, dev):
     # shows: 0xFFFF is no IPv4 or UDP checksum of these frames (~fold(sum) is 0xFFFF only for a zero sum)
     want_tx = [o[0].clone() for o in outs]
     want_st = [s.clone() for s in sts]
-    ran = sorted({k % R for k in range(args.steps)})
+    ran = sorted({k % R for k in range(warm, warm + args.steps)})
 
     def poison():
         for r in ran:
             outs[r][0].fill_(-1)
             sts[r].fill_(0xEE)
 
+    LAUNCHES.add(kern, 1 if engine else per_step * warm)  # the warm-up timed() runs again first
     sel = LAUNCHES.select(kern, 1 if engine else per_step * args.steps)
-    wall, step_s = timed(step, args.steps, 0, world, streams, begin, end, between=None if args.no_check else poison)
+    # the warm-up again, right before the timed region: the checks above leave the GPU idle for
+    # milliseconds, and a run that starts cold pays for it (+50 us after a 20 ms gap, +175 us after
+    # 100 ms: profiles/r06_run_cost.log)
+    wall, step_s = timed(step, args.steps, warm, world, streams, begin, end, between=None if args.no_check else poison)
     LAUNCHES.add(kern, 1 if engine else per_step * args.steps)
     avg_launch_s = step_s / per_step
     stream = streams[0]
