@@ -746,7 +746,7 @@ def run_udp1500(args, world, rank, dev):
             eng.start(streams[0])
 
         def end():
-            eng.finish()  # waits on the run's last step (a give-up raises), then stops the grid
+            eng.finish()  # stops the grid (it leaves once its steps are done), then waits on the run's last step (a give-up raises)
 
     def step(k):
         r = k % R
@@ -946,7 +946,7 @@ def run_mixed(args, world, rank, dev):
         def begin():
             eng.start(streams[0])
 
-        end = eng.finish  # waits on the run's last step (a give-up raises), then stops the grid
+        end = eng.finish  # stops the grid (it leaves once its steps are done), then waits on the run's last step (a give-up raises)
     LAUNCHES.add(kern, 1 if engine else warm)
     sel = LAUNCHES.select(kern, 1 if engine else args.steps)
     # the timed run's statuses are checked afterwards (every frame verifies): poisoned before it, so
@@ -1180,7 +1180,7 @@ def run_fill(args, world, rank, dev):
         def begin():
             eng.start(streams[0])
 
-        end = eng.finish  # waits on the run's last step (a give-up raises), then stops the grid
+        end = eng.finish  # stops the grid (it leaves once its steps are done), then waits on the run's last step (a give-up raises)
     else:
         pre = {(r, i): batch.prepare_call("sccsum_ipv4_fill", bs[r].data, bs[r].bytes_len, bs[r].off,
                                           bs[r].length, outs2[i], None, bs[r].n, bs[r].max_len, mode)

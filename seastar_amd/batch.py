@@ -558,14 +558,16 @@ class Engine:
         native.check(self._lib.sccsum_engine_stop(self._h), "sccsum_engine_stop")
 
     def finish(self, timeout_s: float = 10.0) -> None:
-        """Wait until the run's latest step is done, then stop: a give-up
-        (EIDLE) or fault (EFAULT) before it raises here instead of passing
-        unseen (a timed run that only stopped never looked)."""
-        try:
-            if self._last >= 0:
-                self.wait(self._last, timeout_s)
-        finally:
-            self.stop()
+        """Stop the run, then wait until its latest step is done: a give-up
+        (EIDLE) or fault (EFAULT) raises here instead of passing unseen
+        (a timed run that only stopped never looked).  The stop
+        comes first because the grid leaves once its published steps are done:
+        stopped after the wait, it left ~20 us later per run, the time for a
+        waiting wave to poll the host and see the stop
+        (profiles/r06_run_cost.log)."""
+        self.stop()
+        if self._last >= 0:
+            self.wait(self._last, timeout_s)
 
     def close(self) -> None:
         """Destroy the engine (stopping and synchronising a running one).

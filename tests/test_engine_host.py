@@ -110,21 +110,29 @@ def test_close_raises_when_the_run_left_a_step_undone(code):
     assert ok.calls == [("destroy", 0x99)]
 
 
-def test_finish_waits_on_the_last_step_then_stops():
-    """finish(): wait on the run's latest step, then stop — and a give-up seen
-    by the wait raises after the stop was still made (the grid must leave)."""
+def test_finish_stops_then_waits_on_the_last_step():
+    """finish(): stop (the grid leaves once its published steps are done),
+    then wait on the run's latest step — a give-up seen by the wait, or
+    reported by the stop itself, raises."""
     lib = _FakeLib()
     e = _engine(True, lib=lib)
     e._h, e._last = 0x10, 41
     e.finish()
-    assert lib.calls == [("wait", 41), ("stop", 0x10)]
+    assert lib.calls == [("stop", 0x10), ("wait", 41)]
     bad = _FakeLib(wait=native.SCCSUM_EIDLE)
     e = _engine(True, lib=bad)
     e._h, e._last = 0x11, 7
     with pytest.raises(native.SccsumError) as err:
         e.finish()
     assert err.value.code == native.SCCSUM_EIDLE
-    assert bad.calls == [("wait", 7), ("stop", 0x11)]
+    assert bad.calls == [("stop", 0x11), ("wait", 7)]
+    gave_up = _FakeLib(stop=native.SCCSUM_EFAULT)
+    e = _engine(True, lib=gave_up)
+    e._h, e._last = 0x13, 3
+    with pytest.raises(native.SccsumError) as err:
+        e.finish()
+    assert err.value.code == native.SCCSUM_EFAULT
+    assert gave_up.calls == [("stop", 0x13)]
     none = _FakeLib()
     e = _engine(True, lib=none)
     e._h = 0x12

@@ -12,6 +12,8 @@ cost at all (the K=200 run's rate).
 
 RUN_COST_GAP_MS=g: the host sleeps g ms before each run (an idle GPU between
 runs, as bench.py's checks between its warm-up and timed runs leave it).
+RUN_COST_STOP_FIRST=1: stop right after the last submit, then wait on the
+last step (the "last_done" phase is then the stop call, "stop" the wait).
 """
 import json
 import os
@@ -30,6 +32,7 @@ def main():
     ks = [int(a) for a in sys.argv[1:]] or [5, 20, 200]
     reps = int(os.environ.get("RUN_COST_REPS", "5"))
     gap_s = float(os.environ.get("RUN_COST_GAP_MS", "0")) / 1e3  # host idle before each run (the GPU idles too)
+    stop_first = bool(os.environ.get("RUN_COST_STOP_FIRST"))  # stop, then wait (phases last_done / stop swap)
     dev = torch.device("cuda:0")
     n, R = 1 << 20, 4
     o_tx = torch.empty(2 * n, dtype=torch.int16, device=dev)
@@ -58,10 +61,16 @@ def main():
             for k in range(1, K):
                 eng.submit_prepared(preps[k % R])
             t3 = time.perf_counter()
-            eng.wait(eng.last_step)
-            t4 = time.perf_counter()
-            eng.stop()
-            t5 = time.perf_counter()
+            if stop_first:  # the grid leaves as soon as its published steps are done
+                eng.stop()
+                t4 = time.perf_counter()
+                eng.wait(eng.last_step)
+                t5 = time.perf_counter()
+            else:
+                eng.wait(eng.last_step)
+                t4 = time.perf_counter()
+                eng.stop()
+                t5 = time.perf_counter()
             torch.cuda.synchronize()
             t6 = time.perf_counter()
             if rep == 0:
