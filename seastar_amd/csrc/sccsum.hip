@@ -24,6 +24,7 @@
 // for cross-checking.
 
 #include <hip/hip_runtime.h>
+#include "engine_seal.h"
 
 #include <atomic>
 #include <cctype>
@@ -1207,24 +1208,7 @@ constexpr uint32_t kEdQueue = 9;   // + 8 q: bytes, bytes_len, off, len, seed, o
 constexpr uint32_t kEdKind = 41;   // kind | flat-body fill flags << 8 | public fill mode << 16
 constexpr uint32_t kEdDep = 42;    // 0, or 1 + the step whose completion this step's tiles wait for
 constexpr uint32_t kEdIndex = 43;  // the step's index in the run, whole
-// The seal: the step's index mod 2^28 over its end (first tile + tiles) mod
-// 2^36, so that one 8-byte read -- atomic, where three words of a slot are
-// not -- tells whether a slot holds step t and whether tile v lies past t's
-// end.  It misjudges only if 2^28 steps were published between two tiles of
-// one wave, or if 2^35 tiles lay between v and a probed step's end (2^35 tiles
-// of >= 1 packet carry >= 400 GB of offsets and lengths: more than HBM); then
-// the walk's last check faults (SCCSUM_EFAULT), never a wrong result.
-constexpr uint32_t kSealLastBits = 36;
-constexpr uint64_t kSealLastMask = (1ull << kSealLastBits) - 1;
-__host__ __device__ inline uint64_t engine_seal(uint64_t step, uint64_t end) {
-    return (step << kSealLastBits) | (end & kSealLastMask);
-}
-// step t's seal p says t ends at or before tile v, or that the slot holds
-// another step (then t is done, and v's step, unprocessed, lies after it)
-__host__ __device__ inline bool seal_before(uint64_t p, uint64_t t, uint64_t v) {
-    if ((p >> kSealLastBits) != (t & ((1ull << (64 - kSealLastBits)) - 1))) return true;
-    return ((v - p) & kSealLastMask) < (1ull << (kSealLastBits - 1));
-}
+// The seal (kEdStep): engine_seal.h
 // step kinds
 constexpr uint32_t kStepSum = 0;        // checksums into out / status (sccsum_engine_submit)
 constexpr uint32_t kStepFillGen = 1;    // fill, generate half: values into out2, status; frames untouched
@@ -1441,6 +1425,18 @@ struct EngineSrc {
 #pragma unroll
             for (uint32_t k = 0; k < kPollGroup; ++k) {
                 if (k < g) put(ms + k, w[k]);
+            }
+            // A step without tiles is done once copied: the poller says so.
+            // (Marked done by the host at publication, it freed its host slot
+            // before the poller had read it, and a run of such steps let the
+            // host lap the ring past the copy: tests/test_gpu_engine.py
+            // test_engine_walk_across_empty_steps.)
+#pragma unroll
+            for (uint32_t k = 0; k < kPollGroup; ++k) {
+                if (k < g && static_cast<uint32_t>(rl64(w[k], kEdTiles)) == 0u && lane == 0) {
+                    __hip_atomic_store(E.ctl + kEcDone + 8u * ((ms + k) & E.ring_mask), ms + k + 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
 #pragma unroll
             for (uint32_t k = 0; k < kPollGroup; ++k) {
@@ -3597,16 +3593,16 @@ uint64_t engine_put(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbat
     int sync = sccsum::t_knobs.engine_sync_every;
     if (sync < 0) sync = ntiles >= 2 * e->waves ? static_cast<int>(sccsum::kEngineSyncEvery) : 0;
     // The barrier waits for the latest step with tiles: a step without tiles
-    // is done in host memory only (below), and its device done word never
-    // rises, so waiting on it would hold the grid until the dependency limit
-    // (fuzz case 35 at 16x: a barrier step behind an empty step).
+    // is marked done in host memory only (by the poller, once copied), and its
+    // device done word never rises, so waiting on it would hold the grid until
+    // the dependency limit (fuzz case 35 at 16x: a barrier step behind an
+    // empty step).
     if (dep == 0 && sync > 0 && s > 0 && s % static_cast<uint64_t>(sync) == 0 && e->last_tiled != ~0ull) {
         d[sccsum::kEdDep] = e->last_tiled + 1;
     }
     if (ntiles) e->last_tiled = s;
-    if (ntiles == 0) {  // nothing to sum: done at once (the descriptor still keeps the step numbering)
-        __atomic_store_n(e->ctl_h + sccsum::kEcDone + 8u * (s & (e->ring - 1u)), s + 1, __ATOMIC_RELEASE);
-    }
+    // (a step without tiles is done when the grid's poller has copied it: its
+    // host slot is free again only then)
     e->next_first += ntiles;
     e->next_step.store(s + 1, std::memory_order_release);
     // publish: the descriptor is complete before the grid's poller can see the step

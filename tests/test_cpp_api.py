@@ -29,6 +29,18 @@ def test_per_packet_api_matches_oracle(tmp_path):
     assert "OK" in r.stdout
 
 
+def test_engine_seal_arithmetic(tmp_path):
+    """The resident engine's step seal (seastar_amd/csrc/engine_seal.h,
+    DESIGN.md §5.11) on the host: its own step's seal orders every tile within
+    2^35 of the step's end correctly across both fields' wraps, and any other
+    step a ring can put in the slot reads as "before"."""
+    exe = _build(tmp_path, "seal_check", [os.path.join(REPO, "tests", "cpp", "seal_check.cc")],
+                 ["-I", os.path.join(REPO, "seastar_amd", "csrc")])
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "seal_check: OK" in r.stdout
+
+
 def test_batch_header_compiles(tmp_path):
     src = tmp_path / "b.cc"
     src.write_text('#include <seastar/net/ip_checksum_batch.hh>\n'
