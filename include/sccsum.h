@@ -250,7 +250,8 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  *       are sized by (bytes_len / n otherwise, too big for a batch that is a
  *       slice of a larger buffer).  The engine always runs the flat kernel, so
  *       sparse layouts give exact results but belong on the launches, whose
- *       row kernel reads them faster.  Frames take no seeds.
+ *       row kernel reads them faster.  Frames take no seeds.  A step whose
+ *       batches are all empty is done once the grid has taken it in.
  *   sccsum_engine_submit_fill(e, batches, nbatch, max_len, mode, timeout_ns, &step)
  *       an in-place fill (sccsum_ipv4_fill's SCCSUM_FILL_L4 and/or
  *       SCCSUM_FILL_ICMP_ECHO, optionally | SCCSUM_FILL_IP) of every batch

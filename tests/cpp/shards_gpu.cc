@@ -15,7 +15,8 @@
 // resident engine (include/sccsum.h, "Producers"; Seastar's per-core
 // reactors, src/core/reactor.cc:3437-3441, forwarding to the GPU's owner,
 // src/net/net.cc:309-322): a frames + fill engine with a 64-slot ring, then a
-// spans engine, each taking random steps from every thread at once — frames
+// spans engine, each taking random steps from every thread at once (some after
+// runs of steps without tiles) — frames
 // (generate, verify-only, both), in-place fills, seeded spans — every step's
 // results against the oracle.
 #include <hip/hip_runtime.h>
@@ -380,7 +381,18 @@ void producer_main(int shard, sccsum_engine* e, bool spans, int steps, Gate* gat
         uint16_t* o = outs + per_out * r;
         uint8_t* s = st + per_st * r;
         ProducerStep ps{spans ? 3 : static_cast<int>(rng() % 3), r, 0};
-        int rc;
+        int rc = SCCSUM_OK;
+        if (rng() % 4 == 0) {  // a run of steps without tiles first (each done once the grid has copied it)
+            const sccsum_batch z = {dA.bytes, 0, dA.off, dA.len, nullptr, o, s, 0};
+            uint64_t zs = 0;
+            for (int k = 1 + static_cast<int>(rng() % 20); k > 0 && rc == SCCSUM_OK; --k) {
+                rc = sccsum_engine_submit(e, &z, 1, 3100, 10'000'000'000ull, &zs);
+            }
+            if (!ok(rc, shard, "engine submit (no tiles)")) break;
+            if (rng() % 2 == 0 && !ok(sccsum_engine_wait(e, zs, 10'000'000'000ull), shard, "engine wait (no tiles)")) {
+                break;
+            }
+        }
         if (ps.kind == 3) {
             const sccsum_batch b = {dA.bytes, dA.bytes_len, dA.off, dA.len, d_seed, o, s, n};
             rc = sccsum_engine_submit(e, &b, 1, 3100, 10'000'000'000ull, &ps.step);
