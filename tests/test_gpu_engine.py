@@ -641,6 +641,50 @@ def test_engine_fill_stress_small_steps(dev, in_flight, fill_passes):
     eng.close()
 
 
+@pytest.mark.parametrize("ring", [4, 16])
+def test_engine_fill_across_empty_steps_on_a_small_ring(dev, ring, fill_passes):
+    """Fills of tiny batches (their store step, in the two-pass form, waits on
+    the generate step) with runs of 0-20 steps without tiles between them, on
+    a 4- or 16-slot ring with the in-flight limit at the ring: a store tile's
+    dependency and every wave's walk cross slots reused many times over.
+    Every filled batch equals the oracle's fill, every verify the oracle."""
+    from test_gpu_parity import _tx_frames
+
+    rng = np.random.default_rng(0xE5 + ring)
+    m = native.FILL_IP | native.FILL_L4
+    empty = batch.PacketBatch(data=torch.zeros(16, dtype=torch.uint8, device=dev),
+                              off=torch.zeros(0, dtype=torch.int64, device=dev),
+                              length=torch.zeros(0, dtype=torch.int32, device=dev), bytes_len=0, max_len=0)
+    empty_st = torch.empty(1, dtype=torch.uint8, device=dev)
+    plan = []
+    for k in range(150):
+        buf, off, length = _tx_frames(rng, int(rng.integers(1, 41)))
+        b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+        out2 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+        st = torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev)
+        gap = int(rng.integers(0, 21)) if rng.random() < 0.6 else 0
+        plan.append((gap, b, out2, st, oracle.batch_ipv4_fill(buf, off, length, m)))
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, fill=True, ring_slots=ring, max_in_flight=ring)
+    stream = torch.cuda.Stream(device=dev)
+    eng.start(stream)
+    last = 0
+    try:
+        for gap, b, out2, st, _ in plan:
+            for _ in range(gap):
+                last = max(last, eng.submit([(empty, None, empty_st)]))
+            last = max(last, eng.submit_fill([(b, out2, st)], m))
+        eng.wait(last)
+    finally:
+        eng.stop()
+        stream.synchronize()
+    eng.close()
+    for k, (_, b, out2, st, (want_buf, want_out2, want_st)) in enumerate(plan):
+        assert np.array_equal(b.data.cpu().numpy()[: b.bytes_len], want_buf), k
+        assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), want_out2), k
+        assert np.array_equal(st.cpu().numpy(), want_st), k
+
+
 @pytest.mark.parametrize("sync_every", [1, 3, 0])
 def test_engine_barrier_period(dev, sync_every):
     """The grid's barrier (a step that waits for the one before it,
