@@ -1172,19 +1172,21 @@ struct QueueSrc {
 //
 // Unbounded runs: the descriptors live in a RING of 2^k slots (step s in slot
 // s & ring_mask), host and device alike, and so do the steps' done words.  The
-// host publishes step s only once every step up to s - ring is done, so a
-// step that is not done always has its slot; a wave looking for the step of
-// its claimed tile (not done: the wave holds it) finds it by probing slots
-// (walk(): galloping and binary search from its cursor), where a slot that
-// holds another step means that step is done, and every step before it.  The
-// polling wave rewrites a slot seqlock-style (step word invalid, then the
-// other words, then the step word), and a probe reads the step word twice
-// around the descriptor, so a torn read is never taken for a valid one.
+// host publishes step s only once every step up to s - ring is done (a step
+// without tiles is done once the poller has copied it), so a step that is not
+// done always has its slot; a wave looking for the step of its claimed tile
+// (not done: the wave holds it) finds it by probing slots (walk(): the next
+// step, then galloping and binary search from its cursor), where a slot that
+// holds another step means that step is done, and every step before it.  A
+// probe decides from the step's seal, one 8-byte word (engine_seal.h), so the
+// polling wave rewrites a reused slot in one phase: a torn read of the other
+// words is never taken, as a wave reads a whole descriptor only for a step
+// that is not done.
 constexpr uint32_t kEngineSlotWords = 64;  // 512-byte descriptors
 constexpr uint32_t kEngineCountSlots = 64;  // completion counters: steps in flight at most
 constexpr uint32_t kEngineMaxRing = 1u << 16;  // descriptor ring slots (2 x 32 MiB of descriptor rings at most)
 constexpr uint32_t kEngineDefaultRing = 1024;
-// descriptors the polling wave copies per round of its store phases (only a
+// descriptors the polling wave copies per round of its stores (only a
 // waiting wave polls, holding no tile: with the poll inside the tile loop, 4
 // or 8 pushed the fill engine kernel into 224 B of scratch)
 #ifdef SCCSUM_AB_POLL_GROUP
