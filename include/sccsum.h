@@ -284,7 +284,10 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  * under the engine's lock (a few hundred ns, no device call), so steps are
  * published in the order their submits took the lock, and a submit that waits
  * for room waits outside it.  The in-flight limit is the engine's, shared by
- * every producer.  Start, stop and destroy belong to the engine's owner (a
+ * every producer; opts.producer_in_flight adds one per producer thread, so
+ * that no shard holds the whole shared limit: a thread's submit past it first
+ * waits (within its timeout) for that thread's oldest step not yet done.  (A
+ * fill counts once: by its last step.)  Start, stop and destroy belong to the engine's owner (a
  * submit after stop returns SCCSUM_EINVAL; destroy only after every producer's
  * last call has returned).
  *
@@ -308,6 +311,8 @@ typedef struct sccsum_engine_opts {
                                1..3 600 000; 0 = 1000 */
     uint32_t dep_ms;        /* limit of a step's wait on the step it depends on (a fill's store step on its
                                generate step, a barrier; SCCSUM_EFAULT past it), 1..3 600 000; 0 = 2000 */
+    uint32_t producer_in_flight; /* one producer thread's own steps submitted and not yet done,
+                                    1..max_in_flight; 0 = no limit of its own (Producers) */
 } sccsum_engine_opts;
 int sccsum_engine_create(int device, int mode, uint32_t max_steps, uint32_t max_in_flight, sccsum_engine** out);
 int sccsum_engine_create_opts(int device, int mode, const sccsum_engine_opts* opts, sccsum_engine** out);

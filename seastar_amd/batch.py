@@ -442,7 +442,9 @@ class Engine:
     A run takes any number of steps: their descriptors cycle through a ring
     of ring_slots slots (max_steps is its old name).  Any number of threads
     may submit into a running engine and wait on its steps (the shards of one
-    GPU); start / stop / finish / close belong to its owner.
+    GPU); start / stop / finish / close belong to its owner.  max_in_flight
+    is shared by every producer; producer_in_flight (0: none) also limits each
+    submitting thread's own steps not yet done.
 
     fill=True (frames): the run also takes in-place fills, each as a generate
     step and a store step (sccsum_engine_submit_fill):
@@ -454,14 +456,15 @@ class Engine:
     it); while it runs, every other kernel on the device waits for its stop."""
 
     def __init__(self, device: int = 0, frames: bool = True, max_steps: int | None = None, max_in_flight: int = 2,
-                 fill: bool = False, ring_slots: int | None = None, idle_ms: int = 0, dep_ms: int = 0):
+                 fill: bool = False, ring_slots: int | None = None, idle_ms: int = 0, dep_ms: int = 0,
+                 producer_in_flight: int = 0):
         import threading
 
         self._lib = native.load()
         h = ctypes.c_void_p()
         mode = (native.PIPE_IPV4 if frames else native.PIPE_SPANS) | (native.ENGINE_FILL if fill else 0)
         ring = ring_slots if ring_slots is not None else (max_steps if max_steps is not None else 1024)
-        opts = native.EngineOpts(int(ring), int(max_in_flight), int(idle_ms), int(dep_ms))
+        opts = native.EngineOpts(int(ring), int(max_in_flight), int(idle_ms), int(dep_ms), int(producer_in_flight))
         if ring <= 0 or max_in_flight <= 0:  # (0 would mean "the default" to the C-ABI)
             raise ValueError("ring_slots and max_in_flight must be >= 1")
         if hasattr(self._lib, "sccsum_engine_create_opts"):

@@ -3403,6 +3403,8 @@ struct sccsum_engine {
     uint64_t next_first = 0;             // under mu
     uint64_t last_tiled = ~0ull;         // under mu: the latest published step with tiles (a barrier's target)
     uint64_t done_floor = 0;             // under mu: every step below it is known done
+    uint32_t producer_limit = 0;         // opts.producer_in_flight (0: none)
+    uint64_t run = 0;                    // under mu: this run's number, unique in the process (producer records)
 };
 
 namespace {
@@ -3433,6 +3435,30 @@ struct EngineBlock {
 // src/core/reactor.cc:4163; ~16 of them per GPU on an 8-GPU box).
 std::mutex g_live_mu;
 sccsum_engine* g_live[sccsum::kMaxDevices] = {};
+std::atomic<uint64_t> g_engine_runs{0};  // numbers every run of every engine (a producer's records)
+
+// A producer thread's own steps not yet known done, per engine run it feeds
+// (opts.producer_in_flight).  Thread-local: a shard's reactor thread is the
+// producer, as Seastar's shards are (src/core/reactor.cc:3437).
+struct ProducerRecord {
+    const sccsum_engine* e = nullptr;
+    uint64_t run = 0;
+    uint64_t steps[sccsum::kEngineCountSlots] = {};  // a ring of its submitted steps, oldest at head
+    uint32_t head = 0, n = 0;
+};
+thread_local ProducerRecord t_producer[4];  // the runs this thread fed last (an engine per device at most)
+
+ProducerRecord& producer_record(const sccsum_engine* e, uint64_t run) {
+    ProducerRecord* free_one = &t_producer[0];
+    for (ProducerRecord& r : t_producer) {
+        if (r.e == e && r.run == run) return r;
+        if (r.run < free_one->run) free_one = &r;  // the oldest run's record is reused
+    }
+    *free_one = ProducerRecord{};
+    free_one->e = e;
+    free_one->run = run;
+    return *free_one;
+}
 
 void release_live(sccsum_engine* e) {
     std::lock_guard<std::mutex> g(g_live_mu);
@@ -3614,9 +3640,29 @@ uint64_t engine_put(sccsum_engine* e, const sccsum_batch* batches, uint32_t nbat
 
 // Publish k (1 or 2) steps together through put() once there is room,
 // waiting for room outside the lock (other producers publish meanwhile).
+// With a per-producer limit the calling thread first waits, outside the
+// lock, until fewer than that many of its own steps are pending.
 template <class Put>
 int engine_publish(sccsum_engine* e, uint32_t k, uint64_t timeout_ns, const Put& put) {
     const uint64_t t0 = now_ns();
+    ProducerRecord* pr = nullptr;
+    if (e->producer_limit) {
+        uint64_t run;
+        {
+            std::lock_guard<std::mutex> g(e->mu);
+            if (!e->running) return SCCSUM_EINVAL;
+            run = e->run;
+        }
+        pr = &producer_record(e, run);
+        while (pr->n >= e->producer_limit) {
+            const uint64_t oldest = pr->steps[pr->head];
+            const uint64_t spent = now_ns() - t0;
+            const int rc = engine_wait_done(e, oldest, spent < timeout_ns ? timeout_ns - spent : 0);
+            if (rc != SCCSUM_OK) return rc;
+            pr->head = (pr->head + 1) % sccsum::kEngineCountSlots;
+            --pr->n;
+        }
+    }
     for (;;) {
         uint64_t need = 0;
         {
@@ -3625,6 +3671,11 @@ int engine_publish(sccsum_engine* e, uint32_t k, uint64_t timeout_ns, const Put&
             if (const int rc = engine_error(e)) return rc;
             if (engine_room(e, k, &need)) {
                 put();
+                if (pr) {  // the put's last step (a fill's store step) stands for it
+                    pr->steps[(pr->head + pr->n) % sccsum::kEngineCountSlots] =
+                        e->next_step.load(std::memory_order_relaxed) - 1;
+                    ++pr->n;
+                }
                 return SCCSUM_OK;
             }
         }
@@ -3655,6 +3706,7 @@ int sccsum_engine_create_opts(int device, int mode, const sccsum_engine_opts* op
     const uint32_t mif = opts->max_in_flight ? opts->max_in_flight : 8u;
     uint64_t idle_ticks = 0, dep_ticks = 0;
     if (ring_req > sccsum::kEngineMaxRing || mif > sccsum::kEngineCountSlots || (fill && mif < 2) ||
+        opts->producer_in_flight > mif ||
         engine_ms(opts->idle_ms, 1000u, &idle_ticks) != SCCSUM_OK || engine_ms(opts->dep_ms, 2000u, &dep_ticks) != SCCSUM_OK) {
         return SCCSUM_EINVAL;
     }
@@ -3677,6 +3729,7 @@ int sccsum_engine_create_opts(int device, int mode, const sccsum_engine_opts* op
     e->limit = mif < ring ? mif : ring;
     e->idle_ticks = idle_ticks;
     e->dep_ticks = dep_ticks;
+    e->producer_limit = opts->producer_in_flight;
     const uint64_t ring_bytes = uint64_t(ring) * sccsum::kEngineSlotWords * 8u;
     const uint64_t ctl_bytes = (sccsum::kEcDone + 8u * uint64_t(ring)) * 8u;
     const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
@@ -3775,6 +3828,7 @@ int sccsum_engine_start(sccsum_engine* e, void* stream) {
     e->next_first = 0;
     e->last_tiled = ~0ull;
     e->done_floor = 0;
+    e->run = g_engine_runs.fetch_add(1, std::memory_order_relaxed) + 1;
     e->dirty = false;  // (until this run is found to have given up)
     return SCCSUM_OK;
 }

@@ -139,7 +139,7 @@ ENGINE_MAX_BATCHES = 4
 class EngineOpts(ctypes.Structure):
     """sccsum_engine_opts: a resident engine's limits (0 = the default)."""
     _fields_ = [("ring_slots", ctypes.c_uint32), ("max_in_flight", ctypes.c_uint32), ("idle_ms", ctypes.c_uint32),
-                ("dep_ms", ctypes.c_uint32)]
+                ("dep_ms", ctypes.c_uint32), ("producer_in_flight", ctypes.c_uint32)]
 
 
 class Fragment(ctypes.Structure):

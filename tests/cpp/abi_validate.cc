@@ -132,13 +132,17 @@ static void checks() {
     EXPECT(sccsum_set_engine_idle_ms(250) == SCCSUM_OK && sccsum_set_engine_idle_ms(0) == SCCSUM_OK);
     // create with every limit (ABI 4): ranges are checked before any runtime call
     const sccsum_engine_opts big_ring = {65537, 8, 0, 0}, many = {1024, 65, 0, 0}, idle = {1024, 8, 3600001, 0},
-                             dep = {1024, 8, 0, 3600001}, fill1 = {1024, 1, 0, 0};
+                             dep = {1024, 8, 0, 3600001}, fill1 = {1024, 1, 0, 0},
+                             producer = {1024, 8, 0, 0, 9}, producer_default_mif = {1024, 0, 0, 0, 9};
     EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4, nullptr, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4, &big_ring, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4, &many, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_SPANS, &idle, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_SPANS, &dep, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4 | SCCSUM_ENGINE_FILL, &fill1, &eng) == SCCSUM_EINVAL);
+    // a producer's own limit above the shared one (given, or the default 8)
+    EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4, &producer, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_SPANS, &producer_default_mif, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_SPANS | SCCSUM_ENGINE_FILL, &many, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4, &big_ring, nullptr) == SCCSUM_EINVAL);
     EXPECT(eng == nullptr);

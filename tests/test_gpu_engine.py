@@ -924,6 +924,54 @@ def test_engine_unbounded_run_on_a_small_ring(dev, ring, in_flight, steps):
     assert bad.size == 0, f"laps of the burst pool with a wrong frame: {bad[:8].tolist()} of {steps // pool}"
 
 
+def test_engine_producer_limit(dev):
+    """opts.producer_in_flight (a per-producer in-flight
+    limit): four producer threads share a 64-step engine limit, each held to
+    2 of its own steps not yet done.  When a thread's submit of its k-th step
+    returns, its (k-2)-th step is done (a wait with no time left answers 0);
+    every step's frames equal the oracle's."""
+    import threading
+
+    B, per, threads = 32, 300, 4
+    buf, off, lens, _ = synth.udp_ipv4_frames(B * per * threads, 300, seed=53)
+    want, want_st = oracle.batch_ipv4(buf, off, lens)
+    b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+    out = torch.full((B * per * threads * 2,), -1, dtype=torch.int16, device=dev)
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, ring_slots=256, max_in_flight=64, producer_in_flight=2)
+    with pytest.raises(native.SccsumError):  # above the shared limit
+        batch.Engine(0, frames=True, ring_slots=256, max_in_flight=8, producer_in_flight=9)
+    stream = torch.cuda.Stream(device=dev)
+    errors = []
+
+    def producer(t):
+        try:
+            mine = []
+            for k in range(per):
+                q = t * per + k
+                sl = batch.PacketBatch(data=b.data, off=b.off[B * q:B * (q + 1)], length=b.length[B * q:B * (q + 1)],
+                                       bytes_len=b.bytes_len, max_len=300)
+                mine.append(eng.submit([(sl, out[2 * B * q:2 * B * (q + 1)], None)]))
+                if k >= 2:
+                    eng.wait(mine[k - 2], timeout_s=0)  # SccsumError(EBUSY) if the limit let it run ahead
+        except Exception as exc:  # noqa: BLE001
+            errors.append((t, exc))
+
+    eng.start(stream)
+    try:
+        ts = [threading.Thread(target=producer, args=(t,)) for t in range(threads)]
+        for th in ts:
+            th.start()
+        for th in ts:
+            th.join()
+    finally:
+        eng.finish()
+        stream.synchronize()
+    eng.close()
+    assert not errors, errors[:3]
+    assert np.array_equal(batch.as_u16(out).reshape(-1, 2), want)
+
+
 @pytest.mark.parametrize("ring,in_flight", [(2, 2), (4, 4), (64, 8)])
 def test_engine_walk_across_empty_steps(dev, ring, in_flight):
     """Bursts of 32 frames with runs of 0-60 empty steps between them (the
