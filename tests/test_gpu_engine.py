@@ -924,6 +924,104 @@ def test_engine_unbounded_run_on_a_small_ring(dev, ring, in_flight, steps):
     assert bad.size == 0, f"laps of the burst pool with a wrong frame: {bad[:8].tolist()} of {steps // pool}"
 
 
+def test_engine_eight_producers(dev):
+    """eight threads submit random steps into one running
+    engine — frames (generate, verify-only), in-place fills and, in a second
+    engine run, seeded spans — each thread waiting on some of its own steps;
+    every step's results against the oracle.  (The native-thread form of the
+    same is tests/cpp/shards_gpu.cc engine, test_cpp_api.py.)"""
+    import threading
+    from test_gpu_parity import _tx_frames
+
+    threads, per = 8, 30
+    m = native.FILL_IP | native.FILL_L4 | native.FILL_ICMP_ECHO
+
+    def frames_plan(t):
+        rng = np.random.default_rng(0x8E0 + t)
+        plan = []
+        for k in range(per):
+            kind = int(rng.integers(0, 3))
+            if kind == 2:
+                buf, off, length = _tx_frames(rng, int(rng.integers(1, 300)))
+                b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+                out2 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+                st = torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev)
+                plan.append(("fill", b, out2, st, oracle.batch_ipv4_fill(buf, off, length, m)))
+            else:
+                b, want, want_st = _frames_step(rng, dev, int(rng.integers(0, 3)))
+                if kind == 0:
+                    plan.append(("gen", b, torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev), None, want))
+                else:
+                    plan.append(("verify", b, None, torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev), want_st))
+        return plan
+
+    def spans_plan(t):
+        rng = np.random.default_rng(0x8F0 + t)
+        plan = []
+        for k in range(per):
+            n = int(rng.integers(1, 3000))
+            lens = synth.zipf_lengths(n, seed=int(rng.integers(1 << 30)))
+            off, total = synth.pack(lens, seed=int(rng.integers(1 << 30)), max_gap=5)
+            buf = rng.integers(0, 256, total, dtype=np.uint8)
+            seeds = rng.integers(0, 65536, n).astype(np.uint32)
+            b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+            plan.append(("spans", b, torch.empty(n, dtype=torch.int16, device=dev),
+                         torch.from_numpy(seeds.view(np.int32)).to(dev), oracle.batch_spans(buf, off, lens, seeds)))
+        return plan
+
+    def run(eng, plans):
+        errors = []
+
+        def producer(t):
+            try:
+                rng = np.random.default_rng(0x8A0 + t)
+                for what, b, out, st, _ in plans[t]:
+                    if what == "fill":
+                        s = eng.submit_fill([(b, out, st)], m)
+                    elif what == "spans":
+                        s = eng.submit([(b, out, None, st)])
+                    else:
+                        s = eng.submit([(b, out, st)])
+                    if rng.random() < 0.2:
+                        eng.wait(s)
+            except Exception as exc:  # noqa: BLE001
+                errors.append((t, exc))
+
+        stream = torch.cuda.Stream(device=dev)
+        torch.cuda.synchronize()
+        eng.start(stream)
+        try:
+            ts = [threading.Thread(target=producer, args=(t,)) for t in range(threads)]
+            for th in ts:
+                th.start()
+            for th in ts:
+                th.join()
+        finally:
+            eng.finish()
+            stream.synchronize()
+        eng.close()
+        assert not errors, errors[:3]
+
+    plans = [frames_plan(t) for t in range(threads)]
+    run(batch.Engine(0, frames=True, fill=True, ring_slots=64, max_in_flight=16), plans)
+    for t, plan in enumerate(plans):
+        for k, (what, b, out, st, want) in enumerate(plan):
+            msg = f"thread {t} step {k} ({what})"
+            if what == "fill":
+                assert np.array_equal(b.data.cpu().numpy()[: b.bytes_len], want[0]), msg
+                assert np.array_equal(batch.as_u16(out).reshape(-1, 2), want[1]), msg
+                assert np.array_equal(st.cpu().numpy(), want[2]), msg
+            elif what == "gen":
+                assert np.array_equal(batch.as_u16(out).reshape(-1, 2), want), msg
+            else:
+                assert np.array_equal(st.cpu().numpy(), want), msg
+    plans = [spans_plan(t) for t in range(threads)]
+    run(batch.Engine(0, frames=False, ring_slots=64, max_in_flight=16), plans)
+    for t, plan in enumerate(plans):
+        for k, (_, b, out, _, want) in enumerate(plan):
+            assert np.array_equal(batch.as_u16(out), want), f"thread {t} span step {k}"
+
+
 def test_engine_producer_limit(dev):
     """opts.producer_in_flight (a per-producer in-flight
     limit): four producer threads share a 64-step engine limit, each held to
