@@ -1022,6 +1022,72 @@ def test_engine_eight_producers(dev):
             assert np.array_equal(batch.as_u16(out), want), f"thread {t} span step {k}"
 
 
+def test_engine_stop_while_producers_submit(dev):
+    """The owner stops the run while four threads are still submitting:
+    every submit either returns SCCSUM_EINVAL (after the stop) or a step that
+    the leaving grid completes — none is lost (include/sccsum.h, Producers).
+    Every accepted step's outputs against the oracle; the next run of the same
+    engine starts clean."""
+    import threading
+    import time
+
+    B, per, threads = 64, 1000, 4
+    buf, off, lens, _ = synth.udp_ipv4_frames(B * per * threads, 200, seed=59)
+    want, _ = oracle.batch_ipv4(buf, off, lens)
+    b = batch.PacketBatch.from_host(buf, off, lens, device=dev)
+    out = torch.full((B * per * threads * 2,), -1, dtype=torch.int16, device=dev)
+    torch.cuda.synchronize()
+    eng = batch.Engine(0, frames=True, ring_slots=16, max_in_flight=8)
+    stream = torch.cuda.Stream(device=dev)
+    accepted = [[] for _ in range(threads)]
+    errors, started = [], threading.Barrier(threads + 1)
+
+    def producer(t):
+        started.wait()
+        for k in range(per):
+            q = t * per + k
+            sl = batch.PacketBatch(data=b.data, off=b.off[B * q:B * (q + 1)], length=b.length[B * q:B * (q + 1)],
+                                   bytes_len=b.bytes_len, max_len=200)
+            try:
+                accepted[t].append((q, eng.submit([(sl, out[2 * B * q:2 * B * (q + 1)], None)])))
+            except native.SccsumError as exc:
+                if exc.code != native.SCCSUM_EINVAL:
+                    errors.append((t, k, exc))
+                return  # stopped: every later submit would be refused too
+
+    eng.start(stream)
+    ts = [threading.Thread(target=producer, args=(t,)) for t in range(threads)]
+    for th in ts:
+        th.start()
+    started.wait()
+    time.sleep(0.003)
+    eng.stop()
+    for th in ts:
+        th.join()
+    stream.synchronize()
+    assert not errors, errors[:3]
+    n_acc = sum(len(a) for a in accepted)
+    assert 0 < n_acc < per * threads, n_acc  # the stop landed mid-run
+    for a in accepted:
+        for q, s in a:
+            eng.wait(s, timeout_s=0)  # done before the grid left
+    got = batch.as_u16(out).reshape(threads * per, B, 2)
+    ref = want.reshape(threads * per, B, 2)
+    done_q = sorted(q for a in accepted for q, _ in a)
+    assert np.array_equal(got[done_q], ref[done_q])
+    rest = np.setdiff1d(np.arange(threads * per), done_q)
+    assert np.all(batch.as_u16(out).reshape(threads * per, B * 2)[rest] == 0xFFFF)  # refused steps never ran
+    # the same engine runs again
+    out.fill_(-1)
+    eng.start(stream)
+    sl = batch.PacketBatch(data=b.data, off=b.off[:B], length=b.length[:B], bytes_len=b.bytes_len, max_len=200)
+    eng.wait(eng.submit([(sl, out[:2 * B], None)]))
+    eng.finish()
+    stream.synchronize()
+    eng.close()
+    assert np.array_equal(batch.as_u16(out[:2 * B]).reshape(B, 2), ref[0])
+
+
 def test_engine_producer_limit(dev):
     """opts.producer_in_flight (a per-producer in-flight
     limit): four producer threads share a 64-step engine limit, each held to
