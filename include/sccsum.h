@@ -232,7 +232,7 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
  *       max_steps (1..65536, rounded up to a power of two, at least 2) = the
  *       slots of the engine's descriptor RING (512 B of pinned memory and as
  *       much device memory each): a run takes any number of steps, a slot
- *       being reused once its step is done; at most min(max_in_flight (1..64),
+ *       being reused once its step is done; at most min(max_in_flight (1..256),
  *       max_steps) steps submitted and not yet done.  Allocates on `device`;
  *       the calling thread's current device is left as it was.
  *   sccsum_engine_create_opts(device, mode, &opts, &e)   the same with every
@@ -306,7 +306,7 @@ int sccsum_ipv4_frames_multi(const sccsum_batch* batches, uint32_t nbatch, uint3
 typedef struct sccsum_engine sccsum_engine;
 typedef struct sccsum_engine_opts {
     uint32_t ring_slots;    /* descriptor ring slots, 1..65536 (a power of two, at least 2, above); 0 = 1024 */
-    uint32_t max_in_flight; /* steps submitted and not yet done, 1..64 (fill engines: >= 2); 0 = 8 */
+    uint32_t max_in_flight; /* steps submitted and not yet done, 1..256 (fill engines: >= 2); 0 = 8 */
     uint32_t idle_ms;       /* the grid leaves after this long without a new step (SCCSUM_EIDLE),
                                1..3 600 000; 0 = 1000 */
     uint32_t dep_ms;        /* limit of a step's wait on the step it depends on (a fill's store step on its

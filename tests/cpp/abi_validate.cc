@@ -112,7 +112,7 @@ static void checks() {
     EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, 0, 2, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, 65537, 2, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_SPANS, 16, 0, &eng) == SCCSUM_EINVAL);
-    EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_SPANS, 16, 65, &eng) == SCCSUM_EINVAL);
+    EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_SPANS, 16, 257, &eng) == SCCSUM_EINVAL);
     EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, 16, 2, nullptr) == SCCSUM_EINVAL);
     // fill steps: frames only, and at least 2 steps in flight (a fill is two)
     EXPECT(sccsum_engine_create(0, SCCSUM_PIPE_SPANS | SCCSUM_ENGINE_FILL, 16, 2, &eng) == SCCSUM_EINVAL);
@@ -131,7 +131,7 @@ static void checks() {
     EXPECT(sccsum_set_engine_idle_ms(-1) == SCCSUM_EINVAL && sccsum_set_engine_idle_ms(3600001) == SCCSUM_EINVAL);
     EXPECT(sccsum_set_engine_idle_ms(250) == SCCSUM_OK && sccsum_set_engine_idle_ms(0) == SCCSUM_OK);
     // create with every limit (ABI 4): ranges are checked before any runtime call
-    const sccsum_engine_opts big_ring = {65537, 8, 0, 0}, many = {1024, 65, 0, 0}, idle = {1024, 8, 3600001, 0},
+    const sccsum_engine_opts big_ring = {65537, 8, 0, 0}, many = {1024, 257, 0, 0}, idle = {1024, 8, 3600001, 0},
                              dep = {1024, 8, 0, 3600001}, fill1 = {1024, 1, 0, 0},
                              producer = {1024, 8, 0, 0, 9}, producer_default_mif = {1024, 0, 0, 0, 9};
     EXPECT(sccsum_engine_create_opts(0, SCCSUM_PIPE_IPV4, nullptr, &eng) == SCCSUM_EINVAL);

@@ -17,7 +17,8 @@
 // one GPU feeding its one engine (include/sccsum.h "Producers") — each
 // submitting its share of the k steps; the clock runs from a common start to
 // the last thread's last step done.  ENGINE_STEPS_RING sets the engine's ring
-// slots (default 1 024, the library's default).
+// slots (default 1 024, the library's default), ENGINE_STEPS_IN_FLIGHT its
+// in-flight limit (default 64).
 // Prints one JSON line per size.  Build (tools/gpu_session.sh bin: step):
 //   hipcc -O2 -std=c++17 -I include tools/dev/engine_steps.cc -L seastar_amd/lib -lsccsum \
 //         -Wl,-rpath,$PWD/seastar_amd/lib -o tools/dev/engine_steps
@@ -104,6 +105,8 @@ int main(int argc, char** argv) {
     const bool producers = argc > 1 && std::strcmp(argv[1], "producers") == 0;
     const int nprod = producers && argc > 2 ? std::atoi(argv[2]) : 8;
     const uint32_t ring = std::getenv("ENGINE_STEPS_RING") ? std::atoi(std::getenv("ENGINE_STEPS_RING")) : 1024;
+    // steps in flight (ENGINE_STEPS_IN_FLIGHT, default 64: the engine's most)
+    const uint32_t mif = std::getenv("ENGINE_STEPS_IN_FLIGHT") ? std::atoi(std::getenv("ENGINE_STEPS_IN_FLIGHT")) : 64;
     const uint32_t mode = SCCSUM_FILL_IP | SCCSUM_FILL_L4;
     const uint64_t n_all = 1 << 18;  // 262 144 frames, 393 MB
     const uint32_t L = 1500;
@@ -148,7 +151,7 @@ int main(int argc, char** argv) {
             const uint64_t slices = n_all / B;
             const uint64_t k = B <= 128 ? 40000 : 10000;
             sccsum_engine* e = nullptr;
-            SC_OK(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, ring, 64, &e));
+            SC_OK(sccsum_engine_create(0, SCCSUM_PIPE_IPV4, ring, mif, &e));
             (void)producers_run(e, s, 1, 256, B, slices, d_bytes, host.size(), d_off, d_len, d_st);  // warm
             const double one = producers_run(e, s, 1, k, B, slices, d_bytes, host.size(), d_off, d_len, d_st);
             const double many = producers_run(e, s, nprod, k, B, slices, d_bytes, host.size(), d_off, d_len, d_st);
@@ -197,7 +200,7 @@ int main(int argc, char** argv) {
         const double launch_s = now_s() - t0;
         // engine
         sccsum_engine* e = nullptr;
-        SC_OK(sccsum_engine_create(0, SCCSUM_PIPE_IPV4 | (fill ? SCCSUM_ENGINE_FILL : 0), ring, 64, &e));
+        SC_OK(sccsum_engine_create(0, SCCSUM_PIPE_IPV4 | (fill ? SCCSUM_ENGINE_FILL : 0), ring, mif, &e));
         double engine_s = 0;
         for (int run = 0; run < 2; ++run) {  // the first run warms up
             const uint64_t kk = run ? k : 64;
