@@ -1190,13 +1190,16 @@ constexpr uint32_t kEngineSlotWords = 64;  // 512-byte descriptors
 constexpr uint32_t kEngineCountSlots = 256;
 constexpr uint32_t kEngineMaxRing = 1u << 16;  // descriptor ring slots (2 x 32 MiB of descriptor rings at most)
 constexpr uint32_t kEngineDefaultRing = 1024;
-// descriptors the polling wave copies per round of its stores (only a
-// waiting wave polls, holding no tile: with the poll inside the tile loop, 4
-// or 8 pushed the fill engine kernel into 224 B of scratch)
+// descriptors the polling wave copies per round of its stores, their host
+// reads in flight together (only a waiting wave polls, holding no tile: with
+// the poll inside the tile loop, 4 or 8 pushed the fill engine kernel into
+// 224 B of scratch).  16 against 8 at 128 steps in flight: 32 / 128 / 1 024-
+// packet steps 0.63 / 1.03 / 3.02 against 0.70 / 1.10 / 3.10 us, the same
+// registers (profiles/r06_in_flight.log).
 #ifdef SCCSUM_AB_POLL_GROUP
 constexpr uint32_t kPollGroup = SCCSUM_AB_POLL_GROUP;  // A/B only
 #else
-constexpr uint32_t kPollGroup = 8;
+constexpr uint32_t kPollGroup = 16;
 #endif
 // the engine's per-tile checks: their slow paths placed out of the tile loop
 #ifdef SCCSUM_AB_NO_EXPECT  // A/B only
