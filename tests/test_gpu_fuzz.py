@@ -726,6 +726,97 @@ def test_fuzz_engine_spans(dev, case):
             assert np.array_equal(it[2][:n].cpu().numpy(), wst), msg
 
 
+@pytest.mark.parametrize("case", range(2 * SCALE))
+def test_fuzz_engine_producers(dev, case):
+    """Several producer threads into one fill engine at once, each a random
+    mix of frame steps (generate, verify-only), in-place fills and runs of
+    steps without tiles, on a random small ring with a random shared and
+    per-producer in-flight limit: every step's results the oracle's."""
+    import threading
+    from test_gpu_parity import _tx_frames
+
+    rng = np.random.default_rng(8800 + case)
+    threads = int(rng.choice([2, 4, 8]))
+    ring = int(rng.choice([2, 4, 16, 64]))
+    mif = int(rng.choice([2, 8, 64]))
+    plim = int(rng.choice([0, 1, 2])) if mif >= 2 else 0
+    m = native.FILL_IP | native.FILL_L4 | native.FILL_ICMP_ECHO
+    empty = batch.PacketBatch(data=torch.zeros(16, dtype=torch.uint8, device=dev),
+                              off=torch.zeros(0, dtype=torch.int64, device=dev),
+                              length=torch.zeros(0, dtype=torch.int32, device=dev), bytes_len=0, max_len=0)
+    empty_st = torch.empty(1, dtype=torch.uint8, device=dev)
+    plans = []
+    for t in range(threads):
+        trng = np.random.default_rng(8900 + 16 * case + t)
+        plan = []
+        for _ in range(int(trng.integers(5, 25))):
+            r = trng.random()
+            if r < 0.2:
+                plan.append(("empty", int(trng.integers(1, 12))))
+            elif r < 0.45:
+                buf, off, length = _tx_frames(trng, int(trng.integers(1, 200)))
+                b = batch.PacketBatch.from_host(buf, off, length, device=dev)
+                out2 = torch.full((2 * b.n,), -1, dtype=torch.int16, device=dev)
+                st = torch.full((b.n,), 0xEE, dtype=torch.uint8, device=dev)
+                plan.append(("fill", b, out2, st, oracle.batch_ipv4_fill(buf, off, length, m)))
+            else:
+                n = int(trng.choice([1, 64, 700]))
+                L = _lengths(trng, n, huge=False)
+                off, total, _ = _layout(trng, L)
+                buf = trng.integers(0, 256, size=max(total, 1), dtype=np.uint8)
+                _ipv4_headers(trng, buf, off, L)
+                b = batch.PacketBatch.from_host(buf[:total], off, L, device=dev)
+                out2 = torch.full((2 * n,), -1, dtype=torch.int16, device=dev) if trng.random() < 0.6 else None
+                st = torch.full((n,), 0xEE, dtype=torch.uint8, device=dev)
+                plan.append(("sum", b, out2, st, oracle.batch_ipv4(buf, off, L)))
+        plans.append(plan)
+    eng = batch.Engine(0, frames=True, fill=True, ring_slots=ring, max_in_flight=max(mif, 2),
+                       producer_in_flight=min(plim, max(mif, 2)))
+    errors = []
+
+    def producer(t):
+        try:
+            for item in plans[t]:
+                if item[0] == "empty":
+                    for _ in range(item[1]):
+                        eng.submit([(empty, None, empty_st)])
+                elif item[0] == "fill":
+                    eng.submit_fill([(item[1], item[2], item[3])], m)
+                else:
+                    eng.submit([(item[1], item[2], item[3])])
+        except Exception as exc:  # noqa: BLE001
+            errors.append((t, exc))
+
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    eng.start(stream)
+    try:
+        ts = [threading.Thread(target=producer, args=(t,)) for t in range(threads)]
+        for th in ts:
+            th.start()
+        for th in ts:
+            th.join()
+    finally:
+        eng.finish()
+        stream.synchronize()
+        eng.close()
+    knobs = f"threads {threads} ring {ring} in_flight {mif} per-producer {plim}"
+    assert not errors, (knobs, errors[:3])
+    for t, plan in enumerate(plans):
+        for k, item in enumerate(plan):
+            msg = f"case {case} thread {t} item {k} ({item[0]}), {knobs}"
+            if item[0] == "fill":
+                _, b, out2, st, (wbuf, wout2, wst) = item
+                assert np.array_equal(b.data.cpu().numpy()[: b.bytes_len], wbuf), msg
+                assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), wout2), msg
+                assert np.array_equal(st.cpu().numpy(), wst), msg
+            elif item[0] == "sum":
+                _, b, out2, st, (w2, wst) = item
+                if out2 is not None:
+                    assert np.array_equal(batch.as_u16(out2).reshape(-1, 2), w2), msg
+                assert np.array_equal(st.cpu().numpy(), wst), msg
+
+
 @pytest.mark.parametrize("case", range(4 * SCALE))
 def test_fuzz_large_batches(dev, case):
     """100 k-300 k packets under random knobs: long claim chains per wave,
