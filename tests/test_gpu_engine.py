@@ -913,7 +913,7 @@ def test_engine_unbounded_run_on_a_small_ring(dev, ring, in_flight, steps):
         assert step.value == steps - 1
         eng.wait(steps - 1)
         for k in range(max(0, steps - ring), steps):  # the last lap's done words answer too
-            eng.wait(k, timeout_s=0)
+            eng.wait(k)  # (steps finish out of order: the last one done does not make the one before it done)
     finally:
         eng.stop()
         stream.synchronize()
@@ -1167,7 +1167,7 @@ def test_engine_walk_across_empty_steps(dev, ring, in_flight):
     n_steps = 0
     try:
         for k in range(bursts):
-            for _ in range(int(gaps[k])):  # empty steps: no tiles, done when published
+            for _ in range(int(gaps[k])):  # empty steps: no tiles, done once the grid has copied them
                 arr[0] = native.Batch(d0, 0, o0, l0, None, out0, st0, 0)
                 assert fn(h, ap, 1, 400, 10**10, ctypes.byref(step)) == native.SCCSUM_OK
                 n_steps += 1
@@ -1179,7 +1179,7 @@ def test_engine_walk_across_empty_steps(dev, ring, in_flight):
         assert step.value == n_steps - 1
         eng.wait(n_steps - 1)
         for k in range(max(0, n_steps - ring), n_steps):
-            eng.wait(k, timeout_s=0)
+            eng.wait(k)  # (steps finish out of order)
     finally:
         eng.stop()
         stream.synchronize()
