@@ -1509,9 +1509,6 @@ struct EngineSrc {
     __device__ bool wait_ready(uint64_t v) {
         if (ready(v)) return true;
         flush();  // never wait holding counts: a step's completion may hang on them
-#ifdef SCCSUM_AB_DEFER_FLUSH
-        resolve();
-#endif
         const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
 #ifdef SCCSUM_AB_TIMELINE
         ++ab[0];
@@ -1652,18 +1649,10 @@ struct EngineSrc {
     // the counters and reports the step done.
     uint64_t pend_step = ~0ull, pend_first = 0, pend_last = 0;
     uint32_t pend = 0, pend_kind = 0;
-#ifdef SCCSUM_AB_DEFER_FLUSH
-    uint32_t fl_x = 0, fl_k = 0, fl_expect = 0, fl_slot = 0;
-    uint64_t fl_step = 0, fl_ntl = 0;
-    bool fl_live = false;
-#endif
 #ifdef SCCSUM_AB_TIMELINE
     unsigned long long pend_t0 = 0, pend_t1 = 0;
 #endif
     __device__ void flush() {
-#ifdef SCCSUM_AB_DEFER_FLUSH
-        resolve();  // at most one count in flight
-#endif
         if (pend == 0) return;
         const uint32_t k = pend;
         pend = 0;
@@ -1701,40 +1690,21 @@ struct EngineSrc {
         const uint32_t slot = static_cast<uint32_t>(pend_step % kEngineCountSlots);
         uint32_t* const c = E.counts + (slot * kGroups + grp) * kHeadStride;
         const uint32_t x = __hip_atomic_fetch_add(c, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifdef SCCSUM_AB_DEFER_FLUSH  // A/B only: the count's result is checked at the wave's next retire
-        fl_x = x;
-        fl_k = k;
-        fl_expect = expect;
-        fl_slot = slot;
-        fl_step = pend_step;
-        fl_ntl = pend_last - pend_first;
-        fl_live = true;
-    }
-    // (lane 0; all lanes call it)
-    __device__ void resolve() {
-        if (!fl_live) return;
-        fl_live = false;
-        if (lane != 0) return;
-        const uint32_t x = fl_x, k = fl_k, expect = fl_expect, slot = fl_slot;
-        const uint64_t step_done = fl_step, ntl = fl_ntl;
-        uint32_t* const c = E.counts + (slot * kGroups + grp) * kHeadStride;
-#else
-        const uint64_t step_done = pend_step, ntl = pend_last - pend_first;
-#endif
         if (x + k != expect) return;
         __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t* const gd = E.gdone + slot * kHeadStride;
+        const uint64_t ntl = pend_last - pend_first;
         const uint32_t groups = ntl < kGroups ? static_cast<uint32_t>(ntl) : kGroups;
         const uint32_t y = __hip_atomic_fetch_add(gd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (y + 1 != groups) return;
         __hip_atomic_store(gd, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the device's copy first (steps that depend on this one read it), then the host's
-        __hip_atomic_store(E.sdone + 8u * slot, step_done + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(E.sdone + 8u * slot, pend_step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // (a ring of done words like the descriptors': the slot's value only
         // rises, and a value past s + 1 also says s is done)
-        __hip_atomic_store(E.ctl + kEcDone + 8u * (step_done & E.ring_mask), step_done + 1, __ATOMIC_RELAXED,
+        __hip_atomic_store(E.ctl + kEcDone + 8u * (pend_step & E.ring_mask), pend_step + 1, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
 #ifdef SCCSUM_AB_TIMELINE
@@ -1744,9 +1714,6 @@ struct EngineSrc {
     }
 #endif
     __device__ void retire(const Ref& r) {
-#ifdef SCCSUM_AB_DEFER_FLUSH
-        resolve();  // the count issued at the last retire (its round trip overlapped a tile)
-#endif
         if (r.step != pend_step) {
             flush();
             pend_step = r.step;
