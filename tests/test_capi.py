@@ -162,3 +162,26 @@ def test_desc_argument_validation_without_device():
     assert lib.sccsum_ipv4_frames_desc(p, p, p, p, None, p + 2, None, 4, 64, None) == native.SCCSUM_EINVAL
     assert lib.sccsum_set_burst_fused(3) == native.SCCSUM_EINVAL
     assert lib.sccsum_set_burst_fused(2) == native.SCCSUM_OK
+
+
+def test_engine_opts_layout_matches_the_header(tmp_path):
+    """native.EngineOpts (ctypes) against sccsum_engine_opts as a C compiler
+    lays it out from include/sccsum.h: size and every field's offset (a field
+    added on one side only would shift the limits the engine reads)."""
+    import ctypes
+    import os
+
+    src = tmp_path / "opts.c"
+    fields = [name for name, _ in native.EngineOpts._fields_]
+    body = "\n".join(f'    printf("{f} %zu\\n", offsetof(sccsum_engine_opts, {f}));' for f in fields)
+    src.write_text("#include <stddef.h>\n#include <stdio.h>\n#include <sccsum.h>\n"
+                   "int main(void) {\n    printf(\"size %zu\\n\", sizeof(sccsum_engine_opts));\n"
+                   f"{body}\n    return 0;\n}}\n")
+    exe = str(tmp_path / "opts")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(repo, "include"), str(src), "-o", exe], check=True)
+    got = dict(line.split() for line in subprocess.run([exe], check=True, capture_output=True,
+                                                        text=True).stdout.splitlines())
+    assert int(got["size"]) == ctypes.sizeof(native.EngineOpts)
+    for f in fields:
+        assert int(got[f]) == getattr(native.EngineOpts, f).offset, f
